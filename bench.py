@@ -1,0 +1,195 @@
+"""Benchmark: env-steps/s of the batched MergingEnv step on MI355X (BASELINE.json config 3/4).
+
+    python bench.py [--gpus N --steps K --warmup W --envs E]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU)
+
+A step = one launch of mg_step_random over this rank's 2^20 envs: Philox actions for both
+players drawn on the device, the full reference step (merging_env.py:138-195), autoreset,
+episode statistics. Envs are sharded across ranks (rank r owns global envs [r E, (r+1) E),
+Philox keyed by the global index), with no collective inside the timed loop; after it, one
+RCCL all-gather collects the per-env episode statistics (timed separately).
+
+Rank 0 prints ONE JSON line: value = env-steps/s over all ranks (max-over-ranks time),
+roofline = algorithmic bytes per launch / mean kernel time (HIP events on the launch stream)
+against the 8 TB/s HBM3E peak, cpu_baseline = the C oracle on the host cores (N = 1 only).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "merging-gym_amd"))
+
+# Algorithmic bytes per env-step of mg_step_random (DESIGN.md "Roofline"):
+#   read  p1 v1 p2 v2 ret1 ret2 (6 x f64) + tf (u32)                      = 52
+#   write the same state 52 + obs 10 x f32 40 + rew 2 x f32 8 + done 1 + coll 1
+#         + actions 2 x i8 2                                            = 104
+# (final_obs / episode-statistics writes happen only for the ~0.5 % of envs that finish
+#  in a step and are not counted.)
+BYTES_PER_ENV_STEP = 156
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+KERNEL_NAME = "step_kernel<1, false>"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--envs", type=int, default=1 << 20, help="envs per GPU")
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-events", action="store_true", help="skip per-launch HIP events")
+    return ap.parse_args()
+
+
+def cpu_baseline(seconds: float):
+    """C oracle (oracle/merge_oracle.c) on the host cores: same workload, bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+
+    import merge_oracle
+
+    co = merge_oracle.COracle(merge_oracle.build_c_oracle())
+    cores = len(os.sched_getaffinity(0))
+    threads = max(1, min(cores, 16))
+    co.set_threads(threads)
+    n = 16384
+    envs = co.new_envs(n)
+    co.reset(envs)
+    ret_sum = np.zeros((n, 2))
+    counts = np.zeros((n, 4), np.uint32)
+    done_steps, chunk, k = 0, 25, 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        done_steps += co.rollout_random(envs, chunk, 1234, k, True, stats=(ret_sum, counts))
+        k += chunk
+    dt = time.perf_counter() - t0
+    return {"value": done_steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{n} envs x {k} autoreset steps with Philox actions (same workload as the "
+                      f"GPU line), {dt:.1f} s on {threads} of {cores} host threads, "
+                      "oracle/merge_oracle.c (OpenMP, reference QP solved per car-step)"}
+
+
+def load_pmc(envs: int):
+    """HBM traffic per launch from the committed rocprofv3 PMC summary (profiles/), if any."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        if int(d.get("envs", -1)) == envs:
+            return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(device)
+
+    from merging_gym import MergeVecEnv
+
+    E = args.envs
+    env = MergeVecEnv(E, device=device, autoreset=True, env_offset=rank * E,
+                      final_observation=True, episode_stats=True)
+    step = lambda k: env.step_random(args.seed, opponent_random=True, step_idx=k)  # noqa: E731
+
+    for k in range(args.warmup):
+        step(k)
+    env.clear_statistics()
+    torch.cuda.synchronize()
+
+    use_events = not args.no_events
+    if use_events:
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        if use_events:
+            ev[k][0].record()
+        step(args.warmup + k)
+        if use_events:
+            ev[k][1].record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = (sum(a.elapsed_time(b) for a, b in ev) / args.steps) if use_events else None
+
+    t = torch.tensor([elapsed, kernel_ms or 0.0], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kernel_ms_max = float(t[0]), float(t[1])
+
+    # episode statistics: one all-gather over RCCL (xGMI), outside the timed loop
+    from merging_gym.distributed import gather_episode_stats, summarize
+
+    torch.cuda.synchronize()
+    g0 = time.perf_counter()
+    if world > 1:
+        ret_sum, counts = gather_episode_stats(env.ret_sum, env.counts)
+    else:
+        ret_sum, counts = env.ret_sum, env.counts
+    torch.cuda.synchronize()
+    gather_ms = (time.perf_counter() - g0) * 1e3
+    episodes = summarize(ret_sum, counts)
+    episodes["allgather_ms"] = gather_ms
+
+    total_env_steps = world * E * args.steps
+    value = total_env_steps / elapsed
+    if rank == 0:
+        achieved = BYTES_PER_ENV_STEP * E / (kernel_ms * 1e-3) / 1e9 if kernel_ms else None
+        pmc = load_pmc(E)
+        line = {
+            "metric": "env-steps/sec at batch=2^20; achieved HBM GB/s vs peak; 1/2/4/8-GPU scaling",
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (deterministic reset, Philox4x32-10 uniform actions for both players)",
+            "config": {"workload": "config 3/4: 1,048,576 envs per MI355X, device-drawn random actions, "
+                                   "autoreset, episode statistics",
+                       "envs_per_gpu": E, "global_envs": world * E,
+                       "parallelism": f"dp{world} (env shards, no per-step collective)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": (achieved / HBM_PEAK_GBPS) if achieved else None,
+                         "traffic": pmc, "kernel": KERNEL_NAME,
+                         "bytes_per_env_step": BYTES_PER_ENV_STEP,
+                         "kernel_ms_mean": kernel_ms, "kernel_ms_mean_max_rank": kernel_ms_max},
+            "episodes": episodes,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,169 @@
+/*
+ * merging_hip.h — C-ABI of libmerging_hip.so, the MI355X (gfx950) batched MergingEnv.
+ *
+ * The reference (YikangZhang1641/merging-gym) is pure Python and has no FFI. Its plugin
+ * boundary is the gym.Env registered as "merging_env-v0" (merging_gym/__init__.py:3-6).
+ * Each entry point below replaces one method of that env for a whole batch of envs held
+ * as a struct-of-arrays in device memory; merging_gym/_native.py binds them with ctypes.
+ *
+ *   mg_step         replaces MergeEnv.step(action1, action2=None)   merging_env.py:138-195
+ *                     (with action_to_acc :134-136 -> helper.mpc_1d helper.py:152-191,
+ *                      observe :118-132, lon2coord :48-58, is_collided :198-206,
+ *                      corners :232-239)
+ *   mg_step_random  the same step, actions drawn on the device (Philox4x32-10); it replaces
+ *                     the callers' env.action_space.sample() / np.random.randint(0, 5)
+ *                     exploration branch (scripts/main.py:110, scripts/hdqn.py:175)
+ *   mg_reset        replaces MergeEnv.reset()                        merging_env.py:208-230
+ *   mg_observe      replaces MergeEnv.observe() and is_collided()    merging_env.py:118-132,
+ *                     :198-206 (no state change)
+ *   mg_abi_version, mg_last_error, mg_params_default: library plumbing (no reference twin).
+ *
+ * Conventions
+ *   - Every pointer inside mg_state / mg_outputs / mg_stats / action arrays is a DEVICE
+ *     pointer owned by the caller. The library never allocates, frees or synchronises.
+ *   - Calls are stream-ordered on `stream` (a hipStream_t, NULL = default stream) and
+ *     return immediately. Return value: 0 on success, otherwise a hipError_t value
+ *     (as int) and mg_last_error() describes it (thread-local). No exception crosses
+ *     the ABI.
+ *   - Arithmetic is IEEE fp64 with no contraction, like the reference's Python floats;
+ *     the fp32 outputs are the fp64 results rounded once.
+ */
+#ifndef MERGING_HIP_H_
+#define MERGING_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MG_ABI_VERSION 1
+#define MG_OBS_DIM 10   /* merging_env.py:75 observation_shape = (10) */
+#define MG_NUM_ACTIONS 5 /* merging_env.py:101-102 action_dict / Discrete(5) */
+#define MG_ACTION_NONE (-1) /* action2=None: the constant-speed "L0" opponent, merging_env.py:152 */
+
+/* Bits of mg_state.tf (one uint32 per env). */
+#define MG_TF_STEPS_MASK 0x0000FFFFu /* steps since reset, saturating at 65535 */
+#define MG_TF_WINNER_SHIFT 16        /* 2 bits: 0 = None, 1 = ego, 2 = opponent (self.winner) */
+#define MG_TF_WINNER_MASK 0x00030000u
+#define MG_TF_DONE 0x00040000u       /* self.done */
+
+/* Flags argument of mg_step / mg_step_random. */
+#define MG_AUTORESET 0x1u /* gym.vector semantics: an env that is done after this step is reset
+                             in place; obs receives the reset observation and
+                             out->final_obs (if non-NULL) the terminal one */
+
+/* Bits of mg_rec64.status (single-env drop-in path). */
+#define MG_ST_DONE 0x1u
+#define MG_ST_COLLISION 0x2u
+#define MG_ST_R1_INT 0x4u /* reward1 is the Python int the reference returns (merging_env.py:168) */
+#define MG_ST_R2_INT 0x8u /* reward2 likewise (merging_env.py:178) */
+#define MG_ST_V1_INT 0x10u /* vel1 is int 0 from max(0, ...) (merging_env.py:149) */
+#define MG_ST_V2_INT 0x20u /* vel2 likewise (merging_env.py:153) */
+
+/* Environment constants, merging_env.py:22-46 and :101. Fill with mg_params_default(). */
+typedef struct mg_params {
+  double R;            /* 30000: arc radius                          merging_env.py:22 */
+  double H;            /* 1000                                        merging_env.py:23 */
+  double W;            /* 300                                         merging_env.py:23 */
+  double dT;           /* 0.2 s per step                              merging_env.py:25 */
+  double r_first;      /* 2.0  RFirst                                 merging_env.py:28 */
+  double r_second;     /* 1.0  RSecond                                merging_env.py:29 */
+  double r_collision;  /* -10  RCollision                             merging_env.py:30 */
+  double vel_penalty;  /* 0.001                                       merging_env.py:31 */
+  double time_penalty; /* 0                                           merging_env.py:32 */
+  double start_point;  /* 50                                          merging_env.py:36 */
+  double end_point;    /* 950 = H - 50                                merging_env.py:37 */
+  double start_vel;    /* 20.0 (reset)                                merging_env.py:216-217 */
+  double vel_ref;      /* 20.0 (reward reference speed)               merging_env.py:158-159 */
+  double prediction_t; /* 3.0 MPC horizon                             merging_env.py:43 */
+  double angle0;       /* atan2(H, R), host-precomputed               merging_env.py:49 */
+  double action_speed[MG_NUM_ACTIONS]; /* {0,10,20,30,40}             merging_env.py:101 */
+  int32_t veh_w;       /* 4  lateral box size                         merging_env.py:40,97 */
+  int32_t veh_h;       /* 8  longitudinal box size                    merging_env.py:40,97 */
+  int32_t timeout_steps; /* 2501: first step with time_stamp > 500    merging_env.py:141-143 */
+  int32_t _pad;
+} mg_params;
+
+/* Per-env state, struct of arrays, n entries each (device pointers). */
+typedef struct mg_state {
+  double* p1;   /* state1['pos']  (ego) */
+  double* v1;   /* state1['vel'] */
+  double* p2;   /* state2['pos']  (opponent) */
+  double* v2;   /* state2['vel'] */
+  double* ret1; /* r1_accumulate */
+  double* ret2; /* r2_accumulate */
+  uint32_t* tf; /* step count | winner | done, see MG_TF_* */
+} mg_state;
+
+/* Packed fp64 record for the single-env (list API) path. */
+typedef struct mg_rec64 {
+  double obs[MG_OBS_DIM];
+  double rew[2];
+  double acc[2];  /* state1['acc'], state2['acc'] */
+  double pos[2];
+  double vel[2];
+  double ret[2];
+  uint32_t tf;
+  uint32_t status; /* MG_ST_* */
+} mg_rec64;
+
+/* Outputs of one step. Any pointer may be NULL to skip that output. */
+typedef struct mg_outputs {
+  float* obs;           /* [n,10] fp32, 16-byte aligned */
+  float* rew;           /* [n,2]  fp32, 8-byte aligned */
+  uint8_t* done;        /* [n] 0/1 */
+  uint8_t* coll;        /* [n] 0/1, info["collision"] */
+  uint64_t* done_mask;  /* [ceil(n/64)] bit j of word w = done of env 64w+j */
+  float* final_obs;     /* [n,10] written only for envs that finished (with MG_AUTORESET) */
+  mg_rec64* rec64;      /* [n] fp64 record (single-env drop-in path) */
+  int32_t* error;       /* [1] OR-ed with 1 (a1) / 2 (a2) when an action is outside the valid set.
+                           Such an env is advanced exactly as far as the reference gets before its
+                           action_dict[...] KeyError (merging_env.py:141-147, :152): the clock
+                           always, the ego too when only a2 is invalid; nothing else is written. */
+} mg_outputs;
+
+/* Completed-episode statistics, updated only when an env finishes (MG_AUTORESET). */
+typedef struct mg_stats {
+  double* ret_sum;   /* [n,2] sum of completed-episode returns (ego, opponent) */
+  uint32_t* counts;  /* [n,4] episodes, collisions, ego-first arrivals, total steps */
+} mg_stats;
+
+int mg_abi_version(void);
+const char* mg_last_error(void);
+
+/* Fills *p with the reference constants (merging_env.py:22-46, :101). Host only. */
+void mg_params_default(mg_params* p);
+
+/* One env step for n envs. a1[n] in {0..4}; a2[n] in {0..4, -1 = None} or a2 == NULL (all None).
+ * Replaces MergeEnv.step (merging_env.py:138-195). */
+int mg_step(const mg_params* params, const mg_state* state, const int8_t* a1, const int8_t* a2,
+            const mg_outputs* out, const mg_stats* stats, int64_t n, uint32_t flags, void* stream);
+
+/* As mg_step, with actions drawn on the device: Philox4x32-10, key = seed, counter =
+ * (env_offset + env index, step_idx) -- a shard of a larger batch passes its first global
+ * env index as env_offset and draws the same actions it would draw unsharded;
+ * a1 = floor(5 u0 / 2^32), a2 = floor(5 u1 / 2^32) when opponent_random != 0, else None.
+ * If a1_out / a2_out are non-NULL the actions used are written there (-1 for None). */
+int mg_step_random(const mg_params* params, const mg_state* state, int8_t* a1_out,
+                   int8_t* a2_out, const mg_outputs* out, const mg_stats* stats, int64_t n,
+                   int64_t env_offset, uint64_t seed, uint64_t step_idx,
+                   int32_t opponent_random, uint32_t flags, void* stream);
+
+/* Resets the envs whose mask byte is non-zero (mask == NULL: all n) and writes their reset
+ * observation to out->obs / out->rec64 when given. Replaces MergeEnv.reset (merging_env.py:208-230). */
+int mg_reset(const mg_params* params, const mg_state* state, const uint8_t* mask,
+             const mg_outputs* out, int64_t n, void* stream);
+
+/* Observation and collision test of the current state, no state change: out->obs /
+ * out->rec64 (obs only) and out->coll. Replaces MergeEnv.observe (merging_env.py:118-132)
+ * and MergeEnv.is_collided (:198-206). */
+int mg_observe(const mg_params* params, const mg_state* state, const mg_outputs* out, int64_t n,
+               void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MERGING_HIP_H_ */

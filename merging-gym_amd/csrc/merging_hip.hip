@@ -1,0 +1,560 @@
+// merging_hip.hip — batched MergingEnv step for MI355X (gfx950, CDNA4).
+//
+// One thread owns one env. The env batch lives in HBM as a struct of arrays
+// (include/merging_hip.h: mg_state); a step streams every array once in and once out,
+// so the kernel is bound by HBM bandwidth, not by arithmetic (no contraction -> no MFMA).
+//
+// Reference being replaced (all paths relative to YikangZhang1641/merging-gym):
+//   MergeEnv.step            merging_gym/envs/merging_env.py:138-195
+//   MergeEnv.action_to_acc   merging_env.py:134-136  -> scripts/helper.py:152-191 mpc_1d
+//   MergeEnv.observe         merging_env.py:118-132  -> lon2coord :48-58
+//   MergeEnv.is_collided     merging_env.py:198-206  -> corners :232-239 (pygame Rect / Vector2,
+//                                                        shapely Polygon.intersects)
+//   MergeEnv.reset           merging_env.py:208-230
+//
+// Numerics: fp64 throughout, IEEE add/mul/div without contraction (the file is compiled
+// with -ffp-contract=off and the pragma below), so positions, speeds, arrival tests and
+// rewards are the same doubles the reference's Python floats hold. sin/cos come from the
+// device math library (<= 1 ulp); every other operation is correctly rounded.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+#include "merging_hip.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int kBlock = 256;  // 4 waves of 64
+constexpr int kObs = MG_OBS_DIM;
+
+// Action codes after host/device decoding: 0..4 valid, -1 None (opponent only), anything
+// else is the reference's KeyError.
+__device__ __forceinline__ bool valid_action(int a) { return a >= 0 && a < MG_NUM_ACTIONS; }
+
+// lon2coord (merging_env.py:48-58): position along the arc -> (x longitudinal, y lateral).
+// The ego rides the arc on +y, the opponent its mirror image on -y.
+__device__ __forceinline__ void lon2coord(const mg_params& P, double lon, bool ego, double& x,
+                                          double& y) {
+  const double angle = P.angle0 - lon / P.R;
+  double s, c;
+  sincos(angle, &s, &c);
+  x = P.R * s;
+  const double d = P.R - P.R * c;
+  const double half_w = P.W * 0.5;  // W/2 = 150.0 exactly
+  y = ego ? (half_w + d) : (half_w - d);
+}
+
+// corners (merging_env.py:232-239) is called as corners(agent, y=x, x=y, 0) (:201-202), so
+// the pygame Rect is centred at (lateral, longitudinal) with w = VEHICLE_W (lateral) and
+// h = VEHICLE_H (longitudinal) (surfaces :97-98). pygame converts a float centre with a C
+// (int) cast, i.e. truncation toward zero, then sets x = cx - w/2, y = cy - h/2. Each corner
+// is ((double)corner - pivot) + pivot in fp64 (Vector2 difference, rotate(0) = identity,
+// 1.0 * v, + pivot), which is not always the integer corner (no Sterbenz near 0).
+struct Box {
+  double l, r, t, b;  // lateral [l, r], longitudinal [t, b]
+};
+
+__device__ __forceinline__ Box vehicle_box(const mg_params& P, double lat, double lon) {
+  const int rx = static_cast<int>(lat) - P.veh_w / 2;
+  const int ry = static_cast<int>(lon) - P.veh_h / 2;
+  Box bx;
+  bx.l = (static_cast<double>(rx) - lat) + lat;
+  bx.r = (static_cast<double>(rx + P.veh_w) - lat) + lat;
+  bx.t = (static_cast<double>(ry) - lon) + lon;
+  bx.b = (static_cast<double>(ry + P.veh_h) - lon) + lon;
+  return bx;
+}
+
+// shapely Polygon.intersects on two axis-aligned rectangles: the closed boxes share a point.
+__device__ __forceinline__ bool boxes_intersect(const Box& a, const Box& b) {
+  return a.l <= b.r && b.l <= a.r && a.t <= b.b && b.t <= a.b;
+}
+
+// observe (merging_env.py:118-132)
+__device__ __forceinline__ void observe(const mg_params& P, double p1, double v1, double p2,
+                                        double v2, double x1, double y1, double x2, double y2,
+                                        double (&o)[kObs]) {
+  o[0] = x2 - x1;
+  o[1] = y2 - y1;
+  o[2] = v2 - v1;
+  o[3] = P.end_point - p1;
+  o[4] = v1;
+  o[5] = x1 - x2;
+  o[6] = y1 - y2;
+  o[7] = v1 - v2;
+  o[8] = P.end_point - p2;
+  o[9] = v2;
+}
+
+__device__ __forceinline__ void reset_obs(const mg_params& P, double (&o)[kObs]) {
+  double x1, y1, x2, y2;
+  lon2coord(P, P.start_point, true, x1, y1);
+  lon2coord(P, P.start_point, false, x2, y2);
+  observe(P, P.start_point, P.start_vel, P.start_point, P.start_vel, x1, y1, x2, y2, o);
+}
+
+// Philox4x32-10 (Salmon et al., SC'11 "Parallel random numbers: as easy as 1, 2, 3").
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+  }
+  return c;
+}
+
+// floor(5 u / 2^32): uniform over {0..4} up to a 5/2^32 bias.
+__device__ __forceinline__ int action_from_u32(uint32_t u) {
+  return static_cast<int>((static_cast<uint64_t>(u) * MG_NUM_ACTIONS) >> 32);
+}
+
+enum ActMode { kActArrays = 0, kActPhilox = 1 };
+
+struct Launch {
+  mg_params P;
+  mg_state S;
+  mg_outputs O;
+  mg_stats St;
+  const int8_t* a1;
+  const int8_t* a2;
+  int8_t* a1_out;
+  int8_t* a2_out;
+  uint64_t seed;
+  uint64_t step_idx;
+  int64_t env_offset;
+  int64_t n;
+  uint32_t flags;
+  int32_t opp_random;
+};
+
+// The step kernel. OUT64 = the single-env path (packed fp64 record, no LDS staging).
+template <int ACT, bool OUT64>
+__global__ __launch_bounds__(kBlock) void step_kernel(const Launch L) {
+  __shared__ __attribute__((aligned(16))) float obs_tile[kBlock * kObs];
+
+  const mg_params& P = L.P;
+  const int tid = threadIdx.x;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kBlock;
+  const int64_t i = base + tid;
+  const bool live = i < L.n;
+
+  bool done = false;
+  bool coll = false;
+  double o[kObs];
+
+  if (live) {
+    // ---- actions ----
+    int a1, a2;
+    if constexpr (ACT == kActPhilox) {
+      const uint64_t gi = static_cast<uint64_t>(L.env_offset + i);  // shard-invariant stream
+      const uint4 u = philox4x32_10(
+          make_uint4(static_cast<uint32_t>(gi), static_cast<uint32_t>(gi >> 32),
+                     static_cast<uint32_t>(L.step_idx), static_cast<uint32_t>(L.step_idx >> 32)),
+          static_cast<uint32_t>(L.seed), static_cast<uint32_t>(L.seed >> 32));
+      a1 = action_from_u32(u.x);
+      a2 = L.opp_random ? action_from_u32(u.y) : MG_ACTION_NONE;
+      if (L.a1_out) L.a1_out[i] = static_cast<int8_t>(a1);
+      if (L.a2_out) L.a2_out[i] = static_cast<int8_t>(a2);
+    } else {
+      a1 = L.a1[i];
+      a2 = L.a2 ? static_cast<int>(L.a2[i]) : MG_ACTION_NONE;
+    }
+
+    // ---- load state (coalesced SoA) ----
+    double p1 = L.S.p1[i], v1 = L.S.v1[i], p2 = L.S.p2[i], v2 = L.S.v2[i];
+    double ret1 = L.S.ret1[i], ret2 = L.S.ret2[i];
+    const uint32_t tf = L.S.tf[i];
+    uint32_t steps = tf & MG_TF_STEPS_MASK;
+    uint32_t winner = (tf & MG_TF_WINNER_MASK) >> MG_TF_WINNER_SHIFT;
+    done = (tf & MG_TF_DONE) != 0;
+
+    // time_stamp += dT; done if time_stamp > 500 (merging_env.py:141-143). The fp64 clock
+    // first exceeds 500 on step 2501; an integer count reproduces that exactly.
+    steps = steps < MG_TF_STEPS_MASK ? steps + 1 : steps;
+    if (static_cast<int32_t>(steps) >= P.timeout_steps) done = true;
+
+    const bool bad1 = !valid_action(a1);
+    const bool bad2 = !(a2 == MG_ACTION_NONE || valid_action(a2));
+    double acc1 = 0.0, acc2 = 0.0;
+    bool v1_int = false, v2_int = false;
+
+    if (!bad1) {
+      // mpc_1d (helper.py:152-191): min u'(D'D + 0.01 I)u s.t. sum(dt u) = vt - v0 (the
+      // only row of the constraint passed to solve_qp, :172-173, :182). D.1 = 0, so
+      // P.1 = 0.01 * 1 and the minimiser is u = (vt - v0) / t * 1; action() = u[0].
+      const double vt1 = P.action_speed[a1];
+      acc1 = (vt1 - v1) / P.prediction_t;
+      const double nv1 = v1 + acc1 * P.dT;  // max(0, v + acc*dT)  :149
+      v1_int = !(nv1 > 0.0);
+      v1 = v1_int ? 0.0 : nv1;
+      p1 = p1 + v1 * P.dT;  // :150
+    }
+    if (!bad1 && !bad2) {
+      // action2 None -> acc 0 (:152): the "L0" constant-speed opponent
+      if (a2 != MG_ACTION_NONE) acc2 = (P.action_speed[a2] - v2) / P.prediction_t;
+      const double nv2 = v2 + acc2 * P.dT;  // :153
+      v2_int = !(nv2 > 0.0);
+      v2 = v2_int ? 0.0 : nv2;
+      p2 = p2 + v2 * P.dT;  // :154
+    }
+
+    if (bad1 || bad2) {
+      // The reference raises KeyError at action_dict[...] after advancing this far.
+      if (L.O.error) atomicOr(L.O.error, (bad1 ? 1 : 0) | (bad2 ? 2 : 0));
+      L.S.tf[i] = steps | (winner << MG_TF_WINNER_SHIFT) | (done ? MG_TF_DONE : 0u);
+      if (!bad1) {
+        L.S.p1[i] = p1;
+        L.S.v1[i] = v1;
+      }
+      done = false;
+#pragma unroll
+      for (int k = 0; k < kObs; ++k) o[k] = 0.0;
+    } else {
+      double x1, y1, x2, y2;
+      lon2coord(P, p1, true, x1, y1);
+      lon2coord(P, p2, false, x2, y2);
+      observe(P, p1, v1, p2, v2, x1, y1, x2, y2, o);
+
+      // rewards (:158-159): -time_penalty - vel_penalty * |v - 20|
+      double r1 = (0.0 - P.time_penalty) - P.vel_penalty * fabs(v1 - P.vel_ref);
+      double r2 = (0.0 - P.time_penalty) - P.vel_penalty * fabs(v2 - P.vel_ref);
+      bool r1_int = false, r2_int = false;
+
+      // arrival / winner state machine (:163-181); ego strict '>', opponent '>='
+      if (p1 > P.end_point) {
+        if (winner == 0) {
+          winner = 1;
+          r1 += P.r_first;
+        } else if (winner == 1) {
+          r1 = 0.0;
+          r1_int = true;
+        } else {
+          r1 += P.r_second;
+          done = true;
+        }
+      }
+      if (p2 >= P.end_point) {
+        if (winner == 0) {
+          winner = 2;
+          r2 += P.r_first;
+        } else if (winner == 2) {
+          r2 = 0.0;
+          r2_int = true;
+        } else {
+          r2 += P.r_second;
+          done = true;
+        }
+      }
+
+      // is_collided (:183-187, :198-206)
+      coll = boxes_intersect(vehicle_box(P, y1, x1), vehicle_box(P, y2, x2));
+      if (coll) {
+        done = true;
+        r1 += P.r_collision;
+        r2 += P.r_collision;
+      }
+      ret1 += r1;  // :191-192
+      ret2 += r2;
+
+      if constexpr (OUT64) {
+        mg_rec64* rec = L.O.rec64 + i;
+#pragma unroll
+        for (int k = 0; k < kObs; ++k) rec->obs[k] = o[k];
+        rec->rew[0] = r1;
+        rec->rew[1] = r2;
+        rec->acc[0] = acc1;
+        rec->acc[1] = acc2;
+        rec->pos[0] = p1;
+        rec->pos[1] = p2;
+        rec->vel[0] = v1;
+        rec->vel[1] = v2;
+        rec->ret[0] = ret1;
+        rec->ret[1] = ret2;
+        rec->tf = steps | (winner << MG_TF_WINNER_SHIFT) | (done ? MG_TF_DONE : 0u);
+        rec->status = (done ? MG_ST_DONE : 0u) | (coll ? MG_ST_COLLISION : 0u) |
+                      (r1_int ? MG_ST_R1_INT : 0u) | (r2_int ? MG_ST_R2_INT : 0u) |
+                      (v1_int ? MG_ST_V1_INT : 0u) | (v2_int ? MG_ST_V2_INT : 0u);
+      } else {
+        if (L.O.rew) {
+          reinterpret_cast<float2*>(L.O.rew)[i] =
+              make_float2(static_cast<float>(r1), static_cast<float>(r2));
+        }
+      }
+      if (L.O.done) L.O.done[i] = done ? 1 : 0;
+      if (L.O.coll) L.O.coll[i] = coll ? 1 : 0;
+
+      if ((L.flags & MG_AUTORESET) && done) {
+        // gym.vector autoreset: record the finished episode, then reset (merging_env.py:208-230)
+        if (L.St.ret_sum) {
+          L.St.ret_sum[2 * i] += ret1;
+          L.St.ret_sum[2 * i + 1] += ret2;
+        }
+        if (L.St.counts) {
+          uint4* c = reinterpret_cast<uint4*>(L.St.counts) + i;
+          uint4 cv = *c;
+          cv.x += 1;
+          cv.y += coll ? 1u : 0u;
+          cv.z += winner == 1 ? 1u : 0u;
+          cv.w += steps;
+          *c = cv;
+        }
+        if (L.O.final_obs) {
+#pragma unroll
+          for (int k = 0; k < kObs; ++k) L.O.final_obs[i * kObs + k] = static_cast<float>(o[k]);
+        }
+        p1 = p2 = P.start_point;
+        v1 = v2 = P.start_vel;
+        ret1 = ret2 = 0.0;
+        steps = 0;
+        winner = 0;
+        reset_obs(P, o);
+      }
+
+      L.S.p1[i] = p1;
+      L.S.v1[i] = v1;
+      L.S.p2[i] = p2;
+      L.S.v2[i] = v2;
+      L.S.ret1[i] = ret1;
+      L.S.ret2[i] = ret2;
+      const bool still_done = done && !(L.flags & MG_AUTORESET);
+      L.S.tf[i] = steps | (winner << MG_TF_WINNER_SHIFT) | (still_done ? MG_TF_DONE : 0u);
+    }
+  }
+
+  if (L.O.done_mask) {
+    const uint64_t m = __ballot(live && done);
+    if ((tid & 63) == 0 && base + tid < L.n) L.O.done_mask[(base + tid) >> 6] = m;
+  }
+
+  if constexpr (!OUT64) {
+    if (L.O.obs) {
+      // Stage the block's [256,10] fp32 tile in LDS, then write it out as contiguous 16-B
+      // stores: a wave's 64 rows of 40 B become 160 full dwordx4 lanes instead of 640
+      // scattered dwords.
+      float2* t2 = reinterpret_cast<float2*>(obs_tile + tid * kObs);
+#pragma unroll
+      for (int k = 0; k < kObs / 2; ++k)
+        t2[k] = make_float2(static_cast<float>(o[2 * k]), static_cast<float>(o[2 * k + 1]));
+      __syncthreads();
+      const int64_t rem = L.n - base;
+      const int nrows = rem < kBlock ? static_cast<int>(rem) : kBlock;
+      const int nfl = nrows * kObs;
+      const int n4 = nfl >> 2;
+      float4* dst4 = reinterpret_cast<float4*>(L.O.obs + base * kObs);
+      const float4* src4 = reinterpret_cast<const float4*>(obs_tile);
+      for (int j = tid; j < n4; j += kBlock) dst4[j] = src4[j];
+      const int tail = nfl - (n4 << 2);  // 0 or 2
+      if (tid < tail) L.O.obs[base * kObs + (n4 << 2) + tid] = obs_tile[(n4 << 2) + tid];
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void reset_kernel(const mg_params P, const mg_state S,
+                                                       const uint8_t* mask, const mg_outputs O,
+                                                       int64_t n) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= n) return;
+  if (mask && !mask[i]) return;
+  S.p1[i] = P.start_point;
+  S.v1[i] = P.start_vel;
+  S.p2[i] = P.start_point;
+  S.v2[i] = P.start_vel;
+  S.ret1[i] = 0.0;
+  S.ret2[i] = 0.0;
+  S.tf[i] = 0u;
+  if (O.obs || O.rec64) {
+    double o[kObs];
+    reset_obs(P, o);
+    if (O.obs) {
+#pragma unroll
+      for (int k = 0; k < kObs; ++k) O.obs[i * kObs + k] = static_cast<float>(o[k]);
+    }
+    if (O.rec64) {
+      mg_rec64* rec = O.rec64 + i;
+#pragma unroll
+      for (int k = 0; k < kObs; ++k) rec->obs[k] = o[k];
+      rec->rew[0] = rec->rew[1] = 0.0;
+      rec->acc[0] = rec->acc[1] = 0.0;
+      rec->pos[0] = rec->pos[1] = P.start_point;
+      rec->vel[0] = rec->vel[1] = P.start_vel;
+      rec->ret[0] = rec->ret[1] = 0.0;
+      rec->tf = 0u;
+      rec->status = 0u;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void observe_kernel(const mg_params P, const mg_state S,
+                                                         const mg_outputs O, int64_t n) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const double p1 = S.p1[i], v1 = S.v1[i], p2 = S.p2[i], v2 = S.v2[i];
+  double x1, y1, x2, y2, o[kObs];
+  lon2coord(P, p1, true, x1, y1);
+  lon2coord(P, p2, false, x2, y2);
+  observe(P, p1, v1, p2, v2, x1, y1, x2, y2, o);
+  if (O.obs) {
+#pragma unroll
+    for (int k = 0; k < kObs; ++k) O.obs[i * kObs + k] = static_cast<float>(o[k]);
+  }
+  if (O.rec64) {
+#pragma unroll
+    for (int k = 0; k < kObs; ++k) O.rec64[i].obs[k] = o[k];
+  }
+  if (O.coll) O.coll[i] = boxes_intersect(vehicle_box(P, y1, x1), vehicle_box(P, y2, x2)) ? 1 : 0;
+}
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, const char* what) {
+  std::snprintf(g_err, sizeof(g_err), fmt, what);
+  return code ? code : static_cast<int>(hipErrorInvalidValue);
+}
+
+int check_state(const mg_state* s) {
+  if (!s || !s->p1 || !s->v1 || !s->p2 || !s->v2 || !s->ret1 || !s->ret2 || !s->tf)
+    return fail(hipErrorInvalidValue, "%s", "mg_state has a NULL array");
+  return 0;
+}
+
+int check_common(const mg_params* p, const mg_state* s, const mg_outputs* o, int64_t n) {
+  if (!p) return fail(hipErrorInvalidValue, "%s", "params is NULL");
+  if (n < 0) return fail(hipErrorInvalidValue, "%s", "n < 0");
+  if (n > (static_cast<int64_t>(0x7fffffff) * kBlock))
+    return fail(hipErrorInvalidValue, "%s", "n exceeds the grid limit");
+  if (int e = check_state(s)) return e;
+  if (!o) return fail(hipErrorInvalidValue, "%s", "outputs is NULL (pass a zeroed mg_outputs)");
+  if (o->obs && (reinterpret_cast<uintptr_t>(o->obs) & 15))
+    return fail(hipErrorInvalidValue, "%s", "obs must be 16-byte aligned");
+  if (o->rew && (reinterpret_cast<uintptr_t>(o->rew) & 7))
+    return fail(hipErrorInvalidValue, "%s", "rew must be 8-byte aligned");
+  return 0;
+}
+
+int finish_launch(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    std::snprintf(g_err, sizeof(g_err), "%s: %s", what, hipGetErrorString(e));
+    return static_cast<int>(e);
+  }
+  g_err[0] = '\0';
+  return 0;
+}
+
+template <int ACT>
+int launch_step(const Launch& L, hipStream_t stream, const char* what) {
+  const unsigned blocks = static_cast<unsigned>((L.n + kBlock - 1) / kBlock);
+  if (L.O.rec64)
+    hipLaunchKernelGGL((step_kernel<ACT, true>), dim3(blocks), dim3(kBlock), 0, stream, L);
+  else
+    hipLaunchKernelGGL((step_kernel<ACT, false>), dim3(blocks), dim3(kBlock), 0, stream, L);
+  return finish_launch(what);
+}
+
+}  // namespace
+
+extern "C" {
+
+int mg_abi_version(void) { return MG_ABI_VERSION; }
+
+const char* mg_last_error(void) { return g_err; }
+
+void mg_params_default(mg_params* p) {
+  if (!p) return;
+  std::memset(p, 0, sizeof(*p));
+  p->R = 30000.0;
+  p->H = 1000.0;
+  p->W = 300.0;
+  p->dT = 0.2;
+  p->r_first = 2.0;
+  p->r_second = 1.0;
+  p->r_collision = -10.0;
+  p->vel_penalty = 0.001;
+  p->time_penalty = 0.0;
+  p->start_point = 50.0;
+  p->end_point = 950.0;
+  p->start_vel = 20.0;
+  p->vel_ref = 20.0;
+  p->prediction_t = 3.0;
+  volatile double h = 1000.0, r = 30000.0;  // libm at run time, as np.arctan2 does
+  p->angle0 = std::atan2(h, r);                 // merging_env.py:49
+  for (int k = 0; k < MG_NUM_ACTIONS; ++k) p->action_speed[k] = 10.0 * k;
+  p->veh_w = 4;
+  p->veh_h = 8;
+  p->timeout_steps = 2501;
+}
+
+int mg_step(const mg_params* params, const mg_state* state, const int8_t* a1, const int8_t* a2,
+            const mg_outputs* out, const mg_stats* stats, int64_t n, uint32_t flags,
+            void* stream) {
+  if (int e = check_common(params, state, out, n)) return e;
+  if (n == 0) return 0;
+  if (!a1) return fail(hipErrorInvalidValue, "%s", "a1 is NULL");
+  Launch L{};
+  L.P = *params;
+  L.S = *state;
+  L.O = *out;
+  if (stats) L.St = *stats;
+  L.a1 = a1;
+  L.a2 = a2;
+  L.n = n;
+  L.flags = flags;
+  return launch_step<kActArrays>(L, static_cast<hipStream_t>(stream), "mg_step");
+}
+
+int mg_step_random(const mg_params* params, const mg_state* state, int8_t* a1_out,
+                   int8_t* a2_out, const mg_outputs* out, const mg_stats* stats, int64_t n,
+                   int64_t env_offset, uint64_t seed, uint64_t step_idx, int32_t opponent_random, uint32_t flags,
+                   void* stream) {
+  if (int e = check_common(params, state, out, n)) return e;
+  if (n == 0) return 0;
+  Launch L{};
+  L.P = *params;
+  L.S = *state;
+  L.O = *out;
+  if (stats) L.St = *stats;
+  L.a1_out = a1_out;
+  L.a2_out = a2_out;
+  L.seed = seed;
+  L.step_idx = step_idx;
+  L.env_offset = env_offset;
+  L.opp_random = opponent_random;
+  L.n = n;
+  L.flags = flags;
+  return launch_step<kActPhilox>(L, static_cast<hipStream_t>(stream), "mg_step_random");
+}
+
+int mg_reset(const mg_params* params, const mg_state* state, const uint8_t* mask,
+             const mg_outputs* out, int64_t n, void* stream) {
+  if (!params) return fail(hipErrorInvalidValue, "%s", "params is NULL");
+  if (n < 0) return fail(hipErrorInvalidValue, "%s", "n < 0");
+  if (int e = check_state(state)) return e;
+  if (n == 0) return 0;
+  mg_outputs o{};
+  if (out) o = *out;
+  const unsigned blocks = static_cast<unsigned>((n + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(reset_kernel, dim3(blocks), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), *params, *state, mask, o, n);
+  return finish_launch("mg_reset");
+}
+
+int mg_observe(const mg_params* params, const mg_state* state, const mg_outputs* out, int64_t n,
+               void* stream) {
+  if (int e = check_common(params, state, out, n)) return e;
+  if (n == 0) return 0;
+  const unsigned blocks = static_cast<unsigned>((n + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(observe_kernel, dim3(blocks), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), *params, *state, *out, n);
+  return finish_launch("mg_observe");
+}
+
+}  // extern "C"

@@ -1,0 +1,110 @@
+"""ctypes binding of libmerging_hip.so (C-ABI declared in include/merging_hip.h).
+
+The library is built in-tree by __graft_entry__.build() / `python -m merging_gym.build`
+(hipcc --offload-arch=gfx950). There is no CPU fallback: if the library is missing or the
+ABI version differs, importing this module raises, and every env constructor fails loudly.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_NAME = "libmerging_hip.so"
+LIB_PATH = os.environ.get("MERGING_HIP_LIB", os.path.join(_HERE, LIB_NAME))
+ABI_VERSION = 1
+
+OBS_DIM = 10
+NUM_ACTIONS = 5
+ACTION_NONE = -1
+ACTION_INVALID = 127  # host marker for a value the reference's action_dict would reject
+
+TF_STEPS_MASK = 0x0000FFFF
+TF_WINNER_SHIFT = 16
+TF_WINNER_MASK = 0x00030000
+TF_DONE = 0x00040000
+
+AUTORESET = 0x1
+
+ST_DONE, ST_COLLISION, ST_R1_INT, ST_R2_INT, ST_V1_INT, ST_V2_INT = 1, 2, 4, 8, 16, 32
+
+_c = ctypes
+_P = ctypes.c_void_p
+
+
+class Params(_c.Structure):
+    _fields_ = [(n, _c.c_double) for n in (
+        "R", "H", "W", "dT", "r_first", "r_second", "r_collision", "vel_penalty",
+        "time_penalty", "start_point", "end_point", "start_vel", "vel_ref", "prediction_t",
+        "angle0")] + [("action_speed", _c.c_double * NUM_ACTIONS), ("veh_w", _c.c_int32),
+                      ("veh_h", _c.c_int32), ("timeout_steps", _c.c_int32), ("_pad", _c.c_int32)]
+
+
+class State(_c.Structure):
+    _fields_ = [(n, _P) for n in ("p1", "v1", "p2", "v2", "ret1", "ret2", "tf")]
+
+
+class Outputs(_c.Structure):
+    _fields_ = [(n, _P) for n in ("obs", "rew", "done", "coll", "done_mask", "final_obs",
+                                  "rec64", "error")]
+
+
+class Stats(_c.Structure):
+    _fields_ = [("ret_sum", _P), ("counts", _P)]
+
+
+# numpy view of struct mg_rec64 (168 bytes)
+REC64_DTYPE = np.dtype([("obs", np.float64, (OBS_DIM,)), ("rew", np.float64, (2,)),
+                        ("acc", np.float64, (2,)), ("pos", np.float64, (2,)),
+                        ("vel", np.float64, (2,)), ("ret", np.float64, (2,)),
+                        ("tf", np.uint32), ("status", np.uint32)])
+assert REC64_DTYPE.itemsize == 168
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} not found. Build the HIP library first: "
+            "python -c 'import __graft_entry__ as g; g.build()' (hipcc --offload-arch=gfx950)")
+    import torch  # noqa: F401  -- load torch's libamdhip64 first so the library binds to it
+
+    lib = _c.CDLL(LIB_PATH)
+    lib.mg_abi_version.restype = _c.c_int
+    lib.mg_last_error.restype = _c.c_char_p
+    lib.mg_params_default.argtypes = [_c.POINTER(Params)]
+    lib.mg_params_default.restype = None
+    PP, SP, OP, STP = (_c.POINTER(Params), _c.POINTER(State), _c.POINTER(Outputs),
+                       _c.POINTER(Stats))
+    lib.mg_step.argtypes = [PP, SP, _P, _P, OP, STP, _c.c_int64, _c.c_uint32, _P]
+    lib.mg_step_random.argtypes = [PP, SP, _P, _P, OP, STP, _c.c_int64, _c.c_int64,
+                                   _c.c_uint64, _c.c_uint64, _c.c_int32, _c.c_uint32, _P]
+    lib.mg_reset.argtypes = [PP, SP, _P, OP, _c.c_int64, _P]
+    lib.mg_observe.argtypes = [PP, SP, OP, _c.c_int64, _P]
+    for f in (lib.mg_step, lib.mg_step_random, lib.mg_reset, lib.mg_observe):
+        f.restype = _c.c_int
+    v = lib.mg_abi_version()
+    if v != ABI_VERSION:
+        raise ImportError(f"{LIB_PATH}: ABI version {v}, expected {ABI_VERSION} (stale build?)")
+    return lib
+
+
+lib = _load()
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib.mg_last_error().decode(errors="replace")
+        raise NativeError(f"{what} failed (hipError {rc}): {msg}")
+
+
+def default_params() -> Params:
+    p = Params()
+    lib.mg_params_default(_c.byref(p))
+    return p

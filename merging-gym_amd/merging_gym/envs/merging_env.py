@@ -1,0 +1,282 @@
+"""MergeEnv: the drop-in single env behind gym id "merging_env-v0".
+
+Same surface as the reference's MergeEnv (merging_gym/envs/merging_env.py:72-399):
+`reset() -> list[10]`, `step(action1, action2=None) -> (list[10], [r1, r2], done,
+{"collision": bool})`, the attributes its callers read (`winner`, `done`, `time_stamp`,
+`state1`, `state2`, `r1_accumulate`, `r2_accumulate`, `action_dict`, `action_space`,
+`observation_space`, `show_reward()`) and the reference's Python value types (an int 0
+reward after the winner's arrival, int 900 gaps straight after reset, ...), so
+scripts/hdqn.py, scripts/main.py and scripts/human_player.py's list arithmetic
+(`state[5:] + state[:5]`, `[goal] + state`) keeps working.
+
+The step itself runs on the GPU: a batch of one env in the same kernel as MergeVecEnv,
+writing a packed fp64 record (mg_rec64) that is copied back once per call. The pygame UI
+methods (render / plot / intro / prepare / feedback / finish) are out of scope for this
+build and raise NotImplementedError.
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from .. import spaces
+
+# merging_env.py:22-46 (the constants callers may import from the module)
+R = 30000
+H, W = 1000, 300
+WINDOW_H, WINDOW_W = 1000, 300
+dT = 0.2
+RFirst = 2.0
+RSecond = 1.0
+RCollision = -10
+vel_penalty = 0.001
+time_penalty = 0
+START_POINT = 50
+END_POINT = H - 50
+VEHICLE_W, VEHICLE_H = 4, 8
+prediction_t = 3.0
+scale = 5.0
+
+try:  # pragma: no cover - gym is not installed in this image
+    import gym as _gym
+
+    _EnvBase = _gym.Env
+except Exception:  # noqa: BLE001
+    class _EnvBase:  # minimal gym.Env stand-in: the attributes callers touch
+        metadata = {"render.modes": []}
+
+        @property
+        def unwrapped(self):
+            return self
+
+        def close(self):
+            pass
+
+        def seed(self, seed=None):
+            return [seed]
+
+
+class MergeEnv(_EnvBase):
+    """GPU-backed single MergeEnv with the reference's list API."""
+
+    def __init__(self, device=None):
+        super().__init__()
+        import torch
+
+        from .. import _native
+
+        if not torch.cuda.is_available():
+            raise RuntimeError("MergeEnv runs its step on a ROCm GPU (torch.cuda.is_available() is "
+                               "False); there is no CPU fallback")
+        self._torch, self._nat = torch, _native
+        self.device = torch.device(device if device is not None else "cuda")
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+
+        self.observation_shape = (10)
+        self.observation_space = spaces.observation_space()
+        self.action_dict = {0: 0, 1: 10, 2: 20, 3: 30, 4: 40}
+        self.action_space = spaces.action_space(len(self.action_dict.items()))
+        self.action1 = 1
+        self.action2 = 1
+
+        self.params = _native.default_params()
+        self.params.angle0 = float(np.arctan2(H, R))
+        dev = self.device
+        self._dstate = torch.zeros(7, dtype=torch.float64, device=dev)  # p1 v1 p2 v2 ret1 ret2 tf
+        self._rec_dev = torch.zeros(_native.REC64_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+        self._rec_host = torch.zeros(_native.REC64_DTYPE.itemsize, dtype=torch.uint8).pin_memory()
+        self._a_dev = torch.zeros(2, dtype=torch.int8, device=dev)
+        self._a_host = torch.zeros(2, dtype=torch.int8).pin_memory()
+        self._coll_dev = torch.zeros(8, dtype=torch.uint8, device=dev)
+        self._err = torch.zeros(1, dtype=torch.int32, device=dev)
+        base = self._dstate.data_ptr()
+        self._state = _native.State(*(ctypes.c_void_p(base + 8 * k) for k in range(7)))
+        self._out = _native.Outputs(None, None, None, None, None, None,
+                                    ctypes.c_void_p(self._rec_dev.data_ptr()),
+                                    ctypes.c_void_p(self._err.data_ptr()))
+        self._stats = _native.Stats(None, None)
+        self._a1 = ctypes.c_void_p(self._a_dev.data_ptr())
+        self._a2 = ctypes.c_void_p(self._a_dev.data_ptr() + 1)
+
+        self._time, self._steps, self._dirty = 0, 0, False
+        self.reset()
+
+    # ------------------------------------------------------------------ plumbing
+    def _stream(self):
+        return self._torch.cuda.current_stream(self.device)
+
+    def _fetch(self):
+        stream = self._stream()
+        self._rec_host.copy_(self._rec_dev, non_blocking=True)
+        stream.synchronize()
+        return self._rec_host.numpy().view(self._nat.REC64_DTYPE)[0]
+
+    def _push(self):
+        """Write the host-side attributes (after a caller assigned state1, winner, ...) to the
+        device state, like assigning the reference's attributes between steps."""
+        nat = self._nat
+        tf = (self._steps & nat.TF_STEPS_MASK) | ((0 if self._winner is None else int(self._winner))
+                                                  << nat.TF_WINNER_SHIFT)
+        tf |= nat.TF_DONE if self._done else 0
+        host = np.array([self._s1["pos"], self._s1["vel"], self._s2["pos"], self._s2["vel"],
+                         self._r1acc, self._r2acc, 0.0], dtype=np.float64)
+        host[6:7].view(np.uint32)[0] = tf
+        self._dstate.copy_(self._torch.from_numpy(host))
+        self._dirty = False
+
+    def _apply(self, rec):
+        st = int(rec["status"])
+        tf = int(rec["tf"])
+        nat = self._nat
+        w = (tf & nat.TF_WINNER_MASK) >> nat.TF_WINNER_SHIFT
+        self._winner = None if w == 0 else w
+        self._done = bool(tf & nat.TF_DONE)
+        self._steps = tf & nat.TF_STEPS_MASK
+        obs = [float(x) for x in rec["obs"]]
+        v1 = 0 if st & nat.ST_V1_INT else float(rec["vel"][0])
+        v2 = 0 if st & nat.ST_V2_INT else float(rec["vel"][1])
+        if st & nat.ST_V1_INT:
+            obs[4] = 0
+        if st & nat.ST_V2_INT:
+            obs[9] = 0
+        self._s1 = {"pos": float(rec["pos"][0]), "vel": v1, "acc": float(rec["acc"][0])}
+        self._s2 = {"pos": float(rec["pos"][1]), "vel": v2,
+                    "acc": 0 if self.action2 is None else float(rec["acc"][1])}
+        r1 = int(rec["rew"][0]) if st & nat.ST_R1_INT else float(rec["rew"][0])
+        r2 = int(rec["rew"][1]) if st & nat.ST_R2_INT else float(rec["rew"][1])
+        # the device sums r_accumulate in fp64 in the reference's order; an int history stays int
+        self._r1acc = _keep_int(self._r1acc, r1, float(rec["ret"][0]))
+        self._r2acc = _keep_int(self._r2acc, r2, float(rec["ret"][1]))
+        return obs, [r1, r2], bool(st & nat.ST_DONE), {"collision": bool(st & nat.ST_COLLISION)}
+
+    # ------------------------------------------------------------------ reference attributes
+    def _attr(name):  # noqa: N805 - property factory
+        def get(self):
+            return getattr(self, name)
+
+        def put(self, v):
+            setattr(self, name, v)
+            self._dirty = True
+
+        return property(get, put)
+
+    state1 = _attr("_s1")
+    state2 = _attr("_s2")
+    winner = _attr("_winner")
+    done = _attr("_done")
+    r1_accumulate = _attr("_r1acc")
+    r2_accumulate = _attr("_r2acc")
+    del _attr
+
+    @property
+    def time_stamp(self):
+        return self._time
+
+    @time_stamp.setter
+    def time_stamp(self, t):
+        # the device counts steps; the fp64 clock exceeds 500 exactly from step 2501
+        self._time = t
+        self._steps = int(round(float(t) / dT))
+        self._dirty = True
+
+    # ------------------------------------------------------------------ reference API
+    def show_reward(self):
+        return RFirst, RSecond, RCollision, vel_penalty
+
+    def reset(self):
+        """merging_env.py:208-230 -> mg_reset on the GPU."""
+        nat = self._nat
+        nat.check(nat.lib.mg_reset(ctypes.byref(self.params), ctypes.byref(self._state), None,
+                                   ctypes.byref(self._out), 1,
+                                   ctypes.c_void_p(self._stream().cuda_stream)), "mg_reset")
+        rec = self._fetch()
+        self._done, self._winner, self._time, self._steps = False, None, 0, 0
+        self._s1 = {"pos": START_POINT, "vel": 20.0, "acc": 0.0}
+        self._s2 = {"pos": START_POINT, "vel": 20.0, "acc": 0.0}
+        self._r1acc = self._r2acc = 0
+        self._dirty = False
+        obs = [float(x) for x in rec["obs"]]
+        obs[3], obs[8] = int(obs[3]), int(obs[8])  # END_POINT - START_POINT: ints, as the reference
+        return obs
+
+    def step(self, action1, action2=None):
+        """merging_env.py:138-195 -> mg_step on the GPU (one env)."""
+        nat = self._nat
+        if self._dirty:
+            self._push()
+        self.action1, self.action2 = action1, action2
+        c1 = _ACTION_CODE.get(action1, nat.ACTION_INVALID)
+        c2 = nat.ACTION_NONE if action2 is None else _ACTION_CODE.get(action2, nat.ACTION_INVALID)
+        self._time += dT
+        self._a_host[0], self._a_host[1] = c1, c2
+        self._a_dev.copy_(self._a_host, non_blocking=True)
+        nat.check(nat.lib.mg_step(ctypes.byref(self.params), ctypes.byref(self._state), self._a1,
+                                  self._a2, ctypes.byref(self._out), ctypes.byref(self._stats), 1, 0,
+                                  ctypes.c_void_p(self._stream().cuda_stream)), "mg_step")
+        if c1 == nat.ACTION_INVALID or c2 == nat.ACTION_INVALID:
+            self._sync_after_error()
+            raise KeyError(action1 if c1 == nat.ACTION_INVALID else action2)
+        obs, rewards, done, info = self._apply(self._fetch())
+        return obs, rewards, done, info
+
+    def _sync_after_error(self):
+        # the kernel advanced the clock (and the ego when only action2 was bad) as the
+        # reference does before its KeyError; refresh the host mirror from the device
+        self._err.zero_()
+        st = self._dstate.cpu().numpy()
+        tf = int(st[6:7].view(np.uint32)[0])
+        self._done = bool(tf & self._nat.TF_DONE)
+        self._steps = tf & self._nat.TF_STEPS_MASK
+        self._s1 = dict(self._s1, pos=float(st[0]), vel=float(st[1]))
+
+    def observe(self):
+        """merging_env.py:118-132: observation of the current state (GPU, no state change)."""
+        nat = self._nat
+        if self._dirty:
+            self._push()
+        out = nat.Outputs(None, None, None, ctypes.c_void_p(self._coll_dev.data_ptr()), None, None,
+                          self._out.rec64, None)
+        nat.check(nat.lib.mg_observe(ctypes.byref(self.params), ctypes.byref(self._state),
+                                     ctypes.byref(out), 1,
+                                     ctypes.c_void_p(self._stream().cuda_stream)), "mg_observe")
+        return [float(x) for x in self._fetch()["obs"]]
+
+    def is_collided(self):
+        """merging_env.py:198-206 (GPU, no state change)."""
+        self.observe()
+        return bool(self._coll_dev[0].item())
+
+    # ------------------------------------------------------------------ UI: out of scope
+    def _ui(self, *a, **k):
+        raise NotImplementedError("pygame rendering (merging_env.py:241-395) is out of scope for the "
+                                  "MI355X build; see DESIGN.md")
+
+    render = plot = intro = prepare = feedback = finish = _ui
+
+    def close(self):
+        pass
+
+
+_ACTION_CODE = {0: 0, 1: 1, 2: 2, 3: 3, 4: 4}  # keys of action_dict (merging_env.py:101)
+
+
+def _keep_int(prev, r, device_sum):
+    if isinstance(prev, int) and isinstance(r, int):
+        return prev + r
+    return device_sum
+
+
+class MergeEnvExtend(_EnvBase):
+    """merging_env.py:404-410: the reference's print-only placeholder env."""
+
+    def __init__(self):
+        print("MergeEnvExtend Environment initialized")
+
+    def step(self):
+        print("MergeEnvExtend Step successful!")
+
+    def reset(self):
+        print("MergeEnvExtend Environment reset")

@@ -1,0 +1,209 @@
+"""MergeVecEnv: N merging envs stepped together by one HIP kernel on an MI355X.
+
+Batched form of MergeEnv (merging_gym/envs/merging_env.py:72-399 in the reference). State
+lives on the GPU as a struct of arrays (fp64 positions / speeds / returns + one packed
+uint32 of step count, winner and done); a step is one launch of `mg_step` (or
+`mg_step_random`, actions drawn on the device) from libmerging_hip.so. Nothing is computed
+on the host and there is no CPU fallback.
+
+API (gym 0.20 VectorEnv conventions, two players like the reference's step(a1, a2=None)):
+
+    env = MergeVecEnv(num_envs, device="cuda:0")
+    obs = env.reset()                                # [N,10] float32 tensor
+    obs, rew, done, info = env.step(a1, a2=None)     # rew [N,2] f32, done [N] bool
+    info["collision"]                                # [N] bool
+    info["final_observation"]                        # [N,10] f32, valid where done (autoreset)
+
+Outputs are views of buffers the env owns and overwrites on the next call (clone them to
+keep them). With autoreset (the default) an env that finishes is reset inside the same
+kernel: `obs` holds its reset observation and `info["final_observation"]` the terminal one.
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from .. import spaces
+
+_OBS_DIM = 10
+
+
+class MergeVecEnv:
+    metadata = {"render.modes": []}
+
+    def __init__(self, num_envs: int, device=None, autoreset: bool = True, env_offset: int = 0,
+                 final_observation: bool = True, episode_stats: bool = True,
+                 done_mask: bool = False):
+        import torch
+
+        from .. import _native
+
+        if not torch.cuda.is_available():
+            raise RuntimeError("MergeVecEnv needs a ROCm GPU (torch.cuda.is_available() is False); "
+                               "there is no CPU fallback")
+        if num_envs < 1:
+            raise ValueError("num_envs must be >= 1")
+        self._torch = torch
+        self._nat = _native
+        self.num_envs = int(num_envs)
+        self.device = torch.device(device if device is not None else "cuda", )
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self.autoreset = bool(autoreset)
+        self.env_offset = int(env_offset)
+        self.params = _native.default_params()
+        self.params.angle0 = float(np.arctan2(1000, 30000))  # merging_env.py:49
+
+        n, dev = self.num_envs, self.device
+        f64 = dict(dtype=torch.float64, device=dev)
+        self.p1, self.v1 = torch.empty(n, **f64), torch.empty(n, **f64)
+        self.p2, self.v2 = torch.empty(n, **f64), torch.empty(n, **f64)
+        self.ret1, self.ret2 = torch.empty(n, **f64), torch.empty(n, **f64)
+        self.tf = torch.empty(n, dtype=torch.int32, device=dev)
+        self.obs = torch.empty((n, _OBS_DIM), dtype=torch.float32, device=dev)
+        self.rew = torch.empty((n, 2), dtype=torch.float32, device=dev)
+        self.done = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self.coll = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self.final_obs = (torch.full((n, _OBS_DIM), float("nan"), dtype=torch.float32, device=dev)
+                          if final_observation else None)
+        self.done_mask = (torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
+                          if done_mask else None)
+        self.error = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.ret_sum = torch.zeros((n, 2), dtype=torch.float64, device=dev) if episode_stats else None
+        self.counts = torch.zeros((n, 4), dtype=torch.int32, device=dev) if episode_stats else None
+        self.a1_buf = torch.empty(n, dtype=torch.int8, device=dev)
+        self.a2_buf = torch.empty(n, dtype=torch.int8, device=dev)
+
+        ptr = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        self._state = _native.State(*(ptr(t) for t in (self.p1, self.v1, self.p2, self.v2,
+                                                        self.ret1, self.ret2, self.tf)))
+        self._out = _native.Outputs(ptr(self.obs), ptr(self.rew), ptr(self.done), ptr(self.coll),
+                                    ptr(self.done_mask), ptr(self.final_obs), None, ptr(self.error))
+        self._stats = _native.Stats(ptr(self.ret_sum), ptr(self.counts))
+        self._flags = _native.AUTORESET if self.autoreset else 0
+        self._step_idx = 0
+
+        self.single_observation_space = spaces.observation_space()
+        self.single_action_space = spaces.action_space()
+        self.observation_space = spaces.batched_observation_space(n)
+        self.action_space = self.single_action_space
+        self.reset()
+
+    # ------------------------------------------------------------------ helpers
+    def _stream(self):
+        return ctypes.c_void_p(self._torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _actions(self, a, buf, allow_none: bool):
+        torch = self._torch
+        if a is None:
+            if not allow_none:
+                raise KeyError(None)
+            return None
+        if isinstance(a, torch.Tensor):
+            t = a
+        else:
+            t = torch.as_tensor(np.asarray(a))
+        if t.shape != (self.num_envs,):
+            raise ValueError(f"actions must have shape ({self.num_envs},), got {tuple(t.shape)}")
+        if t.dtype == torch.int8 and t.device == self.device and t.is_contiguous():
+            return t
+        if t.is_floating_point() or t.dtype == torch.bool:
+            t = t.to(torch.int64)
+        # values outside int8 must stay invalid, not wrap into {0..4}
+        t = t.to(self.device, non_blocking=True)
+        if t.dtype != torch.int8:
+            t = torch.where((t >= -1) & (t < 5), t, torch.full_like(t, self._nat.ACTION_INVALID))
+        buf.copy_(t)
+        return buf
+
+    def _outputs(self):
+        info = {"collision": self.coll.view(self._torch.bool)}
+        if self.final_obs is not None and self.autoreset:
+            info["final_observation"] = self.final_obs
+        return self.obs, self.rew, self.done.view(self._torch.bool), info
+
+    # ------------------------------------------------------------------ gym API
+    def reset(self, mask=None):
+        """Reset all envs (mask None) or those where mask is true; returns obs [N,10] f32.
+        merging_env.py:208-230."""
+        m = None
+        if mask is not None:
+            mt = self._torch.as_tensor(mask, device=self.device).to(self._torch.uint8).contiguous()
+            self._mask_keepalive = mt
+            m = ctypes.c_void_p(mt.data_ptr())
+        out = self._nat.Outputs(self._out.obs, None, None, None, None, None, None, None)
+        self._nat.check(self._nat.lib.mg_reset(ctypes.byref(self.params), ctypes.byref(self._state),
+                                               m, ctypes.byref(out), self.num_envs, self._stream()),
+                        "mg_reset")
+        if mask is None:
+            self.done.zero_()
+            self.coll.zero_()
+        return self.obs
+
+    def step(self, actions1, actions2=None):
+        """One step of every env: merging_env.py:138-195 batched. actions2=None is the
+        reference's L0 opponent (constant speed); per-env -1 also means None."""
+        a1 = self._actions(actions1, self.a1_buf, allow_none=False)
+        a2 = self._actions(actions2, self.a2_buf, allow_none=True)
+        rc = self._nat.lib.mg_step(
+            ctypes.byref(self.params), ctypes.byref(self._state), ctypes.c_void_p(a1.data_ptr()),
+            None if a2 is None else ctypes.c_void_p(a2.data_ptr()), ctypes.byref(self._out),
+            ctypes.byref(self._stats), self.num_envs, self._flags, self._stream())
+        self._nat.check(rc, "mg_step")
+        return self._outputs()
+
+    def step_random(self, seed: int, opponent_random: bool = True, step_idx=None,
+                    record_actions: bool = True):
+        """One step with actions drawn on the GPU (Philox4x32-10 keyed by seed, counter =
+        (global env index, step index)). The actions used land in self.a1_buf / a2_buf."""
+        k = self._step_idx if step_idx is None else int(step_idx)
+        rc = self._nat.lib.mg_step_random(
+            ctypes.byref(self.params), ctypes.byref(self._state),
+            ctypes.c_void_p(self.a1_buf.data_ptr()) if record_actions else None,
+            ctypes.c_void_p(self.a2_buf.data_ptr()) if record_actions else None,
+            ctypes.byref(self._out), ctypes.byref(self._stats), self.num_envs, self.env_offset,
+            int(seed) & 0xFFFFFFFFFFFFFFFF, k & 0xFFFFFFFFFFFFFFFF, int(bool(opponent_random)),
+            self._flags, self._stream())
+        self._nat.check(rc, "mg_step_random")
+        self._step_idx = k + 1
+        return self._outputs()
+
+    def observe(self):
+        """Observation of the current state without stepping (merging_env.py:118-132)."""
+        out = self._nat.Outputs(self._out.obs, None, None, self._out.coll, None, None, None, None)
+        self._nat.check(self._nat.lib.mg_observe(ctypes.byref(self.params), ctypes.byref(self._state),
+                                                 ctypes.byref(out), self.num_envs, self._stream()),
+                        "mg_observe")
+        return self.obs
+
+    def check_actions(self):
+        """Raise KeyError if any step since the last check saw an action outside the
+        reference's action_dict (merging_env.py:101). Synchronises the stream."""
+        err = int(self.error.item())
+        if err:
+            self.error.zero_()
+            raise KeyError(f"invalid action in batch (a1: {bool(err & 1)}, a2: {bool(err & 2)})")
+
+    # ------------------------------------------------------------------ state views
+    @property
+    def steps(self):
+        return self.tf & self._nat.TF_STEPS_MASK
+
+    @property
+    def winner(self):
+        return (self.tf & self._nat.TF_WINNER_MASK) >> self._nat.TF_WINNER_SHIFT
+
+    def episode_statistics(self):
+        """Completed-episode totals per env: returns sum [N,2] f64 and counts [N,4] i32
+        (episodes, collisions, ego-first arrivals, steps)."""
+        return {"ret_sum": self.ret_sum, "counts": self.counts}
+
+    def clear_statistics(self):
+        if self.ret_sum is not None:
+            self.ret_sum.zero_()
+            self.counts.zero_()
+
+    def close(self):
+        pass

@@ -1,0 +1,338 @@
+/*
+ * merge_oracle.c -- CPU restatement of the reference MergeEnv step path.
+ * TEST INFRASTRUCTURE ONLY: loaded by tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg through oracle/merge_oracle.py. The product never links it.
+ *
+ * It follows the reference (YikangZhang1641/merging-gym @ /root/reference) step by step,
+ * with the reference's own fp64 state layout (a dict per car + float clock), NOT the GPU
+ * kernel's packed state, so the kernel is checked against an independent formulation:
+ *   lon2coord            merging_gym/envs/merging_env.py:48-58   (libm sin/cos/atan2)
+ *   observe              merging_env.py:118-132
+ *   action_to_acc        merging_env.py:134-136 -> mpc_1d scripts/helper.py:152-191: the QP
+ *                        is built and solved (Cholesky + one Goldfarb-Idnani equality step),
+ *                        not replaced by its closed form
+ *   step                 merging_env.py:138-195 (fp64 clock accumulated with += 0.2)
+ *   is_collided/corners  merging_env.py:198-206, :232-239 (pygame C-int truncation, fp64
+ *                        Vector2 arithmetic, closed-box polygon intersection)
+ *   reset                merging_env.py:208-230
+ * plus Philox4x32-10 (Salmon et al. SC'11, the published algorithm) for the device-drawn
+ * actions of mg_step_random.
+ *
+ * Build: oracle/Makefile (gcc -O2 -fopenmp -ffp-contract=off).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+typedef struct oracle_env {
+  double pos1, vel1, acc1; /* self.state1 */
+  double pos2, vel2, acc2; /* self.state2 */
+  double time_stamp;       /* self.time_stamp */
+  double r1_acc, r2_acc;   /* self.r1_accumulate, self.r2_accumulate */
+  int32_t winner;          /* self.winner: 0 = None, 1, 2 */
+  int32_t done;            /* self.done */
+  int32_t steps;           /* steps since reset: bookkeeping for episode statistics only */
+  int32_t pad_;
+} oracle_env;
+
+/* merging_env.py:22-46, :101 */
+static const double R = 30000.0, H = 1000.0, W = 300.0, DT = 0.2;
+static const double R_FIRST = 2.0, R_SECOND = 1.0, R_COLLISION = -10.0;
+static const double VEL_PENALTY = 0.001, TIME_PENALTY = 0.0;
+static const double START_POINT = 50.0, END_POINT = 950.0, PREDICTION_T = 3.0;
+static const int VEHICLE_W = 4, VEHICLE_H = 8;
+static const double ACTION_SPEED[5] = {0.0, 10.0, 20.0, 30.0, 40.0};
+
+/* status bits, identical to include/merging_hip.h MG_ST_* */
+enum { ST_DONE = 1, ST_COLL = 2, ST_R1_INT = 4, ST_R2_INT = 8, ST_V1_INT = 16, ST_V2_INT = 32,
+       ST_ERR1 = 64, ST_ERR2 = 128 };
+
+static double arc_angle(double lon) {
+  volatile double h = H, r = R; /* evaluate atan2 at run time, as numpy does */
+  return atan2(h, r) - lon / R;
+}
+
+static void lon2coord(double lon, int ego, double* x, double* y) {
+  const double a = arc_angle(lon);
+  *x = R * sin(a);
+  const double bulge = R - R * cos(a);
+  *y = ego ? W / 2 + bulge : W / 2 - bulge;
+}
+
+/* mpc_1d(x0, v0, xt, vt, t).action(): helper.py:152-191. */
+static double mpc_first_accel(double x0, double v0, double xt, double vt, double t) {
+  enum { T = 10 };
+  const double dt = t / T;
+  /* A[:, i] = a^(T-1-i) b, built from the last column backwards like the reference */
+  double A[2][T];
+  double pw[2][2] = {{1.0, 0.0}, {0.0, 1.0}};
+  for (int i = T - 1; i >= 0; --i) {
+    A[0][i] = pw[0][0] * 0.0 + pw[0][1] * dt;
+    A[1][i] = pw[1][0] * 0.0 + pw[1][1] * dt;
+    const double n00 = 1.0 * pw[0][0] + dt * pw[1][0], n01 = 1.0 * pw[0][1] + dt * pw[1][1];
+    const double n10 = 0.0 * pw[0][0] + 1.0 * pw[1][0], n11 = 0.0 * pw[0][1] + 1.0 * pw[1][1];
+    pw[0][0] = n00; pw[0][1] = n01; pw[1][0] = n10; pw[1][1] = n11;
+  }
+  (void)xt; /* the position row of the constraint is dropped by the reference (:173) */
+  const double rhs = vt - (pw[1][0] * x0 + pw[1][1] * v0);
+  /* P = D'D + 0.01 I, D[i][i] = 1, D[i][i+1] = -1 (i < T-1) */
+  double P[T][T];
+  memset(P, 0, sizeof(P));
+  for (int i = 0; i < T - 1; ++i) {
+    P[i][i] += 1.0;
+    P[i + 1][i + 1] += 1.0;
+    P[i][i + 1] -= 1.0;
+    P[i + 1][i] -= 1.0;
+  }
+  for (int i = 0; i < T; ++i) P[i][i] += 0.01;
+  /* Cholesky P = L L' */
+  double L[T][T];
+  memset(L, 0, sizeof(L));
+  for (int j = 0; j < T; ++j) {
+    double s = P[j][j];
+    for (int k = 0; k < j; ++k) s -= L[j][k] * L[j][k];
+    L[j][j] = sqrt(s);
+    for (int i = j + 1; i < T; ++i) {
+      double v = P[i][j];
+      for (int k = 0; k < j; ++k) v -= L[i][k] * L[j][k];
+      L[i][j] = v / L[j][j];
+    }
+  }
+  /* z = P^-1 n with n = A[1] (the equality's normal); u = rhs / (n'z) * z */
+  double y[T], z[T];
+  for (int i = 0; i < T; ++i) {
+    double v = A[1][i];
+    for (int k = 0; k < i; ++k) v -= L[i][k] * y[k];
+    y[i] = v / L[i][i];
+  }
+  for (int i = T - 1; i >= 0; --i) {
+    double v = y[i];
+    for (int k = i + 1; k < T; ++k) v -= L[k][i] * z[k];
+    z[i] = v / L[i][i];
+  }
+  double nz = 0.0;
+  for (int i = 0; i < T; ++i) nz += A[1][i] * z[i];
+  return (rhs / nz) * z[0];
+}
+
+/* corners(agent, y=x, x=y, 0) (merging_env.py:232-239) as a closed box */
+typedef struct { double xmin, xmax, ymin, ymax; } box;
+
+static box vehicle_box(double lateral, double longitudinal) {
+  const int left = (int)lateral - VEHICLE_W / 2; /* pygame Rect: C (int) cast of the centre */
+  const int top = (int)longitudinal - VEHICLE_H / 2;
+  const double c[4][2] = {{left, top}, {left + VEHICLE_W, top},
+                          {left + VEHICLE_W, top + VEHICLE_H}, {left, top + VEHICLE_H}};
+  box b = {INFINITY, -INFINITY, INFINITY, -INFINITY};
+  for (int k = 0; k < 4; ++k) {
+    /* scale * (Vector2(corner) - pivot).rotate(-0) + pivot, scale = 1.0 */
+    const double px = 1.0 * (c[k][0] - lateral) + lateral;
+    const double py = 1.0 * (c[k][1] - longitudinal) + longitudinal;
+    b.xmin = fmin(b.xmin, px);
+    b.xmax = fmax(b.xmax, px);
+    b.ymin = fmin(b.ymin, py);
+    b.ymax = fmax(b.ymax, py);
+  }
+  return b;
+}
+
+static int polygons_intersect(box a, box b) { /* closed sets: touching counts */
+  return a.xmin <= b.xmax && b.xmin <= a.xmax && a.ymin <= b.ymax && b.ymin <= a.ymax;
+}
+
+static int is_collided(const oracle_env* e) {
+  double x1, y1, x2, y2;
+  lon2coord(e->pos1, 1, &x1, &y1);
+  lon2coord(e->pos2, 0, &x2, &y2);
+  return polygons_intersect(vehicle_box(y1, x1), vehicle_box(y2, x2));
+}
+
+static void observe(const oracle_env* e, double o[10]) {
+  double x1, y1, x2, y2;
+  lon2coord(e->pos1, 1, &x1, &y1);
+  lon2coord(e->pos2, 0, &x2, &y2);
+  o[0] = x2 - x1; o[1] = y2 - y1; o[2] = e->vel2 - e->vel1; o[3] = END_POINT - e->pos1;
+  o[4] = e->vel1; o[5] = x1 - x2; o[6] = y1 - y2; o[7] = e->vel1 - e->vel2;
+  o[8] = END_POINT - e->pos2; o[9] = e->vel2;
+}
+
+static void env_reset(oracle_env* e, double o[10]) {
+  memset(e, 0, sizeof(*e));
+  e->pos1 = e->pos2 = START_POINT;
+  e->vel1 = e->vel2 = 20.0;
+  if (o) observe(e, o);
+}
+
+static int valid(int a) { return a >= 0 && a < 5; }
+
+/* one MergeEnv.step; a2 < 0 means None. Returns ST_* bits. */
+static uint32_t env_step(oracle_env* e, int a1, int a2, double o[10], double rew[2], int* coll) {
+  uint32_t st = 0;
+  e->time_stamp += DT;
+  e->steps += 1;
+  if (e->time_stamp > 500) e->done = 1;
+  *coll = 0;
+  if (!valid(a1)) return ST_ERR1;
+  {
+    const double vt = ACTION_SPEED[a1];
+    e->acc1 = mpc_first_accel(e->pos1, e->vel1, e->pos1 + vt * PREDICTION_T, vt, PREDICTION_T);
+    const double v = e->vel1 + e->acc1 * DT;
+    if (v > 0) e->vel1 = v; else { e->vel1 = 0.0; st |= ST_V1_INT; } /* max(0, v) */
+    e->pos1 += e->vel1 * DT;
+  }
+  if (a2 >= 0 && !valid(a2)) return st | ST_ERR2;
+  if (a2 < 0) {
+    e->acc2 = 0.0;
+  } else {
+    const double vt = ACTION_SPEED[a2];
+    e->acc2 = mpc_first_accel(e->pos2, e->vel2, e->pos2 + vt * PREDICTION_T, vt, PREDICTION_T);
+  }
+  {
+    const double v = e->vel2 + e->acc2 * DT;
+    if (v > 0) e->vel2 = v; else { e->vel2 = 0.0; st |= ST_V2_INT; }
+    e->pos2 += e->vel2 * DT;
+  }
+  observe(e, o);
+  double r1 = (0.0 - TIME_PENALTY) - VEL_PENALTY * fabs(e->vel1 - 20.0);
+  double r2 = (0.0 - TIME_PENALTY) - VEL_PENALTY * fabs(e->vel2 - 20.0);
+  if (e->pos1 > END_POINT) {
+    if (e->winner == 0) { e->winner = 1; r1 += R_FIRST; }
+    else if (e->winner == 1) { r1 = 0.0; st |= ST_R1_INT; }
+    else { r1 += R_SECOND; e->done = 1; }
+  }
+  if (e->pos2 >= END_POINT) {
+    if (e->winner == 0) { e->winner = 2; r2 += R_FIRST; }
+    else if (e->winner == 2) { r2 = 0.0; st |= ST_R2_INT; }
+    else { r2 += R_SECOND; e->done = 1; }
+  }
+  if (is_collided(e)) {
+    e->done = 1;
+    r1 += R_COLLISION;
+    r2 += R_COLLISION;
+    *coll = 1;
+    st |= ST_COLL;
+  }
+  e->r1_acc += r1;
+  e->r2_acc += r2;
+  rew[0] = r1;
+  rew[1] = r2;
+  if (e->done) st |= ST_DONE;
+  return st;
+}
+
+/* Episode bookkeeping + gym.vector autoreset (obs <- reset obs, fobs <- terminal obs). */
+static void finish_episode(oracle_env* e, int coll, double* o, double* fobs, double* ret_sum,
+                           uint32_t* counts) {
+  if (ret_sum) { ret_sum[0] += e->r1_acc; ret_sum[1] += e->r2_acc; }
+  if (counts) {
+    counts[0] += 1;
+    counts[1] += coll ? 1u : 0u;
+    counts[2] += e->winner == 1 ? 1u : 0u;
+    counts[3] += (uint32_t)e->steps;
+  }
+  if (fobs) memcpy(fobs, o, 10 * sizeof(double));
+  env_reset(e, o);
+}
+
+/* ------------------------------------------------------------------ Philox4x32-10 */
+void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+  uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3], k0 = key[0], k1 = key[1];
+  for (int r = 0; r < 10; ++r) {
+    if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n1 = (uint32_t)p1;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1, n3 = (uint32_t)p0;
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+static void draw_actions(int64_t gi, uint64_t seed, uint64_t step, int opp_random, int* a1, int* a2) {
+  const uint32_t c[4] = {(uint32_t)gi, (uint32_t)((uint64_t)gi >> 32), (uint32_t)step,
+                         (uint32_t)(step >> 32)};
+  const uint32_t k[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  uint32_t u[4];
+  oracle_philox4x32_10(c, k, u);
+  *a1 = (int)(((uint64_t)u[0] * 5u) >> 32);
+  *a2 = opp_random ? (int)(((uint64_t)u[1] * 5u) >> 32) : -1;
+}
+
+void oracle_random_actions(int64_t n, int64_t env_offset, uint64_t seed, uint64_t step,
+                           int32_t opp_random, int8_t* a1, int8_t* a2) {
+  for (int64_t i = 0; i < n; ++i) {
+    int x, y;
+    draw_actions(env_offset + i, seed, step, opp_random, &x, &y);
+    a1[i] = (int8_t)x;
+    a2[i] = (int8_t)y;
+  }
+}
+
+/* ------------------------------------------------------------------ batched entry points */
+void oracle_set_threads(int32_t n) {
+#ifdef _OPENMP
+  omp_set_num_threads(n > 0 ? n : 1);
+#else
+  (void)n;
+#endif
+}
+
+int32_t oracle_max_threads(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
+}
+
+void oracle_reset_batch(oracle_env* envs, int64_t n, double* obs) {
+  for (int64_t i = 0; i < n; ++i) env_reset(&envs[i], obs ? obs + 10 * i : NULL);
+}
+
+/* One step of n envs. a2 may be NULL (all None). Returns OR of the error bits (1: a1, 2: a2). */
+int32_t oracle_step_batch(oracle_env* envs, int64_t n, const int8_t* a1, const int8_t* a2,
+                          int32_t autoreset, double* obs, double* rew, uint8_t* done,
+                          uint8_t* coll, double* final_obs, double* ret_sum, uint32_t* counts,
+                          uint32_t* status, int32_t unused) {
+  (void)unused;
+  int32_t err = 0;
+#pragma omp parallel for schedule(static) reduction(| : err)
+  for (int64_t i = 0; i < n; ++i) {
+    double o[10] = {0}, r[2] = {0, 0};
+    int c = 0;
+    const uint32_t st = env_step(&envs[i], a1[i], a2 ? a2[i] : -1, o, r, &c);
+    if (st & ST_ERR1) err |= 1;
+    if (st & ST_ERR2) err |= 2;
+    const int d = (st & (ST_ERR1 | ST_ERR2)) ? 0 : envs[i].done;
+    if (autoreset && d)
+      finish_episode(&envs[i], c, o, final_obs ? final_obs + 10 * i : NULL,
+                     ret_sum ? ret_sum + 2 * i : NULL, counts ? counts + 4 * i : NULL);
+    if (obs) memcpy(obs + 10 * i, o, sizeof(o));
+    if (rew) { rew[2 * i] = r[0]; rew[2 * i + 1] = r[1]; }
+    if (done) done[i] = (uint8_t)d;
+    if (coll) coll[i] = (uint8_t)c;
+    if (status) status[i] = st;
+  }
+  return err;
+}
+
+/* `steps` autoreset steps with Philox actions: the CPU baseline of the bench workload. */
+int64_t oracle_rollout_random(oracle_env* envs, int64_t n, int64_t steps, uint64_t seed,
+                              uint64_t first_step, int32_t opp_random, int32_t env_offset,
+                              double* ret_sum, uint32_t* counts) {
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < n; ++i) {
+    for (int64_t k = 0; k < steps; ++k) {
+      int x, y, c = 0;
+      double o[10], r[2];
+      draw_actions(env_offset + i, seed, first_step + (uint64_t)k, opp_random, &x, &y);
+      env_step(&envs[i], x, y, o, r, &c);
+      if (envs[i].done)
+        finish_episode(&envs[i], c, o, NULL, ret_sum ? ret_sum + 2 * i : NULL,
+                       counts ? counts + 4 * i : NULL);
+    }
+  }
+  return n * steps;
+}

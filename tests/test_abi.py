@@ -1,0 +1,86 @@
+"""The C-ABI library loads on a CPU-only host and exports every entry point include/*.h declares."""
+
+import ctypes
+import glob
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+
+def _declared():
+    names = set()
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        text = open(h).read()
+        names |= set(re.findall(r"^\s*(?:int|void|const char\*)\s+(mg_\w+)\s*\(", text, re.M))
+    return names
+
+
+def test_header_declares_the_step_path():
+    assert {"mg_step", "mg_step_random", "mg_reset", "mg_observe", "mg_abi_version",
+            "mg_last_error", "mg_params_default"} <= _declared()
+
+
+def test_library_exports_every_declared_symbol():
+    from merging_gym import _native
+
+    lib = ctypes.CDLL(_native.LIB_PATH)
+    for name in sorted(_declared()):
+        assert hasattr(lib, name), name
+    assert _native.lib.mg_abi_version() == _native.ABI_VERSION
+
+
+def test_struct_layouts_match_header():
+    from merging_gym import _native
+
+    # mg_params: 15 doubles + 5 doubles + 4 int32; mg_rec64: 20 doubles + 2 uint32
+    assert ctypes.sizeof(_native.Params) == 20 * 8 + 16
+    assert ctypes.sizeof(_native.State) == 7 * 8
+    assert ctypes.sizeof(_native.Outputs) == 8 * 8
+    assert ctypes.sizeof(_native.Stats) == 2 * 8
+    assert _native.REC64_DTYPE.itemsize == 168
+
+
+def test_default_params_are_the_reference_constants():
+    """merging_env.py:22-46, :101 -- filled by the library itself (host code, no GPU)."""
+    import numpy as np
+
+    from merging_gym import _native
+
+    p = _native.default_params()
+    assert (p.R, p.H, p.W, p.dT) == (30000.0, 1000.0, 300.0, 0.2)
+    assert (p.r_first, p.r_second, p.r_collision, p.vel_penalty, p.time_penalty) == (2.0, 1.0, -10.0, 0.001, 0.0)
+    assert (p.start_point, p.end_point, p.start_vel, p.vel_ref, p.prediction_t) == (50.0, 950.0, 20.0, 20.0, 3.0)
+    assert list(p.action_speed) == [0.0, 10.0, 20.0, 30.0, 40.0]
+    assert (p.veh_w, p.veh_h, p.timeout_steps) == (4, 8, 2501)
+    assert p.angle0 == float(np.arctan2(1000, 30000))
+
+
+def test_argument_errors_without_gpu():
+    """Validation happens before any launch, so it is testable on a CPU-only host."""
+    from merging_gym import _native
+
+    rc = _native.lib.mg_step(ctypes.byref(_native.default_params()), ctypes.byref(_native.State()),
+                             None, None, ctypes.byref(_native.Outputs()), None, 16, 0, None)
+    assert rc != 0 and b"NULL" in _native.lib.mg_last_error()
+    rc = _native.lib.mg_reset(None, None, None, None, 1, None)
+    assert rc != 0
+
+
+def test_timeout_step_is_2501():
+    """time_stamp += 0.2 in fp64 first exceeds 500 at step 2501 (merging_env.py:141-143)."""
+    t, k = 0.0, 0
+    while not t > 500:
+        t += 0.2
+        k += 1
+    assert k == 2501
+
+
+def test_build_flags_disable_contraction():
+    from merging_gym import build
+
+    assert "-ffp-contract=off" in build.HIPCC_FLAGS and "--offload-arch=gfx950" in build.HIPCC_FLAGS
+    src = open(build.SRC).read()
+    assert "#pragma clang fp contract(off)" in src

@@ -1,0 +1,230 @@
+"""GPU parity: libmerging_hip.so (through the C-ABI, via MergeVecEnv / MergeEnv) vs the CPU oracle.
+
+Bar (north_star): done / collision / winner flags bit-exact; fp32 outputs equal to the
+oracle's fp64 values rounded to fp32 (rtol 1e-6, atol 1e-5 -- tighter than the 1e-5 fp32
+bound); fp64 state (positions, speeds, returns) within 1e-9 absolute (the oracle solves the
+reference's QP numerically, the kernel uses its closed form; they differ by fp64 rounding).
+"""
+
+import ctypes
+
+import numpy as np
+import pytest
+
+import merge_oracle as mo
+
+pytestmark = pytest.mark.gpu
+
+OBS_TOL = dict(rtol=1e-6, atol=1e-5)
+STATE_TOL = dict(rtol=0, atol=1e-9)
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+
+    return t
+
+
+def _check_state(env, envs):
+    np.testing.assert_allclose(env.p1.cpu().numpy(), envs["pos1"], **STATE_TOL)
+    np.testing.assert_allclose(env.p2.cpu().numpy(), envs["pos2"], **STATE_TOL)
+    np.testing.assert_allclose(env.v1.cpu().numpy(), envs["vel1"], **STATE_TOL)
+    np.testing.assert_allclose(env.v2.cpu().numpy(), envs["vel2"], **STATE_TOL)
+    np.testing.assert_allclose(env.ret1.cpu().numpy(), envs["r1_acc"], **STATE_TOL)
+    np.testing.assert_allclose(env.ret2.cpu().numpy(), envs["r2_acc"], **STATE_TOL)
+    np.testing.assert_array_equal(env.winner.cpu().numpy(), envs["winner"])
+    np.testing.assert_array_equal(env.steps.cpu().numpy(), envs["steps"])
+
+
+def _check_step(out, ref, k):
+    obs, rew, done, info = out
+    o_obs, o_rew, o_done, o_coll, _, o_fobs, err = ref
+    assert err == 0
+    np.testing.assert_array_equal(done.cpu().numpy(), o_done.astype(bool), err_msg=f"done @ {k}")
+    np.testing.assert_array_equal(info["collision"].cpu().numpy(), o_coll.astype(bool), err_msg=f"coll @ {k}")
+    np.testing.assert_allclose(obs.cpu().numpy(), o_obs.astype(np.float32), **OBS_TOL, err_msg=f"obs @ {k}")
+    np.testing.assert_allclose(rew.cpu().numpy(), o_rew.astype(np.float32), **OBS_TOL, err_msg=f"rew @ {k}")
+    if o_fobs is not None and "final_observation" in info:
+        d = o_done.astype(bool)
+        np.testing.assert_allclose(info["final_observation"].cpu().numpy()[d], o_fobs[d].astype(np.float32),
+                                   **OBS_TOL, err_msg=f"final_obs @ {k}")
+
+
+@pytest.mark.parametrize("opponent", ["uniform", "none", "mixed"])
+def test_config2_host_actions_autoreset(torch, coracle, opponent):
+    """BASELINE config 2: 4,096 envs, 500 steps, host-drawn actions, gym.vector autoreset."""
+    from merging_gym import MergeVecEnv
+
+    n, steps = 4096, 500
+    rng = np.random.default_rng(11)
+    env = MergeVecEnv(n, device="cuda:0")
+    envs = coracle.new_envs(n)
+    o0 = coracle.reset(envs)
+    np.testing.assert_allclose(env.obs.cpu().numpy(), o0.astype(np.float32), **OBS_TOL)
+    ret_sum = np.zeros((n, 2))
+    counts = np.zeros((n, 4), np.uint32)
+    for k in range(steps):
+        a1 = rng.integers(0, 5, n).astype(np.int8)
+        if opponent == "uniform":
+            a2 = rng.integers(0, 5, n).astype(np.int8)
+        elif opponent == "none":
+            a2 = None
+        else:
+            a2 = rng.integers(-1, 5, n).astype(np.int8)
+        out = env.step(torch.from_numpy(a1).cuda(), None if a2 is None else torch.from_numpy(a2).cuda())
+        ref = coracle.step(envs, a1, a2, autoreset=True, final_obs=True, stats=(ret_sum, counts))
+        _check_step(out, ref, k)
+    _check_state(env, envs)
+    st = env.episode_statistics()
+    np.testing.assert_array_equal(st["counts"].cpu().numpy().astype(np.uint32), counts)
+    np.testing.assert_allclose(st["ret_sum"].cpu().numpy(), ret_sum, rtol=0, atol=1e-8)
+    assert counts[:, 0].sum() > 0 and counts[:, 1].sum() > 0  # episodes finished, some collided
+    # size-independent invariant: every step is in a finished episode or the running one
+    np.testing.assert_array_equal(counts[:, 3] + envs["steps"], steps)
+
+
+def test_past_done_no_autoreset(torch, coracle):
+    """Reference semantics without reset: cars keep driving past done, the 2501-step timeout
+    fires, the winner keeps its flag, and the x ~ 0 corner rounding region is crossed."""
+    from merging_gym import MergeVecEnv
+
+    n, steps = 1024, 2600
+    rng = np.random.default_rng(5)
+    env = MergeVecEnv(n, device="cuda:0", autoreset=False)
+    envs = coracle.new_envs(n)
+    coracle.reset(envs)
+    for k in range(steps):
+        a1 = rng.integers(0, 5, n).astype(np.int8)
+        a2 = rng.integers(-1, 5, n).astype(np.int8)
+        out = env.step(torch.from_numpy(a1).cuda(), torch.from_numpy(a2).cuda())
+        ref = coracle.step(envs, a1, a2)
+        if k % 50 == 0 or k > 2490:
+            _check_step(out, ref, k)
+    _check_step(out, ref, steps)
+    _check_state(env, envs)
+    assert envs["done"].all()  # the timeout caught every env
+    np.testing.assert_array_equal(env.done.cpu().numpy(), np.ones(n, np.uint8))
+
+
+def test_device_random_actions_match_philox(torch, coracle):
+    """mg_step_random: the device Philox stream equals the oracle's, and the step matches."""
+    from merging_gym import MergeVecEnv
+
+    n, steps, seed = 3000, 300, 99
+    env = MergeVecEnv(n, device="cuda:0")
+    envs = coracle.new_envs(n)
+    coracle.reset(envs)
+    for k in range(steps):
+        out = env.step_random(seed, opponent_random=(k % 3 != 0), step_idx=k)
+        a1, a2 = coracle.random_actions(n, 0, seed, k, k % 3 != 0)
+        np.testing.assert_array_equal(env.a1_buf.cpu().numpy(), a1)
+        np.testing.assert_array_equal(env.a2_buf.cpu().numpy(), a2)
+        ref = coracle.step(envs, a1, a2, autoreset=True, final_obs=True)
+        _check_step(out, ref, k)
+    _check_state(env, envs)
+
+
+def test_golden_one_step_rows(torch, golden):
+    """The reference's own one-step outputs from 8,000 states near the boundaries."""
+    from merging_gym import MergeVecEnv
+
+    g = golden
+    n = len(g["one_a1"])
+    env = MergeVecEnv(n, device="cuda:0", autoreset=False)
+    dev = env.device
+    env.p1.copy_(torch.from_numpy(g["one_p"][:, 0]))
+    env.p2.copy_(torch.from_numpy(g["one_p"][:, 1]))
+    env.v1.copy_(torch.from_numpy(g["one_v"][:, 0]))
+    env.v2.copy_(torch.from_numpy(g["one_v"][:, 1]))
+    env.ret1.copy_(torch.from_numpy(g["one_racc"][:, 0]))
+    env.ret2.copy_(torch.from_numpy(g["one_racc"][:, 1]))
+    tf = (g["one_k"].astype(np.int64) & 0xFFFF) | (g["one_winner"].astype(np.int64) << 16) | (
+        g["one_done"].astype(np.int64) << 18)
+    env.tf.copy_(torch.from_numpy(tf.astype(np.int32)))
+    obs, rew, done, info = env.step(torch.from_numpy(g["one_a1"]).to(dev), torch.from_numpy(g["one_a2"]).to(dev))
+    np.testing.assert_array_equal(done.cpu().numpy(), g["one_done_out"])
+    np.testing.assert_array_equal(info["collision"].cpu().numpy(), g["one_coll"])
+    np.testing.assert_array_equal(env.winner.cpu().numpy(), g["one_winner_out"])
+    np.testing.assert_allclose(obs.cpu().numpy(), g["one_obs"].astype(np.float32), **OBS_TOL)
+    np.testing.assert_allclose(rew.cpu().numpy(), g["one_rew"].astype(np.float32), **OBS_TOL)
+    np.testing.assert_allclose(env.p1.cpu().numpy(), g["one_pos"][:, 0], **STATE_TOL)
+    np.testing.assert_allclose(env.p2.cpu().numpy(), g["one_pos"][:, 1], **STATE_TOL)
+    np.testing.assert_allclose(env.ret1.cpu().numpy(), g["one_racc_out"][:, 0], **STATE_TOL)
+
+
+def test_sharding_matches_unsharded(torch):
+    """Two shards with env_offset draw the same actions and reach the same state as one batch."""
+    from merging_gym import MergeVecEnv
+
+    n, steps, seed = 5000, 200, 3
+    full = MergeVecEnv(n, device="cuda:0")
+    a = MergeVecEnv(2048, device="cuda:0", env_offset=0)
+    b = MergeVecEnv(n - 2048, device="cuda:0", env_offset=2048)
+    for k in range(steps):
+        full.step_random(seed, step_idx=k)
+        a.step_random(seed, step_idx=k)
+        b.step_random(seed, step_idx=k)
+    for name in ("p1", "v1", "p2", "v2", "ret1", "ret2", "tf", "obs"):
+        whole = getattr(full, name)
+        parts = torch.cat([getattr(a, name), getattr(b, name)])
+        assert torch.equal(whole, parts), name
+
+
+def test_full_size_properties(torch, coracle):
+    """Config 3 size (2^20 envs): invariants over the whole batch plus oracle spot checks of
+    2,048 random envs (Philox is keyed by the global env index, so any env can be replayed)."""
+    from merging_gym import MergeVecEnv
+
+    n, steps, seed = 1 << 20, 120, 2024
+    env = MergeVecEnv(n, device="cuda:0", done_mask=True)
+    reset_row = env.obs[0].clone()
+    for k in range(steps):
+        obs, rew, done, info = env.step_random(seed, step_idx=k)
+        if k % 40 == 39:
+            d = done.cpu().numpy()
+            # autoreset: finished envs show the reset observation
+            assert torch.equal(obs[done], reset_row.expand(int(d.sum()), -1))
+            # the ballot mask agrees with the done bytes
+            words = env.done_mask.cpu().numpy().view(np.uint64)
+            bits = np.unpackbits(words.view(np.uint8), bitorder="little")[:n].astype(bool)
+            np.testing.assert_array_equal(bits, d)
+            assert not torch.isnan(obs).any()
+    counts = env.counts.cpu().numpy().astype(np.int64)
+    np.testing.assert_array_equal(counts[:, 3] + env.steps.cpu().numpy(), steps)
+    assert counts[:, 0].sum() > 0
+    idx = np.sort(np.random.default_rng(0).choice(n, 2048, replace=False))
+    p1 = env.p1.cpu().numpy()[idx]
+    r1 = env.ret1.cpu().numpy()[idx]
+    c = counts[idx]
+    for j, gi in enumerate(idx):
+        e = coracle.new_envs(1)
+        coracle.reset(e)
+        rs, ct = np.zeros((1, 2)), np.zeros((1, 4), np.uint32)
+        coracle.rollout_random(e, steps, seed, 0, True, env_offset=int(gi), stats=(rs, ct))
+        assert abs(e["pos1"][0] - p1[j]) <= 1e-9 and abs(e["r1_acc"][0] - r1[j]) <= 1e-9, gi
+        np.testing.assert_array_equal(ct[0], c[j])
+
+
+def test_invalid_actions_flag_error(torch):
+    from merging_gym import MergeVecEnv
+
+    env = MergeVecEnv(64, device="cuda:0", autoreset=False)
+    a1 = torch.full((64,), 2, dtype=torch.int8, device="cuda:0")
+    a1[5] = 9
+    env.step(a1)
+    with pytest.raises(KeyError):
+        env.check_actions()
+    assert int(env.steps[5]) == 1 and float(env.p1[5]) == 50.0  # clock advanced, car not
+    env.step(torch.full((64,), 2, dtype=torch.int8, device="cuda:0"))
+    env.check_actions()
+
+
+def test_native_errors_are_raised(torch):
+    from merging_gym import _native
+
+    st = _native.State()
+    out = _native.Outputs()
+    rc = _native.lib.mg_step(ctypes.byref(_native.default_params()), ctypes.byref(st), None, None,
+                             ctypes.byref(out), None, 16, 0, None)
+    assert rc != 0 and b"NULL" in _native.lib.mg_last_error()
