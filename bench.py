@@ -116,25 +116,29 @@ def main():
     env.clear_statistics()
     torch.cuda.synchronize()
 
+    # per-launch kernel time: HIP events recorded by each dispatch packet (hipExtLaunchKernel)
     use_events = not args.no_events
     if use_events:
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(args.steps)]
+        from merging_gym.profiling import KernelTimer
+
+        timer = KernelTimer(args.steps)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
         if use_events:
-            ev[k][0].record()
+            timer.arm(k)
         step(args.warmup + k)
-        if use_events:
-            ev[k][1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kernel_ms = (sum(a.elapsed_time(b) for a, b in ev) / args.steps) if use_events else None
+    kernel_ms = None
+    if use_events:
+        durs = timer.durations_ms()
+        kernel_ms = sum(durs) / len(durs)
+        timer.close()
 
     t = torch.tensor([elapsed, kernel_ms or 0.0], dtype=torch.float64, device=device)
     if world > 1:

@@ -16,7 +16,8 @@
  *   mg_reset        replaces MergeEnv.reset()                        merging_env.py:208-230
  *   mg_observe      replaces MergeEnv.observe() and is_collided()    merging_env.py:118-132,
  *                     :198-206 (no state change)
- *   mg_abi_version, mg_last_error, mg_params_default: library plumbing (no reference twin).
+ *   mg_abi_version, mg_last_error, mg_params_default, mg_time_next_launch: library plumbing
+ *                     and profiling (no reference twin).
  *
  * Conventions
  *   - Every pointer inside mg_state / mg_outputs / mg_stats / action arrays is a DEVICE
@@ -132,6 +133,12 @@ typedef struct mg_stats {
 
 int mg_abi_version(void);
 const char* mg_last_error(void);
+
+/* Profiling hook: the next mg_step / mg_step_random launch made by the calling thread records
+ * start_event / stop_event (hipEvent_t created by the caller; either may be NULL) in its own
+ * dispatch packet (hipExtLaunchKernel), so hipEventElapsedTime(start, stop) is the kernel's
+ * duration without the launch gap. Consumed by that launch. Always returns 0. */
+int mg_time_next_launch(void* start_event, void* stop_event);
 
 /* Fills *p with the reference constants (merging_env.py:22-46, :101). Host only. */
 void mg_params_default(mg_params* p);

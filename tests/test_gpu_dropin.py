@@ -1,0 +1,127 @@
+"""Drop-in parity: merging_gym.make("merging_env-v0") (GPU-backed, list API) replays the
+reference's own traces (tests/golden) -- values, flags and Python value types."""
+
+import numpy as np
+import pytest
+
+import merge_oracle as mo
+from test_gpu_parity import merge_zone
+
+pytestmark = pytest.mark.gpu
+
+TRACES = [f"kat{k}" for k in "ABCDEFG"] + ["rndL0", "rndRR", "past"]
+T_R1_INT, T_R2_INT, T_OBS3_INT, T_OBS8_INT, T_OBS4_INT, T_OBS9_INT = 1, 2, 4, 8, 16, 32
+
+
+def _types(obs, rew):
+    t = 0
+    for bit, v in ((T_R1_INT, rew[0]), (T_R2_INT, rew[1]), (T_OBS3_INT, obs[3]),
+                   (T_OBS8_INT, obs[8]), (T_OBS4_INT, obs[4]), (T_OBS9_INT, obs[9])):
+        t |= bit if isinstance(v, int) else 0
+    return t
+
+
+@pytest.fixture(scope="module")
+def env():
+    import merging_gym
+
+    e = merging_gym.make("merging_env-v0").unwrapped
+    assert e.action_space.n == 5 and e.observation_space.shape[0] == 10
+    return e
+
+
+@pytest.mark.parametrize("trace", TRACES)
+def test_replay_reference_trace(env, golden, trace):
+    g = {k[len(trace) + 1:]: golden[k] for k in golden.files if k.startswith(trace + "_")}
+    flips = 0.0
+    for k in range(len(g["a1"])):
+        if g["reset"][k]:
+            obs, rew, done, coll = env.reset(), [0.0, 0.0], False, False
+            flips = 0.0
+        else:
+            a2 = int(g["a2"][k])
+            obs, rew, done, info = env.step(int(g["a1"][k]), None if a2 < 0 else a2)
+            coll = info["collision"]
+        assert isinstance(obs, list) and len(obs) == 10
+        if coll != bool(g["coll"][k]):
+            assert merge_zone(g["pos"][k][0], g["pos"][k][1]) and g["done"][k - 1], (trace, k)
+            flips += 10.0 if coll else -10.0
+            continue
+        assert bool(done) == bool(g["done"][k]), (trace, k)
+        assert (0 if env.winner is None else env.winner) == g["winner"][k], (trace, k)
+        assert _types(obs, rew) == g["types"][k], (trace, k)
+        np.testing.assert_allclose(np.asarray(obs, float), g["obs"][k], rtol=0, atol=1e-9)
+        np.testing.assert_allclose(np.asarray(rew, float), g["rew"][k], rtol=0, atol=1e-9)
+        np.testing.assert_allclose([env.state1["pos"], env.state2["pos"]], g["pos"][k], rtol=0, atol=1e-9)
+        np.testing.assert_allclose([env.state1["acc"], env.state2["acc"]], g["acc"][k], rtol=0, atol=1e-9)
+        np.testing.assert_allclose([env.r1_accumulate - flips, env.r2_accumulate - flips], g["racc"][k],
+                                   rtol=0, atol=1e-9)
+        assert env.time_stamp == g["time"][k]
+
+
+def test_assigned_state_reaches_the_device(env, golden):
+    """Assigning state1 / winner / time_stamp between steps (as the reference allows) is honoured."""
+    ts = [0.0]
+    for _ in range(2700):
+        ts.append(ts[-1] + 0.2)
+    zone = merge_zone(golden["one_p"][:, 0], golden["one_p"][:, 1])
+    for r in range(0, len(golden["one_a1"]), 13):
+        env.reset()
+        env.state1 = {"pos": float(golden["one_p"][r, 0]), "vel": float(golden["one_v"][r, 0]), "acc": 0.0}
+        env.state2 = {"pos": float(golden["one_p"][r, 1]), "vel": float(golden["one_v"][r, 1]), "acc": 0.0}
+        w = int(golden["one_winner"][r])
+        env.winner = None if w == 0 else w
+        env.done = bool(golden["one_done"][r])
+        env.time_stamp = ts[int(golden["one_k"][r])]
+        env.r1_accumulate, env.r2_accumulate = map(float, golden["one_racc"][r])
+        a2 = int(golden["one_a2"][r])
+        obs, rew, done, info = env.step(int(golden["one_a1"][r]), None if a2 < 0 else a2)
+        if info["collision"] != bool(golden["one_coll"][r]):
+            assert zone[r], r
+            continue
+        assert done == bool(golden["one_done_out"][r]), r
+        np.testing.assert_allclose(obs, golden["one_obs"][r], rtol=0, atol=1e-9)
+        np.testing.assert_allclose(rew, golden["one_rew"][r], rtol=0, atol=1e-9)
+        assert env.time_stamp == golden["one_time"][r]
+
+
+@pytest.mark.parametrize("bad", [(7, 2), (None, 2), (2, 9), (2.5, None), (2, -1)])
+def test_invalid_action_raises_like_reference(env, bad):
+    """KeyError from action_dict, after the clock (and the ego for a bad action2) advanced."""
+    ref = mo.PyMergeEnv()
+    env.reset()
+    for _ in range(3):
+        env.step(3, 1)
+        ref.step(3, 1)
+    with pytest.raises(KeyError):
+        ref.step(*bad)
+    with pytest.raises(KeyError):
+        env.step(*bad)
+    assert env.time_stamp == ref.time_stamp
+    assert env.done == ref.done
+    np.testing.assert_allclose([env.state1["pos"], env.state1["vel"]],
+                               [ref.state1["pos"], ref.state1["vel"]], rtol=0, atol=1e-9)
+    # the env keeps working afterwards, in step with the reference
+    o, r, d, i = env.step(4, 0)
+    ro, rr, rd, ri = ref.step(4, 0)
+    np.testing.assert_allclose(o, ro, rtol=0, atol=1e-9)
+
+
+def test_observe_and_is_collided(env):
+    ref = mo.PyMergeEnv()
+    env.reset()
+    for k in range(151):  # KAT A: constant speed ego vs L0 opponent collide at step 151
+        env.step(2)
+        ref.step(2)
+    assert env.is_collided() and ref.collided()
+    np.testing.assert_allclose(env.observe(), ref.observe(), rtol=0, atol=1e-9)
+
+
+def test_action_types_accepted_like_dict_lookup(env):
+    """action_dict[...] accepts anything equal and hash-equal to 0..4 (np.int64, 3.0, True)."""
+    env.reset()
+    ref = mo.PyMergeEnv()
+    for a1, a2 in [(np.int64(3), np.int8(1)), (3.0, True), (False, None)]:
+        o, r, d, i = env.step(a1, a2)
+        ro, rr, rd, ri = ref.step(int(a1), None if a2 is None else int(a2))
+        np.testing.assert_allclose(o, ro, rtol=0, atol=1e-9)

@@ -1,7 +1,14 @@
+# One GPU session: smoke -> GPU tests -> bench -> rocprof kernel stats -> PMC passes.
+# Every GPU step has its own time limit and the chain stops at the first failure.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
 mkdir -p gpurun_out
-echo "== smoke" && timeout -k 10 400 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && tail -3 gpurun_out/smoke.log \
-&& echo "== pytest gpu" && timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -30 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] \
-&& echo "== bench" && timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1 && tail -2 gpurun_out/bench.log \
-&& echo "== rocprof" && cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o r01 -- python bench.py --steps 300 --warmup 20 --no-cpu-baseline > gpurun_out/prof.log 2>&1 && tail -2 gpurun_out/prof.log
+TAG=${TAG:-r01}
+echo "== smoke" && timeout -k 10 400 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && tail -1 gpurun_out/smoke.log \
+&& echo "== pytest gpu" && { timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -5 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ]; } \
+&& echo "== bench" && timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1 && tail -1 gpurun_out/bench.log \
+&& echo "== rocprof stats" && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o $TAG -- python bench.py --steps 300 --warmup 20 --no-cpu-baseline > gpurun_out/prof.log 2>&1 && tail -1 gpurun_out/prof.log \
+&& echo "== pmc fetch" && timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o pmc -- python tools/profile_pmc.py > gpurun_out/pmc_fetch.log 2>&1 \
+&& echo "== pmc write" && timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o pmc -- python tools/profile_pmc.py > gpurun_out/pmc_write.log 2>&1 \
+&& echo "== bench 2^22" && timeout -k 10 300 python bench.py --envs 4194304 --steps 300 --no-cpu-baseline > gpurun_out/bench_4m.log 2>&1 && tail -1 gpurun_out/bench_4m.log

@@ -1,0 +1,70 @@
+"""Per-launch memory-side bytes from rocprofv3 PMC passes (FETCH_SIZE and WRITE_SIZE, separate runs).
+
+    python tools/pmc_summary.py FETCH_DIR WRITE_DIR --envs 1048576 4194304 8388608 [--out profiles/pmc_traffic.json]
+
+Dispatch order inside each env count is reset x reps, observe x reps, step x reps (tools/profile_pmc.py),
+so rows are grouped by kernel name and then split evenly over the env counts.
+Calibration (MI355X_MICROARCH.md "HBM": on gfx950 FETCH_SIZE under-reads wide streaming loads and
+other widths are uncalibrated): reset_kernel writes exactly 52 B/env, observe_kernel reads exactly
+32 B/env (obs written only); the step kernel's counters are divided by those ratios. Both
+counters see L2 -> fabric traffic, so Infinity Cache (MALL) hits are counted too.
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+from collections import defaultdict
+
+
+def load(d, counter):
+    paths = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    if not paths:
+        raise SystemExit(f"no counter_collection.csv under {d}")
+    per = defaultdict(list)  # kernel -> [(dispatch, value)]
+    for p in paths:
+        for r in csv.DictReader(open(p)):
+            if r.get("Counter_Name") != counter:
+                continue
+            name = r["Kernel_Name"]
+            key = "reset" if "reset_kernel" in name else "observe" if "observe_kernel" in name else \
+                "step" if "step_kernel" in name else None
+            if key:
+                per[key].append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
+    return {k: [v for _, v in sorted(vals)] for k, vals in per.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch_dir")
+    ap.add_argument("write_dir")
+    ap.add_argument("--envs", type=int, nargs="+", required=True)
+    ap.add_argument("--out")
+    a = ap.parse_args()
+    f = load(a.fetch_dir, "FETCH_SIZE")
+    w = load(a.write_dir, "WRITE_SIZE")
+    res = {}
+    for i, n in enumerate(a.envs):
+        def mean(tab, k):
+            v = tab[k]
+            per = len(v) // len(a.envs)
+            chunk = v[i * per:(i + 1) * per]
+            return 1024.0 * sum(chunk) / len(chunk)  # counters are in KiB
+        cal_w = mean(w, "reset") / (52.0 * n)
+        cal_r = mean(f, "observe") / (32.0 * n)
+        sf, sw = mean(f, "step"), mean(w, "step")
+        res[n] = {"envs": n, "fetch_raw_bytes": sf, "write_raw_bytes": sw,
+                  "read_calibration": cal_r, "write_calibration": cal_w,
+                  "fetch_bytes": sf / cal_r, "write_bytes": sw / cal_w,
+                  "hbm_bytes_per_launch": sf / cal_r + sw / cal_w,
+                  "algorithmic_bytes_per_launch": 156.0 * n,
+                  "ratio_to_algorithmic": (sf / cal_r + sw / cal_w) / (156.0 * n)}
+    print(json.dumps(res, indent=1))
+    if a.out:
+        first = res[a.envs[0]]
+        json.dump(dict(first, by_envs=res, source="rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, "
+                       "tools/profile_pmc.py + tools/pmc_summary.py"), open(a.out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
