@@ -46,6 +46,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="skip per-launch HIP events")
+    ap.add_argument("--rollout-steps", type=int, default=16,
+                    help="T of the fused rollout leg (mg_rollout_random); 0 disables it")
+    ap.add_argument("--rollout-launches", type=int, default=60)
     return ap.parse_args()
 
 
@@ -88,6 +91,45 @@ def load_pmc(envs: int):
     except (OSError, ValueError):
         pass
     return None
+
+
+def rollout_leg(env, args, world, dist, torch):
+    """The fused T-step kernel (mg_rollout_random): same per-step work and outputs, the env's
+    state read and written once per launch. Algorithmic bytes per env-step:
+    52 (obs 40 + rew 8 + done 1 + coll 1 + actions 2) + 104 / T (state in and out)."""
+    from merging_gym.profiling import KernelTimer
+
+    T, L, E = args.rollout_steps, args.rollout_launches, env.num_envs
+    k = 10_000_000
+    for _ in range(3):
+        env.rollout_random(T, args.seed, first_step=k, final_observation=False)
+        k += T
+    timer = KernelTimer(L)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for j in range(L):
+        timer.arm(j)
+        env.rollout_random(T, args.seed, first_step=k, final_observation=False)
+        k += T
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    durs = timer.durations_ms()
+    timer.close()
+    kernel_ms = sum(durs) / len(durs)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=env.device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    bytes_per_env_step = 52.0 + 104.0 / T
+    achieved = bytes_per_env_step * E * T / (kernel_ms * 1e-3) / 1e9
+    return {"kernel": "rollout_kernel", "steps_per_launch": T, "launches": L,
+            "value": world * E * T * L / float(t[0]), "unit": "env-steps/s",
+            "ms_per_step": float(t[0]) / (L * T) * 1e3, "kernel_ms_mean": kernel_ms,
+            "bytes_per_env_step": bytes_per_env_step, "achieved": achieved, "peak": HBM_PEAK_GBPS,
+            "unit_bw": "GB/s", "frac": achieved / HBM_PEAK_GBPS}
 
 
 def main():
@@ -159,6 +201,10 @@ def main():
     episodes = summarize(ret_sum, counts)
     episodes["allgather_ms"] = gather_ms
 
+    rollout = None
+    if args.rollout_steps > 0:
+        rollout = rollout_leg(env, args, world, dist, torch)
+
     total_env_steps = world * E * args.steps
     value = total_env_steps / elapsed
     if rank == 0:
@@ -188,6 +234,8 @@ def main():
                          "kernel_ms_mean": kernel_ms, "kernel_ms_mean_max_rank": kernel_ms_max},
             "episodes": episodes,
         }
+        if rollout is not None:
+            line["rollout"] = rollout
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         print(json.dumps(line), flush=True)

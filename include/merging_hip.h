@@ -16,6 +16,8 @@
  *   mg_reset        replaces MergeEnv.reset()                        merging_env.py:208-230
  *   mg_observe      replaces MergeEnv.observe() and is_collided()    merging_env.py:118-132,
  *                     :198-206 (no state change)
+ *   mg_rollout_random  T steps of mg_step_random in one launch (trajectory outputs); it
+ *                     replaces the callers' per-step collection loop (scripts/main.py:192-220)
  *   mg_abi_version, mg_last_error, mg_params_default, mg_time_next_launch: library plumbing
  *                     and profiling (no reference twin).
  *
@@ -125,6 +127,18 @@ typedef struct mg_outputs {
                            always, the ego too when only a2 is invalid; nothing else is written. */
 } mg_outputs;
 
+/* Trajectory buffers of mg_rollout_random: the outputs of step t for env i sit at row
+ * t * n + i. Any pointer may be NULL to skip that output. */
+typedef struct mg_traj {
+  float* obs;       /* [T, n, 10] fp32, 16-byte aligned (reset observation where autoreset fired) */
+  float* rew;       /* [T, n, 2] fp32 */
+  uint8_t* done;    /* [T, n] */
+  uint8_t* coll;    /* [T, n] */
+  int8_t* a1;       /* [T, n] actions drawn */
+  int8_t* a2;       /* [T, n] (-1 = None) */
+  float* final_obs; /* [T, n, 10] written only at rows whose env finished at that step */
+} mg_traj;
+
 /* Completed-episode statistics, updated only when an env finishes (MG_AUTORESET). */
 typedef struct mg_stats {
   double* ret_sum;   /* [n,2] sum of completed-episode returns (ego, opponent) */
@@ -134,7 +148,7 @@ typedef struct mg_stats {
 int mg_abi_version(void);
 const char* mg_last_error(void);
 
-/* Profiling hook: the next mg_step / mg_step_random launch made by the calling thread records
+/* Profiling hook: the next mg_step / mg_step_random / mg_rollout_random launch made by the calling thread records
  * start_event / stop_event (hipEvent_t created by the caller; either may be NULL) in its own
  * dispatch packet (hipExtLaunchKernel), so hipEventElapsedTime(start, stop) is the kernel's
  * duration without the launch gap. Consumed by that launch. Always returns 0. */
@@ -157,6 +171,16 @@ int mg_step_random(const mg_params* params, const mg_state* state, int8_t* a1_ou
                    int8_t* a2_out, const mg_outputs* out, const mg_stats* stats, int64_t n,
                    int64_t env_offset, uint64_t seed, uint64_t step_idx,
                    int32_t opponent_random, uint32_t flags, void* stream);
+
+/* num_steps consecutive steps with device-drawn actions in ONE launch: identical results to
+ * num_steps calls of mg_step_random with step_idx = first_step + t, output of step t written
+ * to slice t of *traj. Each env stays in registers for the whole launch, so its state is read
+ * and written once instead of once per step. Replaces the callers' collection loop around
+ * MergeEnv.step (scripts/main.py:192-220, scripts/hdqn.py:288-323) for a random policy. */
+int mg_rollout_random(const mg_params* params, const mg_state* state, const mg_traj* traj,
+                      const mg_stats* stats, int64_t n, int64_t env_offset, uint64_t seed,
+                      uint64_t first_step, int32_t num_steps, int32_t opponent_random,
+                      uint32_t flags, void* stream);
 
 /* Resets the envs whose mask byte is non-zero (mask == NULL: all n) and writes their reset
  * observation to out->obs / out->rec64 when given. Replaces MergeEnv.reset (merging_env.py:208-230). */

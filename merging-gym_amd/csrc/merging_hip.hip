@@ -120,6 +120,204 @@ __device__ __forceinline__ int action_from_u32(uint32_t u) {
 
 enum ActMode { kActArrays = 0, kActPhilox = 1 };
 
+// One env's state, held in registers for the duration of a launch.
+struct Env {
+  double p1, v1, p2, v2, ret1, ret2;
+  uint32_t steps, winner;
+  bool done;
+};
+
+__device__ __forceinline__ Env load_env(const mg_state& S, int64_t i) {
+  Env e;
+  e.p1 = S.p1[i];
+  e.v1 = S.v1[i];
+  e.p2 = S.p2[i];
+  e.v2 = S.v2[i];
+  e.ret1 = S.ret1[i];
+  e.ret2 = S.ret2[i];
+  const uint32_t tf = S.tf[i];
+  e.steps = tf & MG_TF_STEPS_MASK;
+  e.winner = (tf & MG_TF_WINNER_MASK) >> MG_TF_WINNER_SHIFT;
+  e.done = (tf & MG_TF_DONE) != 0;
+  return e;
+}
+
+__device__ __forceinline__ uint32_t pack_tf(const Env& e) {
+  return e.steps | (e.winner << MG_TF_WINNER_SHIFT) | (e.done ? MG_TF_DONE : 0u);
+}
+
+__device__ __forceinline__ void store_env(const mg_state& S, int64_t i, const Env& e) {
+  S.p1[i] = e.p1;
+  S.v1[i] = e.v1;
+  S.p2[i] = e.p2;
+  S.v2[i] = e.v2;
+  S.ret1[i] = e.ret1;
+  S.ret2[i] = e.ret2;
+  S.tf[i] = pack_tf(e);
+}
+
+// What one step returns besides the new state.
+struct StepOut {
+  double o[kObs];  // observation (the reset observation once autoreset has fired)
+  double r1, r2, acc1, acc2;
+  bool done, coll, r1_int, r2_int, v1_int, v2_int;
+  int bad;  // 1: action1 invalid, 2: action2 invalid (the reference's KeyError)
+};
+
+__device__ __forceinline__ void draw_actions(uint64_t gi, uint64_t step, uint64_t seed,
+                                             int opp_random, int& a1, int& a2) {
+  const uint4 u = philox4x32_10(
+      make_uint4(static_cast<uint32_t>(gi), static_cast<uint32_t>(gi >> 32),
+                 static_cast<uint32_t>(step), static_cast<uint32_t>(step >> 32)),
+      static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32));
+  a1 = action_from_u32(u.x);
+  a2 = opp_random ? action_from_u32(u.y) : MG_ACTION_NONE;
+}
+
+// MergeEnv.step (merging_env.py:138-195) for one env held in registers.
+__device__ __forceinline__ void env_step(const mg_params& P, Env& e, int a1, int a2, StepOut& r) {
+  // time_stamp += dT; done if time_stamp > 500 (:141-143). The fp64 clock first exceeds 500
+  // on step 2501; an integer count reproduces that exactly.
+  e.steps = e.steps < MG_TF_STEPS_MASK ? e.steps + 1 : e.steps;
+  if (static_cast<int32_t>(e.steps) >= P.timeout_steps) e.done = true;
+
+  const bool bad1 = !valid_action(a1);
+  const bool bad2 = !(a2 == MG_ACTION_NONE || valid_action(a2));
+  r.bad = (bad1 ? 1 : 0) | (bad2 ? 2 : 0);
+  r.acc1 = r.acc2 = 0.0;
+  r.v1_int = r.v2_int = false;
+  r.done = r.coll = r.r1_int = r.r2_int = false;
+  r.r1 = r.r2 = 0.0;
+  if (!bad1) {
+    // mpc_1d (helper.py:152-191): min u'(D'D + 0.01 I)u s.t. sum(dt u) = vt - v0 (the only
+    // row of the constraint passed to solve_qp, :172-173, :182). D.1 = 0, so P.1 = 0.01 * 1
+    // and the minimiser is u = (vt - v0) / t * 1; action() = u[0].
+    r.acc1 = (P.action_speed[a1] - e.v1) / P.prediction_t;
+    const double nv = e.v1 + r.acc1 * P.dT;  // max(0, v + acc*dT)  :149
+    r.v1_int = !(nv > 0.0);
+    e.v1 = r.v1_int ? 0.0 : nv;
+    e.p1 = e.p1 + e.v1 * P.dT;  // :150
+  }
+  if (r.bad) {  // the reference raises KeyError at action_dict[...] after advancing this far
+#pragma unroll
+    for (int k = 0; k < kObs; ++k) r.o[k] = 0.0;
+    return;
+  }
+  // action2 None -> acc 0 (:152): the "L0" constant-speed opponent
+  if (a2 != MG_ACTION_NONE) r.acc2 = (P.action_speed[a2] - e.v2) / P.prediction_t;
+  const double nv2 = e.v2 + r.acc2 * P.dT;  // :153
+  r.v2_int = !(nv2 > 0.0);
+  e.v2 = r.v2_int ? 0.0 : nv2;
+  e.p2 = e.p2 + e.v2 * P.dT;  // :154
+
+  double x1, y1, x2, y2;
+  lon2coord(P, e.p1, true, x1, y1);
+  lon2coord(P, e.p2, false, x2, y2);
+  observe(P, e.p1, e.v1, e.p2, e.v2, x1, y1, x2, y2, r.o);
+
+  // rewards (:158-159): -time_penalty - vel_penalty * |v - 20|
+  double r1 = (0.0 - P.time_penalty) - P.vel_penalty * fabs(e.v1 - P.vel_ref);
+  double r2 = (0.0 - P.time_penalty) - P.vel_penalty * fabs(e.v2 - P.vel_ref);
+
+  // arrival / winner state machine (:163-181); ego strict '>', opponent '>='
+  if (e.p1 > P.end_point) {
+    if (e.winner == 0) {
+      e.winner = 1;
+      r1 += P.r_first;
+    } else if (e.winner == 1) {
+      r1 = 0.0;
+      r.r1_int = true;
+    } else {
+      r1 += P.r_second;
+      e.done = true;
+    }
+  }
+  if (e.p2 >= P.end_point) {
+    if (e.winner == 0) {
+      e.winner = 2;
+      r2 += P.r_first;
+    } else if (e.winner == 2) {
+      r2 = 0.0;
+      r.r2_int = true;
+    } else {
+      r2 += P.r_second;
+      e.done = true;
+    }
+  }
+
+  // is_collided (:183-187, :198-206)
+  r.coll = boxes_intersect(vehicle_box(P, y1, x1), vehicle_box(P, y2, x2));
+  if (r.coll) {
+    e.done = true;
+    r1 += P.r_collision;
+    r2 += P.r_collision;
+  }
+  e.ret1 += r1;  // :191-192
+  e.ret2 += r2;
+  r.r1 = r1;
+  r.r2 = r2;
+  r.done = e.done;
+}
+
+// gym.vector autoreset: record the finished episode, keep its terminal observation, reset
+// the env (merging_env.py:208-230) and put the reset observation in r.o.
+__device__ __forceinline__ void finish_episode(const mg_params& P, Env& e, StepOut& r,
+                                               const mg_stats& St, float* final_obs_row,
+                                               int64_t i) {
+  if (St.ret_sum) {
+    St.ret_sum[2 * i] += e.ret1;
+    St.ret_sum[2 * i + 1] += e.ret2;
+  }
+  if (St.counts) {
+    uint4* c = reinterpret_cast<uint4*>(St.counts) + i;
+    uint4 cv = *c;
+    cv.x += 1;
+    cv.y += r.coll ? 1u : 0u;
+    cv.z += e.winner == 1 ? 1u : 0u;
+    cv.w += e.steps;
+    *c = cv;
+  }
+  if (final_obs_row) {
+#pragma unroll
+    for (int k = 0; k < kObs; ++k) final_obs_row[k] = static_cast<float>(r.o[k]);
+  }
+  e.p1 = e.p2 = P.start_point;
+  e.v1 = e.v2 = P.start_vel;
+  e.ret1 = e.ret2 = 0.0;
+  e.steps = 0;
+  e.winner = 0;
+  e.done = false;
+  reset_obs(P, r.o);
+}
+
+// Write a block's [rows,10] fp32 observation tile through LDS as contiguous 16-byte stores
+// (a wave's 64 rows of 40 B become 160 dwordx4 lanes instead of 640 scattered dwords).
+// Every thread of the block must call it (two barriers).
+__device__ __forceinline__ void store_obs_tile(float* tile, const double (&o)[kObs], float* dst,
+                                               int nrows) {
+  const int tid = threadIdx.x;
+  float2* t2 = reinterpret_cast<float2*>(tile + tid * kObs);
+#pragma unroll
+  for (int k = 0; k < kObs / 2; ++k)
+    t2[k] = make_float2(static_cast<float>(o[2 * k]), static_cast<float>(o[2 * k + 1]));
+  __syncthreads();
+  const int nfl = nrows * kObs;
+  if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+    const int n4 = nfl >> 2;
+    float4* d4 = reinterpret_cast<float4*>(dst);
+    const float4* s4 = reinterpret_cast<const float4*>(tile);
+    for (int j = tid; j < n4; j += kBlock) d4[j] = s4[j];
+    const int tail = nfl - (n4 << 2);  // 0 or 2
+    if (tid < tail) dst[(n4 << 2) + tid] = tile[(n4 << 2) + tid];
+  } else {  // rows are 8-byte aligned whenever the buffer is
+    const int n2 = nfl >> 1;
+    float2* d2 = reinterpret_cast<float2*>(dst);
+    const float2* s2 = reinterpret_cast<const float2*>(tile);
+    for (int j = tid; j < n2; j += kBlock) d2[j] = s2[j];
+  }
+  __syncthreads();
+}
+
 struct Launch {
   mg_params P;
   mg_state S;
@@ -147,216 +345,119 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const Launch L) {
   const int64_t base = static_cast<int64_t>(blockIdx.x) * kBlock;
   const int64_t i = base + tid;
   const bool live = i < L.n;
-
-  bool done = false;
-  bool coll = false;
-  double o[kObs];
+  StepOut r;
+  r.done = false;
 
   if (live) {
-    // ---- actions ----
     int a1, a2;
     if constexpr (ACT == kActPhilox) {
-      const uint64_t gi = static_cast<uint64_t>(L.env_offset + i);  // shard-invariant stream
-      const uint4 u = philox4x32_10(
-          make_uint4(static_cast<uint32_t>(gi), static_cast<uint32_t>(gi >> 32),
-                     static_cast<uint32_t>(L.step_idx), static_cast<uint32_t>(L.step_idx >> 32)),
-          static_cast<uint32_t>(L.seed), static_cast<uint32_t>(L.seed >> 32));
-      a1 = action_from_u32(u.x);
-      a2 = L.opp_random ? action_from_u32(u.y) : MG_ACTION_NONE;
+      draw_actions(static_cast<uint64_t>(L.env_offset + i), L.step_idx, L.seed, L.opp_random, a1, a2);
       if (L.a1_out) L.a1_out[i] = static_cast<int8_t>(a1);
       if (L.a2_out) L.a2_out[i] = static_cast<int8_t>(a2);
     } else {
       a1 = L.a1[i];
       a2 = L.a2 ? static_cast<int>(L.a2[i]) : MG_ACTION_NONE;
     }
-
-    // ---- load state (coalesced SoA) ----
-    double p1 = L.S.p1[i], v1 = L.S.v1[i], p2 = L.S.p2[i], v2 = L.S.v2[i];
-    double ret1 = L.S.ret1[i], ret2 = L.S.ret2[i];
-    const uint32_t tf = L.S.tf[i];
-    uint32_t steps = tf & MG_TF_STEPS_MASK;
-    uint32_t winner = (tf & MG_TF_WINNER_MASK) >> MG_TF_WINNER_SHIFT;
-    done = (tf & MG_TF_DONE) != 0;
-
-    // time_stamp += dT; done if time_stamp > 500 (merging_env.py:141-143). The fp64 clock
-    // first exceeds 500 on step 2501; an integer count reproduces that exactly.
-    steps = steps < MG_TF_STEPS_MASK ? steps + 1 : steps;
-    if (static_cast<int32_t>(steps) >= P.timeout_steps) done = true;
-
-    const bool bad1 = !valid_action(a1);
-    const bool bad2 = !(a2 == MG_ACTION_NONE || valid_action(a2));
-    double acc1 = 0.0, acc2 = 0.0;
-    bool v1_int = false, v2_int = false;
-
-    if (!bad1) {
-      // mpc_1d (helper.py:152-191): min u'(D'D + 0.01 I)u s.t. sum(dt u) = vt - v0 (the
-      // only row of the constraint passed to solve_qp, :172-173, :182). D.1 = 0, so
-      // P.1 = 0.01 * 1 and the minimiser is u = (vt - v0) / t * 1; action() = u[0].
-      const double vt1 = P.action_speed[a1];
-      acc1 = (vt1 - v1) / P.prediction_t;
-      const double nv1 = v1 + acc1 * P.dT;  // max(0, v + acc*dT)  :149
-      v1_int = !(nv1 > 0.0);
-      v1 = v1_int ? 0.0 : nv1;
-      p1 = p1 + v1 * P.dT;  // :150
-    }
-    if (!bad1 && !bad2) {
-      // action2 None -> acc 0 (:152): the "L0" constant-speed opponent
-      if (a2 != MG_ACTION_NONE) acc2 = (P.action_speed[a2] - v2) / P.prediction_t;
-      const double nv2 = v2 + acc2 * P.dT;  // :153
-      v2_int = !(nv2 > 0.0);
-      v2 = v2_int ? 0.0 : nv2;
-      p2 = p2 + v2 * P.dT;  // :154
-    }
-
-    if (bad1 || bad2) {
-      // The reference raises KeyError at action_dict[...] after advancing this far.
-      if (L.O.error) atomicOr(L.O.error, (bad1 ? 1 : 0) | (bad2 ? 2 : 0));
-      L.S.tf[i] = steps | (winner << MG_TF_WINNER_SHIFT) | (done ? MG_TF_DONE : 0u);
-      if (!bad1) {
-        L.S.p1[i] = p1;
-        L.S.v1[i] = v1;
-      }
-      done = false;
-#pragma unroll
-      for (int k = 0; k < kObs; ++k) o[k] = 0.0;
+    Env e = load_env(L.S, i);
+    env_step(P, e, a1, a2, r);
+    if (r.bad) {
+      if (L.O.error) atomicOr(L.O.error, r.bad);
+      store_env(L.S, i, e);  // clock (and the ego for a bad action2) advanced, nothing else
     } else {
-      double x1, y1, x2, y2;
-      lon2coord(P, p1, true, x1, y1);
-      lon2coord(P, p2, false, x2, y2);
-      observe(P, p1, v1, p2, v2, x1, y1, x2, y2, o);
-
-      // rewards (:158-159): -time_penalty - vel_penalty * |v - 20|
-      double r1 = (0.0 - P.time_penalty) - P.vel_penalty * fabs(v1 - P.vel_ref);
-      double r2 = (0.0 - P.time_penalty) - P.vel_penalty * fabs(v2 - P.vel_ref);
-      bool r1_int = false, r2_int = false;
-
-      // arrival / winner state machine (:163-181); ego strict '>', opponent '>='
-      if (p1 > P.end_point) {
-        if (winner == 0) {
-          winner = 1;
-          r1 += P.r_first;
-        } else if (winner == 1) {
-          r1 = 0.0;
-          r1_int = true;
-        } else {
-          r1 += P.r_second;
-          done = true;
-        }
-      }
-      if (p2 >= P.end_point) {
-        if (winner == 0) {
-          winner = 2;
-          r2 += P.r_first;
-        } else if (winner == 2) {
-          r2 = 0.0;
-          r2_int = true;
-        } else {
-          r2 += P.r_second;
-          done = true;
-        }
-      }
-
-      // is_collided (:183-187, :198-206)
-      coll = boxes_intersect(vehicle_box(P, y1, x1), vehicle_box(P, y2, x2));
-      if (coll) {
-        done = true;
-        r1 += P.r_collision;
-        r2 += P.r_collision;
-      }
-      ret1 += r1;  // :191-192
-      ret2 += r2;
-
       if constexpr (OUT64) {
         mg_rec64* rec = L.O.rec64 + i;
 #pragma unroll
-        for (int k = 0; k < kObs; ++k) rec->obs[k] = o[k];
-        rec->rew[0] = r1;
-        rec->rew[1] = r2;
-        rec->acc[0] = acc1;
-        rec->acc[1] = acc2;
-        rec->pos[0] = p1;
-        rec->pos[1] = p2;
-        rec->vel[0] = v1;
-        rec->vel[1] = v2;
-        rec->ret[0] = ret1;
-        rec->ret[1] = ret2;
-        rec->tf = steps | (winner << MG_TF_WINNER_SHIFT) | (done ? MG_TF_DONE : 0u);
-        rec->status = (done ? MG_ST_DONE : 0u) | (coll ? MG_ST_COLLISION : 0u) |
-                      (r1_int ? MG_ST_R1_INT : 0u) | (r2_int ? MG_ST_R2_INT : 0u) |
-                      (v1_int ? MG_ST_V1_INT : 0u) | (v2_int ? MG_ST_V2_INT : 0u);
-      } else {
-        if (L.O.rew) {
-          reinterpret_cast<float2*>(L.O.rew)[i] =
-              make_float2(static_cast<float>(r1), static_cast<float>(r2));
-        }
+        for (int k = 0; k < kObs; ++k) rec->obs[k] = r.o[k];
+        rec->rew[0] = r.r1;
+        rec->rew[1] = r.r2;
+        rec->acc[0] = r.acc1;
+        rec->acc[1] = r.acc2;
+        rec->pos[0] = e.p1;
+        rec->pos[1] = e.p2;
+        rec->vel[0] = e.v1;
+        rec->vel[1] = e.v2;
+        rec->ret[0] = e.ret1;
+        rec->ret[1] = e.ret2;
+        rec->tf = pack_tf(e);
+        rec->status = (r.done ? MG_ST_DONE : 0u) | (r.coll ? MG_ST_COLLISION : 0u) |
+                      (r.r1_int ? MG_ST_R1_INT : 0u) | (r.r2_int ? MG_ST_R2_INT : 0u) |
+                      (r.v1_int ? MG_ST_V1_INT : 0u) | (r.v2_int ? MG_ST_V2_INT : 0u);
+      } else if (L.O.rew) {
+        reinterpret_cast<float2*>(L.O.rew)[i] =
+            make_float2(static_cast<float>(r.r1), static_cast<float>(r.r2));
       }
-      if (L.O.done) L.O.done[i] = done ? 1 : 0;
-      if (L.O.coll) L.O.coll[i] = coll ? 1 : 0;
-
-      if ((L.flags & MG_AUTORESET) && done) {
-        // gym.vector autoreset: record the finished episode, then reset (merging_env.py:208-230)
-        if (L.St.ret_sum) {
-          L.St.ret_sum[2 * i] += ret1;
-          L.St.ret_sum[2 * i + 1] += ret2;
-        }
-        if (L.St.counts) {
-          uint4* c = reinterpret_cast<uint4*>(L.St.counts) + i;
-          uint4 cv = *c;
-          cv.x += 1;
-          cv.y += coll ? 1u : 0u;
-          cv.z += winner == 1 ? 1u : 0u;
-          cv.w += steps;
-          *c = cv;
-        }
-        if (L.O.final_obs) {
-#pragma unroll
-          for (int k = 0; k < kObs; ++k) L.O.final_obs[i * kObs + k] = static_cast<float>(o[k]);
-        }
-        p1 = p2 = P.start_point;
-        v1 = v2 = P.start_vel;
-        ret1 = ret2 = 0.0;
-        steps = 0;
-        winner = 0;
-        reset_obs(P, o);
-      }
-
-      L.S.p1[i] = p1;
-      L.S.v1[i] = v1;
-      L.S.p2[i] = p2;
-      L.S.v2[i] = v2;
-      L.S.ret1[i] = ret1;
-      L.S.ret2[i] = ret2;
-      const bool still_done = done && !(L.flags & MG_AUTORESET);
-      L.S.tf[i] = steps | (winner << MG_TF_WINNER_SHIFT) | (still_done ? MG_TF_DONE : 0u);
+      if (L.O.done) L.O.done[i] = r.done ? 1 : 0;
+      if (L.O.coll) L.O.coll[i] = r.coll ? 1 : 0;
+      if ((L.flags & MG_AUTORESET) && r.done)
+        finish_episode(P, e, r, L.St, L.O.final_obs ? L.O.final_obs + i * kObs : nullptr, i);
+      store_env(L.S, i, e);
     }
   }
 
   if (L.O.done_mask) {
-    const uint64_t m = __ballot(live && done);
-    if ((tid & 63) == 0 && base + tid < L.n) L.O.done_mask[(base + tid) >> 6] = m;
+    const uint64_t m = __ballot(live && r.done);
+    if ((tid & 63) == 0 && live) L.O.done_mask[i >> 6] = m;
   }
-
   if constexpr (!OUT64) {
     if (L.O.obs) {
-      // Stage the block's [256,10] fp32 tile in LDS, then write it out as contiguous 16-B
-      // stores: a wave's 64 rows of 40 B become 160 full dwordx4 lanes instead of 640
-      // scattered dwords.
-      float2* t2 = reinterpret_cast<float2*>(obs_tile + tid * kObs);
-#pragma unroll
-      for (int k = 0; k < kObs / 2; ++k)
-        t2[k] = make_float2(static_cast<float>(o[2 * k]), static_cast<float>(o[2 * k + 1]));
-      __syncthreads();
       const int64_t rem = L.n - base;
-      const int nrows = rem < kBlock ? static_cast<int>(rem) : kBlock;
-      const int nfl = nrows * kObs;
-      const int n4 = nfl >> 2;
-      float4* dst4 = reinterpret_cast<float4*>(L.O.obs + base * kObs);
-      const float4* src4 = reinterpret_cast<const float4*>(obs_tile);
-      for (int j = tid; j < n4; j += kBlock) dst4[j] = src4[j];
-      const int tail = nfl - (n4 << 2);  // 0 or 2
-      if (tid < tail) L.O.obs[base * kObs + (n4 << 2) + tid] = obs_tile[(n4 << 2) + tid];
+      store_obs_tile(obs_tile, r.o, L.O.obs + base * kObs, rem < kBlock ? static_cast<int>(rem) : kBlock);
     }
   }
+}
+
+struct Rollout {
+  mg_params P;
+  mg_state S;
+  mg_traj T;
+  mg_stats St;
+  uint64_t seed;
+  uint64_t first_step;
+  int64_t env_offset;
+  int64_t n;
+  int32_t num_steps;
+  int32_t opp_random;
+  uint32_t flags;
+};
+
+// num_steps consecutive mg_step_random steps with the env kept in registers: the state is
+// read once and written once per launch; step t's outputs go to slice t of the trajectory.
+__global__ __launch_bounds__(kBlock) void rollout_kernel(const Rollout R) {
+  __shared__ __attribute__((aligned(16))) float obs_tile[kBlock * kObs];
+
+  const mg_params& P = R.P;
+  const int tid = threadIdx.x;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kBlock;
+  const int64_t i = base + tid;
+  const bool live = i < R.n;
+  const int64_t rem = R.n - base;
+  const int nrows = rem < kBlock ? static_cast<int>(rem) : kBlock;
+  const bool autoreset = (R.flags & MG_AUTORESET) != 0;
+
+  Env e;
+  if (live) e = load_env(R.S, i);
+  StepOut r;
+  for (int t = 0; t < R.num_steps; ++t) {
+    const int64_t row = static_cast<int64_t>(t) * R.n + i;
+    if (live) {
+      int a1, a2;
+      draw_actions(static_cast<uint64_t>(R.env_offset + i), R.first_step + t, R.seed, R.opp_random,
+                   a1, a2);
+      env_step(P, e, a1, a2, r);  // Philox actions are always valid
+      if (R.T.a1) R.T.a1[row] = static_cast<int8_t>(a1);
+      if (R.T.a2) R.T.a2[row] = static_cast<int8_t>(a2);
+      if (R.T.rew)
+        reinterpret_cast<float2*>(R.T.rew)[row] =
+            make_float2(static_cast<float>(r.r1), static_cast<float>(r.r2));
+      if (R.T.done) R.T.done[row] = r.done ? 1 : 0;
+      if (R.T.coll) R.T.coll[row] = r.coll ? 1 : 0;
+      if (autoreset && r.done)
+        finish_episode(P, e, r, R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i);
+    }
+    if (R.T.obs)
+      store_obs_tile(obs_tile, r.o, R.T.obs + (static_cast<int64_t>(t) * R.n + base) * kObs, nrows);
+  }
+  if (live) store_env(R.S, i, e);
 }
 
 __global__ __launch_bounds__(kBlock) void reset_kernel(const mg_params P, const mg_state S,
@@ -474,6 +575,17 @@ int launch_step(const Launch& L, hipStream_t stream, const char* what) {
   return finish_launch(what);
 }
 
+int launch_rollout(const Rollout& R, hipStream_t stream) {
+  const unsigned blocks = static_cast<unsigned>((R.n + kBlock - 1) / kBlock);
+  hipEvent_t start = g_ev_start, stop = g_ev_stop;
+  g_ev_start = g_ev_stop = nullptr;
+  if (start || stop)
+    hipExtLaunchKernelGGL(rollout_kernel, dim3(blocks), dim3(kBlock), 0, stream, start, stop, 0, R);
+  else
+    hipLaunchKernelGGL(rollout_kernel, dim3(blocks), dim3(kBlock), 0, stream, R);
+  return finish_launch("mg_rollout_random");
+}
+
 }  // namespace
 
 extern "C" {
@@ -551,6 +663,34 @@ int mg_step_random(const mg_params* params, const mg_state* state, int8_t* a1_ou
   L.n = n;
   L.flags = flags;
   return launch_step<kActPhilox>(L, static_cast<hipStream_t>(stream), "mg_step_random");
+}
+
+int mg_rollout_random(const mg_params* params, const mg_state* state, const mg_traj* traj,
+                      const mg_stats* stats, int64_t n, int64_t env_offset, uint64_t seed,
+                      uint64_t first_step, int32_t num_steps, int32_t opponent_random,
+                      uint32_t flags, void* stream) {
+  mg_outputs none{};
+  if (int e = check_common(params, state, &none, n)) return e;
+  if (!traj) return fail(hipErrorInvalidValue, "%s", "traj is NULL (pass a zeroed mg_traj)");
+  if (num_steps < 0) return fail(hipErrorInvalidValue, "%s", "num_steps < 0");
+  if ((traj->obs && (reinterpret_cast<uintptr_t>(traj->obs) & 15)) ||
+      (traj->final_obs && (reinterpret_cast<uintptr_t>(traj->final_obs) & 7)) ||
+      (traj->rew && (reinterpret_cast<uintptr_t>(traj->rew) & 7)))
+    return fail(hipErrorInvalidValue, "%s", "traj.obs must be 16-byte, rew/final_obs 8-byte aligned");
+  if (n == 0 || num_steps == 0) return 0;
+  Rollout R{};
+  R.P = *params;
+  R.S = *state;
+  R.T = *traj;
+  if (stats) R.St = *stats;
+  R.seed = seed;
+  R.first_step = first_step;
+  R.env_offset = env_offset;
+  R.n = n;
+  R.num_steps = num_steps;
+  R.opp_random = opponent_random;
+  R.flags = flags;
+  return launch_rollout(R, static_cast<hipStream_t>(stream));
 }
 
 int mg_reset(const mg_params* params, const mg_state* state, const uint8_t* mask,

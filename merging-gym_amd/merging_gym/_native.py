@@ -52,6 +52,10 @@ class Outputs(_c.Structure):
                                   "rec64", "error")]
 
 
+class Traj(_c.Structure):
+    _fields_ = [(n, _P) for n in ("obs", "rew", "done", "coll", "a1", "a2", "final_obs")]
+
+
 class Stats(_c.Structure):
     _fields_ = [("ret_sum", _P), ("counts", _P)]
 
@@ -87,8 +91,11 @@ def _load():
                                    _c.c_uint64, _c.c_uint64, _c.c_int32, _c.c_uint32, _P]
     lib.mg_reset.argtypes = [PP, SP, _P, OP, _c.c_int64, _P]
     lib.mg_observe.argtypes = [PP, SP, OP, _c.c_int64, _P]
+    lib.mg_rollout_random.argtypes = [PP, SP, _c.POINTER(Traj), STP, _c.c_int64, _c.c_int64,
+                                      _c.c_uint64, _c.c_uint64, _c.c_int32, _c.c_int32, _c.c_uint32, _P]
     lib.mg_time_next_launch.argtypes = [_P, _P]
-    for f in (lib.mg_step, lib.mg_step_random, lib.mg_reset, lib.mg_observe, lib.mg_time_next_launch):
+    for f in (lib.mg_step, lib.mg_step_random, lib.mg_reset, lib.mg_observe, lib.mg_rollout_random,
+              lib.mg_time_next_launch):
         f.restype = _c.c_int
     v = lib.mg_abi_version()
     if v != ABI_VERSION:

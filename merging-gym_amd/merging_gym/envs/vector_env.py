@@ -84,6 +84,15 @@ class MergeVecEnv:
         self._stats = _native.Stats(ptr(self.ret_sum), ptr(self.counts))
         self._flags = _native.AUTORESET if self.autoreset else 0
         self._step_idx = 0
+        # pre-bound call arguments: a step costs one ctypes call and no allocations
+        self._p_ref, self._s_ref = ctypes.byref(self.params), ctypes.byref(self._state)
+        self._o_ref, self._st_ref = ctypes.byref(self._out), ctypes.byref(self._stats)
+        self._a1_ptr, self._a2_ptr = self.a1_buf.data_ptr(), self.a2_buf.data_ptr()
+        self._raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+        info = {"collision": self.coll.view(torch.bool)}
+        if self.final_obs is not None and self.autoreset:
+            info["final_observation"] = self.final_obs
+        self._result = (self.obs, self.rew, self.done.view(torch.bool), info)
 
         self.single_observation_space = spaces.observation_space()
         self.single_action_space = spaces.action_space()
@@ -93,7 +102,10 @@ class MergeVecEnv:
 
     # ------------------------------------------------------------------ helpers
     def _stream(self):
-        return ctypes.c_void_p(self._torch.cuda.current_stream(self.device).cuda_stream)
+        """Raw handle of torch's current stream on this device (honours `torch.cuda.stream(...)`)."""
+        if self._raw_stream is not None:
+            return self._raw_stream(self.device.index)
+        return self._torch.cuda.current_stream(self.device).cuda_stream
 
     def _actions(self, a, buf, allow_none: bool):
         torch = self._torch
@@ -119,10 +131,7 @@ class MergeVecEnv:
         return buf
 
     def _outputs(self):
-        info = {"collision": self.coll.view(self._torch.bool)}
-        if self.final_obs is not None and self.autoreset:
-            info["final_observation"] = self.final_obs
-        return self.obs, self.rew, self.done.view(self._torch.bool), info
+        return self._result
 
     # ------------------------------------------------------------------ gym API
     def reset(self, mask=None):
@@ -135,7 +144,8 @@ class MergeVecEnv:
             m = ctypes.c_void_p(mt.data_ptr())
         out = self._nat.Outputs(self._out.obs, None, None, None, None, None, None, None)
         self._nat.check(self._nat.lib.mg_reset(ctypes.byref(self.params), ctypes.byref(self._state),
-                                               m, ctypes.byref(out), self.num_envs, self._stream()),
+                                               m, ctypes.byref(out), self.num_envs,
+                                               ctypes.c_void_p(self._stream())),
                         "mg_reset")
         if mask is None:
             self.done.zero_()
@@ -148,9 +158,8 @@ class MergeVecEnv:
         a1 = self._actions(actions1, self.a1_buf, allow_none=False)
         a2 = self._actions(actions2, self.a2_buf, allow_none=True)
         rc = self._nat.lib.mg_step(
-            ctypes.byref(self.params), ctypes.byref(self._state), ctypes.c_void_p(a1.data_ptr()),
-            None if a2 is None else ctypes.c_void_p(a2.data_ptr()), ctypes.byref(self._out),
-            ctypes.byref(self._stats), self.num_envs, self._flags, self._stream())
+            self._p_ref, self._s_ref, a1.data_ptr(), None if a2 is None else a2.data_ptr(),
+            self._o_ref, self._st_ref, self.num_envs, self._flags, self._stream())
         self._nat.check(rc, "mg_step")
         return self._outputs()
 
@@ -160,21 +169,57 @@ class MergeVecEnv:
         (global env index, step index)). The actions used land in self.a1_buf / a2_buf."""
         k = self._step_idx if step_idx is None else int(step_idx)
         rc = self._nat.lib.mg_step_random(
-            ctypes.byref(self.params), ctypes.byref(self._state),
-            ctypes.c_void_p(self.a1_buf.data_ptr()) if record_actions else None,
-            ctypes.c_void_p(self.a2_buf.data_ptr()) if record_actions else None,
-            ctypes.byref(self._out), ctypes.byref(self._stats), self.num_envs, self.env_offset,
-            int(seed) & 0xFFFFFFFFFFFFFFFF, k & 0xFFFFFFFFFFFFFFFF, int(bool(opponent_random)),
-            self._flags, self._stream())
+            self._p_ref, self._s_ref, self._a1_ptr if record_actions else None,
+            self._a2_ptr if record_actions else None, self._o_ref, self._st_ref, self.num_envs,
+            self.env_offset, seed & 0xFFFFFFFFFFFFFFFF, k & 0xFFFFFFFFFFFFFFFF,
+            1 if opponent_random else 0, self._flags, self._stream())
         self._nat.check(rc, "mg_step_random")
         self._step_idx = k + 1
         return self._outputs()
+
+    def rollout_random(self, num_steps: int, seed: int, opponent_random: bool = True,
+                       first_step=None, final_observation: bool = True):
+        """`num_steps` steps with device-drawn actions in ONE kernel launch (the env stays in
+        registers; its state is read and written once). Bit-identical to `num_steps` calls of
+        step_random(seed, step_idx=first_step + t). Returns a dict of [T, N, ...] tensors:
+        obs, rew, done (bool), collision (bool), a1, a2 and final_observation (rows where
+        done). The buffers are reused by the next rollout of the same length."""
+        torch, nat = self._torch, self._nat
+        T, n = int(num_steps), self.num_envs
+        k0 = self._step_idx if first_step is None else int(first_step)
+        buf = getattr(self, "_traj_bufs", None)
+        if buf is None or buf["T"] != T or (buf["final_observation"] is None) == final_observation:
+            dev = self.device
+            buf = {"T": T,
+                   "obs": torch.empty((T, n, _OBS_DIM), dtype=torch.float32, device=dev),
+                   "rew": torch.empty((T, n, 2), dtype=torch.float32, device=dev),
+                   "done": torch.empty((T, n), dtype=torch.uint8, device=dev),
+                   "collision": torch.empty((T, n), dtype=torch.uint8, device=dev),
+                   "a1": torch.empty((T, n), dtype=torch.int8, device=dev),
+                   "a2": torch.empty((T, n), dtype=torch.int8, device=dev),
+                   "final_observation": (torch.full((T, n, _OBS_DIM), float("nan"), dtype=torch.float32,
+                                                    device=dev) if final_observation else None)}
+            ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+            buf["_traj"] = nat.Traj(*(ptr(buf[k]) for k in ("obs", "rew", "done", "collision", "a1", "a2",
+                                                             "final_observation")))
+            buf["_result"] = {"obs": buf["obs"], "rew": buf["rew"], "done": buf["done"].view(torch.bool),
+                              "collision": buf["collision"].view(torch.bool), "a1": buf["a1"],
+                              "a2": buf["a2"], "final_observation": buf["final_observation"]}
+            self._traj_bufs = buf
+        rc = nat.lib.mg_rollout_random(
+            self._p_ref, self._s_ref, ctypes.byref(buf["_traj"]), self._st_ref, n, self.env_offset,
+            seed & 0xFFFFFFFFFFFFFFFF, k0 & 0xFFFFFFFFFFFFFFFF, T, 1 if opponent_random else 0,
+            self._flags, self._stream())
+        nat.check(rc, "mg_rollout_random")
+        self._step_idx = k0 + T
+        return buf["_result"]
 
     def observe(self):
         """Observation of the current state without stepping (merging_env.py:118-132)."""
         out = self._nat.Outputs(self._out.obs, None, None, self._out.coll, None, None, None, None)
         self._nat.check(self._nat.lib.mg_observe(ctypes.byref(self.params), ctypes.byref(self._state),
-                                                 ctypes.byref(out), self.num_envs, self._stream()),
+                                                 ctypes.byref(out), self.num_envs,
+                                                 ctypes.c_void_p(self._stream())),
                         "mg_observe")
         return self.obs
 

@@ -260,3 +260,30 @@ def test_native_errors_are_raised(torch):
     rc = _native.lib.mg_step(ctypes.byref(_native.default_params()), ctypes.byref(st), None, None,
                              ctypes.byref(out), None, 16, 0, None)
     assert rc != 0 and b"NULL" in _native.lib.mg_last_error()
+
+
+@pytest.mark.parametrize("n,T", [(4096, 37), (3001, 64), (1, 5)])
+def test_rollout_equals_step_sequence(torch, n, T):
+    """mg_rollout_random (env in registers for T steps) is bit-identical to T launches of
+    mg_step_random, including autoreset, final observations and episode statistics."""
+    from merging_gym import MergeVecEnv
+
+    seed = 77
+    a = MergeVecEnv(n, device="cuda:0")
+    b = MergeVecEnv(n, device="cuda:0")
+    for k in range(180):  # start mid-episode
+        a.step_random(seed, step_idx=k)
+        b.step_random(seed, step_idx=k)
+    traj = {key: v.clone() if v is not None else None
+            for key, v in b.rollout_random(T, seed, first_step=180).items()}
+    for t in range(T):
+        obs, rew, done, info = a.step_random(seed, step_idx=180 + t)
+        assert torch.equal(traj["obs"][t], obs), t
+        assert torch.equal(traj["rew"][t], rew), t
+        assert torch.equal(traj["done"][t], done), t
+        assert torch.equal(traj["collision"][t], info["collision"]), t
+        assert torch.equal(traj["a1"][t], a.a1_buf) and torch.equal(traj["a2"][t], a.a2_buf), t
+        assert torch.equal(traj["final_observation"][t][done], info["final_observation"][done]), t
+    for name in ("p1", "v1", "p2", "v2", "ret1", "ret2", "tf", "ret_sum", "counts"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+    assert b._step_idx == 180 + T
