@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--envs", type=int, default=1 << 20, help="envs per GPU")
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL, one GPU per rank) or gloo (multi-rank rehearsal, ranks may share a GPU)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="skip per-launch HIP events")
@@ -120,7 +122,8 @@ def rollout_leg(env, args, world, dist, torch):
     durs = timer.durations_ms()
     timer.close()
     kernel_ms = sum(durs) / len(durs)
-    t = torch.tensor([elapsed], dtype=torch.float64, device=env.device)
+    t = torch.tensor([elapsed], dtype=torch.float64,
+                     device="cpu" if args.dist_backend != "nccl" else env.device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     bytes_per_env_step = 52.0 + 104.0 / T
@@ -140,11 +143,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    device = torch.device("cuda", local if world > 1 else 0)
+    device = torch.device("cuda", local % max(torch.cuda.device_count(), 1) if world > 1 else 0)
     torch.cuda.set_device(device)
+    if world > 1:
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(args.dist_backend)
+    host_coll = world > 1 and args.dist_backend != "nccl"
 
     from merging_gym import MergeVecEnv
 
@@ -182,7 +188,8 @@ def main():
         kernel_ms = sum(durs) / len(durs)
         timer.close()
 
-    t = torch.tensor([elapsed, kernel_ms or 0.0], dtype=torch.float64, device=device)
+    t = torch.tensor([elapsed, kernel_ms or 0.0], dtype=torch.float64,
+                     device="cpu" if host_coll else device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kernel_ms_max = float(t[0]), float(t[1])

@@ -50,10 +50,11 @@ def gather_episode_stats(ret_sum, counts, group=None):
         out = torch.empty((world * packed.shape[0], packed.shape[1]), dtype=packed.dtype,
                           device=packed.device)
         dist.all_gather_into_tensor(out, packed, group=group)
-    else:  # gloo: list form
-        parts = [torch.empty_like(packed) for _ in range(world)]
-        dist.all_gather(parts, packed, group=group)
-        out = torch.cat(parts)
+    else:  # gloo: list form, on host memory
+        host = packed.cpu()
+        parts = [torch.empty_like(host) for _ in range(world)]
+        dist.all_gather(parts, host, group=group)
+        out = torch.cat(parts).to(packed.device)
     return unpack_stats(out)
 
 

@@ -1,0 +1,156 @@
+"""In-process A/B of libmerging_hip.so build variants (cdna_hip_programming.md §5.4 rule 24).
+
+    python tools/ab_kernels.py merging-gym_amd/variants/lib_*.so [--envs N] [--rounds R]
+
+Every variant library is loaded into the same process and run on the same GPU in interleaved
+rounds; kernel time per launch comes from events recorded by the dispatch packet
+(mg_time_next_launch). Reports the median / min per variant for the step kernel
+(mg_step_random) and the fused rollout (mg_rollout_random, T steps per launch).
+"""
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "merging-gym_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from merging_gym import _native as nat  # noqa: E402  (struct definitions)
+
+
+def bind(path):
+    lib = ctypes.CDLL(path)
+    PP, SP, OP, STP = (ctypes.POINTER(nat.Params), ctypes.POINTER(nat.State), ctypes.POINTER(nat.Outputs),
+                       ctypes.POINTER(nat.Stats))
+    P = ctypes.c_void_p
+    lib.mg_params_default.argtypes = [PP]
+    lib.mg_reset.argtypes = [PP, SP, P, OP, ctypes.c_int64, P]
+    lib.mg_step_random.argtypes = [PP, SP, P, P, OP, STP, ctypes.c_int64, ctypes.c_int64, ctypes.c_uint64,
+                                   ctypes.c_uint64, ctypes.c_int32, ctypes.c_uint32, P]
+    lib.mg_rollout_random.argtypes = [PP, SP, ctypes.POINTER(nat.Traj), STP, ctypes.c_int64, ctypes.c_int64,
+                                      ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32,
+                                      ctypes.c_uint32, P]
+    lib.mg_time_next_launch.argtypes = [P, P]
+    return lib
+
+
+class Bed:
+    """State + outputs for one variant (separate buffers so variants do not share cache lines)."""
+
+    def __init__(self, lib, n, T):
+        self.lib, self.n, self.T = lib, n, T
+        dev = "cuda"
+        f = lambda: torch.empty(n, dtype=torch.float64, device=dev)  # noqa: E731
+        self.t = [f() for _ in range(6)] + [torch.empty(n, dtype=torch.int32, device=dev)]
+        self.obs = torch.empty((n, 10), device=dev)
+        self.rew = torch.empty((n, 2), device=dev)
+        self.done = torch.empty(n, dtype=torch.uint8, device=dev)
+        self.coll = torch.empty(n, dtype=torch.uint8, device=dev)
+        self.fobs = torch.empty((n, 10), device=dev)
+        self.a = torch.empty((2, n), dtype=torch.int8, device=dev)
+        self.ret_sum = torch.zeros((n, 2), dtype=torch.float64, device=dev)
+        self.counts = torch.zeros((n, 4), dtype=torch.int32, device=dev)
+        self.tobs = torch.empty((T, n, 10), device=dev)
+        self.trew = torch.empty((T, n, 2), device=dev)
+        self.tdone = torch.empty((T, n), dtype=torch.uint8, device=dev)
+        self.tcoll = torch.empty((T, n), dtype=torch.uint8, device=dev)
+        self.ta = torch.empty((2, T, n), dtype=torch.int8, device=dev)
+        self.params = nat.Params()
+        lib.mg_params_default(ctypes.byref(self.params))
+        self.params.angle0 = float(np.arctan2(1000, 30000))
+        self.state = nat.State(*(x.data_ptr() for x in self.t))
+        self.out = nat.Outputs(self.obs.data_ptr(), self.rew.data_ptr(), self.done.data_ptr(),
+                               self.coll.data_ptr(), None, self.fobs.data_ptr(), None, None)
+        self.stats = nat.Stats(self.ret_sum.data_ptr(), self.counts.data_ptr())
+        self.traj = nat.Traj(self.tobs.data_ptr(), self.trew.data_ptr(), self.tdone.data_ptr(),
+                             self.tcoll.data_ptr(), self.ta[0].data_ptr(), self.ta[1].data_ptr(), None)
+        self.k = 0
+        assert lib.mg_reset(ctypes.byref(self.params), ctypes.byref(self.state), None, None, n, None) == 0
+
+    def step(self, ev=None):
+        if ev:
+            self.lib.mg_time_next_launch(*ev)
+        rc = self.lib.mg_step_random(ctypes.byref(self.params), ctypes.byref(self.state), self.a[0].data_ptr(),
+                                     self.a[1].data_ptr(), ctypes.byref(self.out), ctypes.byref(self.stats),
+                                     self.n, 0, 5, self.k, 1, 1, torch.cuda.current_stream().cuda_stream)
+        assert rc == 0
+        self.k += 1
+
+    def rollout(self, ev=None):
+        if ev:
+            self.lib.mg_time_next_launch(*ev)
+        rc = self.lib.mg_rollout_random(ctypes.byref(self.params), ctypes.byref(self.state),
+                                        ctypes.byref(self.traj), ctypes.byref(self.stats), self.n, 0, 5, self.k,
+                                        self.T, 1, 1, torch.cuda.current_stream().cuda_stream)
+        assert rc == 0
+        self.k += self.T
+
+
+class Events:
+    def __init__(self, n):
+        self.hip = ctypes.CDLL("libamdhip64.so.7")
+        self.hip.hipEventCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+        self.hip.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
+        self.ev = []
+        for _ in range(n):
+            a, b = ctypes.c_void_p(), ctypes.c_void_p()
+            self.hip.hipEventCreate(ctypes.byref(a))
+            self.hip.hipEventCreate(ctypes.byref(b))
+            self.ev.append((a, b))
+
+    def ms(self, k):
+        v = ctypes.c_float()
+        self.hip.hipEventElapsedTime(ctypes.byref(v), *self.ev[k])
+        return v.value
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--envs", type=int, default=1 << 20)
+    ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--T", type=int, default=16)
+    ap.add_argument("--rollouts", type=int, default=4)
+    a = ap.parse_args()
+    beds = {os.path.basename(p): Bed(bind(p), a.envs, a.T) for p in a.libs}
+    ev = Events(max(a.steps, a.rollouts))
+    res = {k: {"step": [], "rollout": []} for k in beds}
+    for b in beds.values():  # warm up (and get into mixed episode phases)
+        for _ in range(200):
+            b.step()
+        b.rollout()
+    torch.cuda.synchronize()
+    for r in range(a.rounds):
+        order = list(beds) if r % 2 == 0 else list(reversed(beds))
+        for name in order:
+            b = beds[name]
+            for j in range(a.steps):
+                b.step(ev.ev[j])
+            torch.cuda.synchronize()
+            res[name]["step"] += [ev.ms(j) for j in range(a.steps)]
+            for j in range(a.rollouts):
+                b.rollout(ev.ev[j])
+            torch.cuda.synchronize()
+            res[name]["rollout"] += [ev.ms(j) / a.T for j in range(a.rollouts)]
+    out = {}
+    for name, d in res.items():
+        s, ro = d["step"], d["rollout"]
+        out[name] = {"step_us_median": 1e3 * statistics.median(s), "step_us_min": 1e3 * min(s),
+                     "step_TBps": 156 * a.envs / (statistics.median(s) * 1e-3) / 1e12,
+                     "rollout_us_per_step_median": 1e3 * statistics.median(ro),
+                     "rollout_us_per_step_min": 1e3 * min(ro),
+                     "rollout_TBps": (52 + 104 / a.T) * a.envs / (statistics.median(ro) * 1e-3) / 1e12}
+        print(f"{name:24s} step {out[name]['step_us_median']:7.2f} us (min {out[name]['step_us_min']:6.2f}, "
+              f"{out[name]['step_TBps']:.2f} TB/s)   rollout {out[name]['rollout_us_per_step_median']:6.2f} us/step "
+              f"(min {out[name]['rollout_us_per_step_min']:6.2f}, {out[name]['rollout_TBps']:.2f} TB/s)", flush=True)
+    print(json.dumps({"envs": a.envs, "T": a.T, "results": out}))
+
+
+if __name__ == "__main__":
+    main()
