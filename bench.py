@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="skip per-launch HIP events")
+    ap.add_argument("--event-every", type=int, default=8,
+                    help="time every k-th launch with dispatch-recorded events (arming costs host time)")
     ap.add_argument("--rollout-steps", type=int, default=16,
                     help="T of the fused rollout leg (mg_rollout_random); 0 disables it")
     ap.add_argument("--rollout-launches", type=int, default=60)
@@ -166,17 +168,18 @@ def main():
 
     # per-launch kernel time: HIP events recorded by each dispatch packet (hipExtLaunchKernel)
     use_events = not args.no_events
+    every = max(1, args.event_every)
     if use_events:
         from merging_gym.profiling import KernelTimer
 
-        timer = KernelTimer(args.steps)
+        timer = KernelTimer((args.steps + every - 1) // every)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        if use_events:
-            timer.arm(k)
+        if use_events and k % every == 0:
+            timer.arm(k // every)
         step(args.warmup + k)
     torch.cuda.synchronize()
     if world > 1:

@@ -36,6 +36,12 @@ namespace {
 #ifndef MG_NT_STORES
 #define MG_NT_STORES 1    // non-temporal stores for the per-step outputs
 #endif
+#ifndef MG_SC1_OUT
+#define MG_SC1_OUT 0      // write-through (sc1) stores for the per-step outputs (overrides NT)
+#endif
+#ifndef MG_SC1_STATE
+#define MG_SC1_STATE 0    // write-through (sc1) stores for the env state
+#endif
 #ifndef MG_BLOCK
 #define MG_BLOCK 256
 #endif
@@ -49,10 +55,47 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // Store of a per-step output (observation, reward, flags, actions): written once, never
 // re-read by the step, so optionally non-temporal. The env state is stored normally: the
 // next step reads it back.
+// Write-through store: leaves no dirty line in the XCD's L2 for the kernel-boundary release
+// to write back (MI355X_MICROARCH.md: sc1 stores drop the line; relaxed agent-scope atomic
+// stores lower to `global_store_* sc1`).
+template <class T>
+__device__ __forceinline__ void st_sc1(T* p, T v) {
+  if constexpr (sizeof(T) == 16) {
+    uint64_t w[2];
+    __builtin_memcpy(w, &v, 16);
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(p), w[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(p) + 1, w[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else if constexpr (sizeof(T) == 8) {
+    uint64_t w;
+    __builtin_memcpy(&w, &v, 8);
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(p), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else if constexpr (sizeof(T) == 4) {
+    uint32_t w;
+    __builtin_memcpy(&w, &v, 4);
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(p), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    static_assert(sizeof(T) == 1, "st_sc1: 1, 4, 8 or 16 bytes");
+    uint8_t w;
+    __builtin_memcpy(&w, &v, 1);
+    __hip_atomic_store(reinterpret_cast<uint8_t*>(p), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 template <class T>
 __device__ __forceinline__ void st_out(T* p, T v) {
-#if MG_NT_STORES
+#if MG_SC1_OUT
+  st_sc1(p, v);
+#elif MG_NT_STORES
   __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
+template <class T>
+__device__ __forceinline__ void st_state(T* p, T v) {
+#if MG_SC1_STATE
+  st_sc1(p, v);
 #else
   *p = v;
 #endif
@@ -198,13 +241,13 @@ __device__ __forceinline__ uint32_t pack_tf(const Env& e) {
 }
 
 __device__ __forceinline__ void store_env(const mg_state& S, int64_t i, const Env& e) {
-  S.p1[i] = e.p1;
-  S.v1[i] = e.v1;
-  S.p2[i] = e.p2;
-  S.v2[i] = e.v2;
-  S.ret1[i] = e.ret1;
-  S.ret2[i] = e.ret2;
-  S.tf[i] = pack_tf(e);
+  st_state(S.p1 + i, e.p1);
+  st_state(S.v1 + i, e.v1);
+  st_state(S.p2 + i, e.p2);
+  st_state(S.v2 + i, e.v2);
+  st_state(S.ret1 + i, e.ret1);
+  st_state(S.ret2 + i, e.ret2);
+  st_state(S.tf + i, pack_tf(e));
 }
 
 // What one step returns besides the new state.

@@ -120,7 +120,8 @@ def main():
     a = ap.parse_args()
     beds = {os.path.basename(p): Bed(bind(p), a.envs, a.T) for p in a.libs}
     ev = Events(max(a.steps, a.rollouts))
-    res = {k: {"step": [], "rollout": []} for k in beds}
+    res = {k: {"step": [], "rollout": [], "step_wall": [], "rollout_wall": []} for k in beds}
+    import time
     for b in beds.values():  # warm up (and get into mixed episode phases)
         for _ in range(200):
             b.step()
@@ -138,6 +139,17 @@ def main():
                 b.rollout(ev.ev[j])
             torch.cuda.synchronize()
             res[name]["rollout"] += [ev.ms(j) / a.T for j in range(a.rollouts)]
+            # back-to-back wall clock (no events): kernel + launch boundary
+            t0 = time.perf_counter()
+            for j in range(a.steps):
+                b.step()
+            torch.cuda.synchronize()
+            res[name]["step_wall"].append((time.perf_counter() - t0) / a.steps * 1e3)
+            t0 = time.perf_counter()
+            for j in range(a.rollouts):
+                b.rollout()
+            torch.cuda.synchronize()
+            res[name]["rollout_wall"].append((time.perf_counter() - t0) / (a.rollouts * a.T) * 1e3)
     out = {}
     for name, d in res.items():
         s, ro = d["step"], d["rollout"]
@@ -145,10 +157,14 @@ def main():
                      "step_TBps": 156 * a.envs / (statistics.median(s) * 1e-3) / 1e12,
                      "rollout_us_per_step_median": 1e3 * statistics.median(ro),
                      "rollout_us_per_step_min": 1e3 * min(ro),
-                     "rollout_TBps": (52 + 104 / a.T) * a.envs / (statistics.median(ro) * 1e-3) / 1e12}
+                     "rollout_TBps": (52 + 104 / a.T) * a.envs / (statistics.median(ro) * 1e-3) / 1e12,
+                     "step_wall_us_median": 1e3 * statistics.median(d["step_wall"]),
+                     "rollout_wall_us_per_step_median": 1e3 * statistics.median(d["rollout_wall"])}
         print(f"{name:24s} step {out[name]['step_us_median']:7.2f} us (min {out[name]['step_us_min']:6.2f}, "
               f"{out[name]['step_TBps']:.2f} TB/s)   rollout {out[name]['rollout_us_per_step_median']:6.2f} us/step "
-              f"(min {out[name]['rollout_us_per_step_min']:6.2f}, {out[name]['rollout_TBps']:.2f} TB/s)", flush=True)
+              f"(min {out[name]['rollout_us_per_step_min']:6.2f}, {out[name]['rollout_TBps']:.2f} TB/s)  "
+              f"wall: step {out[name]['step_wall_us_median']:6.2f} rollout {out[name]['rollout_wall_us_per_step_median']:6.2f}",
+              flush=True)
     print(json.dumps({"envs": a.envs, "T": a.T, "results": out}))
 
 
