@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--rollout-steps", type=int, default=16,
                     help="T of the fused rollout leg (mg_rollout_random); 0 disables it")
     ap.add_argument("--rollout-launches", type=int, default=60)
+    ap.add_argument("--qnet-launches", type=int, default=20,
+                    help="launches of the config-5 leg (fused epsilon-greedy DQN rollout); 0 disables it")
     return ap.parse_args()
 
 
@@ -137,6 +139,55 @@ def rollout_leg(env, args, world, dist, torch):
             "unit_bw": "GB/s", "frac": achieved / HBM_PEAK_GBPS}
 
 
+QNET_USEFUL_FLOP = 2 * (10 * 200 + 200 * 100 + 100 * 5)      # one Net forward, main.py:30-47
+QNET_MFMA_FLOP = 142 * 32 * 32 * 16 * 2 // 64                 # padded 224/128/32 tiles, per env
+MFMA_BF16_PEAK_TFLOPS = 2500.0                                 # MI355X dense bf16
+
+
+def qnet_leg(env, args, world, dist, torch, opponent):
+    """BASELINE config 5: the reference's epsilon-greedy DQN (weights: the checkpoint
+    human_player.py:68 loads, tests/golden/dqn_checkpoints.npz) fused with the env step."""
+    import numpy as np
+
+    from merging_gym.policy import QNet
+    from merging_gym.profiling import KernelTimer
+
+    f = np.load(os.path.join(ROOT, "tests", "golden", "dqn_checkpoints.npz"))
+    qnet = QNet.from_state_dict({k.split("/", 1)[1]: f[k] for k in f.files if k.startswith("l1/")},
+                                device=env.device)
+    T, L, E = args.rollout_steps, args.qnet_launches, env.num_envs
+    k = 20_000_000
+    for _ in range(2):
+        env.rollout_qnet(T, qnet, args.seed, opponent=opponent, first_step=k, final_observation=False)
+        k += T
+    timer = KernelTimer(L)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for j in range(L):
+        timer.arm(j)
+        env.rollout_qnet(T, qnet, args.seed, opponent=opponent, first_step=k, final_observation=False)
+        k += T
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    durs = timer.durations_ms()
+    timer.close()
+    kernel_ms = sum(durs) / len(durs)
+    nets = 2 if opponent == "self" else 1
+    per_s = E * T / (kernel_ms * 1e-3)
+    return {"kernel": f"qnet_rollout_kernel<{ {'none': 0, 'uniform': 1, 'self': 2}[opponent] }>",
+            "opponent": opponent, "steps_per_launch": T, "launches": L, "dtype": "bf16 (fp32 accumulate)",
+            "value": world * E * T * L / elapsed, "unit": "env-steps/s",
+            "ms_per_step": elapsed / (L * T) * 1e3, "kernel_ms_mean": kernel_ms,
+            "useful_tflops": nets * QNET_USEFUL_FLOP * per_s / 1e12,
+            "mfma_tflops": nets * QNET_MFMA_FLOP * per_s / 1e12,
+            "peak_tflops": MFMA_BF16_PEAK_TFLOPS,
+            "frac_useful": nets * QNET_USEFUL_FLOP * per_s / 1e12 / MFMA_BF16_PEAK_TFLOPS}
+
+
 def main():
     args = parse()
     import torch
@@ -215,6 +266,10 @@ def main():
     if args.rollout_steps > 0:
         rollout = rollout_leg(env, args, world, dist, torch)
 
+    qnet = None
+    if args.qnet_launches > 0 and args.rollout_steps > 0:
+        qnet = [qnet_leg(env, args, world, dist, torch, opp) for opp in ("none", "self")]
+
     total_env_steps = world * E * args.steps
     value = total_env_steps / elapsed
     if rank == 0:
@@ -246,6 +301,8 @@ def main():
         }
         if rollout is not None:
             line["rollout"] = rollout
+        if qnet is not None:
+            line["qnet_policy"] = qnet
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         print(json.dumps(line), flush=True)

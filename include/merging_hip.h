@@ -18,6 +18,10 @@
  *                     :198-206 (no state change)
  *   mg_rollout_random  T steps of mg_step_random in one launch (trajectory outputs); it
  *                     replaces the callers' per-step collection loop (scripts/main.py:192-220)
+ *   mg_rollout_qnet T steps with the epsilon-greedy DQN policy fused in (bf16 MFMA): replaces
+ *                     DQN.choose_action (scripts/main.py:99-112, hdqn.py:165-177) + env.step
+ *   mg_qnet_pack / mg_qnet_forward / mg_qnet_packed_bytes: the Q-net Net (main.py:30-47,
+ *                     hdqn.py:38-55) in the kernel's packed bf16 layout, and its forward pass
  *   mg_abi_version, mg_last_error, mg_params_default, mg_time_next_launch: library plumbing
  *                     and profiling (no reference twin).
  *
@@ -181,6 +185,36 @@ int mg_rollout_random(const mg_params* params, const mg_state* state, const mg_t
                       const mg_stats* stats, int64_t n, int64_t env_offset, uint64_t seed,
                       uint64_t first_step, int32_t num_steps, int32_t opponent_random,
                       uint32_t flags, void* stream);
+
+/* ---- DQN policy (scripts/main.py:30-47 Net, :99-112 choose_action) ---------------------------
+ * A packed Q-net is one device buffer of mg_qnet_packed_bytes() bytes (16-byte aligned) made by
+ * mg_qnet_pack from the fp32 torch tensors fc1.weight [200,in], fc1.bias [200], fc2.weight
+ * [100,200], fc2.bias [100], out.weight [out,100], out.bias [out] (device pointers, row-major).
+ * Weights are stored as bf16, biases as fp32; hidden sizes are the reference's 200 and 100;
+ * 1 <= in_dim <= 16, 1 <= out_dim <= 8. */
+size_t mg_qnet_packed_bytes(void);
+int mg_qnet_pack(const float* fc1_w, const float* fc1_b, const float* fc2_w, const float* fc2_b,
+                 const float* out_w, const float* out_b, int32_t in_dim, int32_t out_dim,
+                 void* packed, void* stream);
+
+/* q[n,8] fp32 = Net(obs[n,10]) with bf16 operands and fp32 accumulation (rows >= out_dim are
+ * padding). swap_halves != 0 feeds the opponent's view obs[5:] + obs[:5] (main.py:199). */
+int mg_qnet_forward(const void* packed, const float* obs, int32_t swap_halves, float* q, int64_t n,
+                    void* stream);
+
+/* num_steps steps in ONE launch with the epsilon-greedy Q-net policy computed on the device:
+ * for each env and step, Philox4x32-10 (key = seed, counter = (env_offset + i, first_step + t))
+ * gives u = (u0, u1, u2, u3); the ego acts greedily (argmax of Q(obs), lowest index on ties)
+ * when u0 < greedy_threshold and takes floor(5 u1 / 2^32) otherwise -- greedy_threshold =
+ * round(Phi(0.7) 2^32) reproduces `np.random.randn() <= EPISILO` (main.py:105). The opponent
+ * is None (opponent_mode 0), uniform floor(5 u3 / 2^32) (1), or the same net on the swapped
+ * observation with u2 / u3 and opp_greedy_threshold (2). Outputs as mg_rollout_random
+ * (traj->obs[t] = observation after step t, the network input of step t + 1). */
+int mg_rollout_qnet(const mg_params* params, const mg_state* state, const mg_traj* traj,
+                    const mg_stats* stats, int64_t n, int64_t env_offset, uint64_t seed,
+                    uint64_t first_step, int32_t num_steps, const void* net, int32_t out_dim,
+                    uint64_t greedy_threshold, int32_t opponent_mode,
+                    uint64_t opp_greedy_threshold, uint32_t flags, void* stream);
 
 /* Resets the envs whose mask byte is non-zero (mask == NULL: all n) and writes their reset
  * observation to out->obs / out->rec64 when given. Replaces MergeEnv.reset (merging_env.py:208-230). */

@@ -387,8 +387,8 @@ __device__ __forceinline__ void finish_episode(const mg_params& P, Env& e, StepO
 // Write a block's [rows,10] fp32 observation tile through LDS as contiguous 16-byte stores
 // (a wave's 64 rows of 40 B become 160 dwordx4 lanes instead of 640 scattered dwords).
 // Every thread of the block must call it (two barriers).
-__device__ __forceinline__ void store_obs_tile(float* tile, const double (&o)[kObs], float* dst,
-                                               int nrows) {
+__device__ __forceinline__ void store_obs_tile_n(float* tile, const double (&o)[kObs], float* dst,
+                                                 int nrows, int block) {
   const int tid = threadIdx.x;
   float2* t2 = reinterpret_cast<float2*>(tile + tid * kObs);
 #pragma unroll
@@ -396,20 +396,26 @@ __device__ __forceinline__ void store_obs_tile(float* tile, const double (&o)[kO
     t2[k] = make_float2(static_cast<float>(o[2 * k]), static_cast<float>(o[2 * k + 1]));
   __syncthreads();
   const int nfl = nrows * kObs;
-  if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+  if (dst == nullptr) {
+  } else if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
     const int n4 = nfl >> 2;
     f32x4* d4 = reinterpret_cast<f32x4*>(dst);
     const f32x4* s4 = reinterpret_cast<const f32x4*>(tile);
-    for (int j = tid; j < n4; j += kBlock) st_out(d4 + j, s4[j]);
+    for (int j = tid; j < n4; j += block) st_out(d4 + j, s4[j]);
     const int tail = nfl - (n4 << 2);  // 0 or 2
     if (tid < tail) st_out(dst + (n4 << 2) + tid, tile[(n4 << 2) + tid]);
   } else {  // rows are 8-byte aligned whenever the buffer is
     const int n2 = nfl >> 1;
     f32x2* d2 = reinterpret_cast<f32x2*>(dst);
     const f32x2* s2 = reinterpret_cast<const f32x2*>(tile);
-    for (int j = tid; j < n2; j += kBlock) st_out(d2 + j, s2[j]);
+    for (int j = tid; j < n2; j += block) st_out(d2 + j, s2[j]);
   }
   __syncthreads();
+}
+
+__device__ __forceinline__ void store_obs_tile(float* tile, const double (&o)[kObs], float* dst,
+                                               int nrows) {
+  store_obs_tile_n(tile, o, dst, nrows, kBlock);
 }
 
 struct Launch {
@@ -550,6 +556,301 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(const Rollout R) {
     }
     if (R.T.obs)
       store_obs_tile(obs_tile, r.o, R.T.obs + (static_cast<int64_t>(t) * R.n + base) * kObs, nrows);
+  }
+  if (live) store_env(R.S, i, e);
+}
+
+// ============================================================================ Q-net policy
+// The reference's DQN Net (scripts/main.py:30-47, scripts/hdqn.py:38-55): Linear(in,200) ->
+// ReLU -> Linear(200,100) -> ReLU -> Linear(100,out), and its epsilon-greedy choose_action
+// (main.py:99-112: greedy argmax when np.random.randn() <= EPISILO, else uniform). Computed
+// in bf16 on the matrix cores with fp32 accumulation (v_mfma_f32_32x32x16_bf16), one wave per
+// 64 envs, in the TRANSPOSED form  H1' = W1 X',  H2' = W2 H1',  Q' = W3 H2'  (hidden units
+// on the 32 rows of a tile, envs on its 32 columns = lanes). A 32x32 accumulator keeps its
+// rows in registers, so it feeds the next MFMA directly as the B operand (k = hidden unit):
+// registers 8s..8s+7 of lane half h hold rows 16s + 8(j>>2) + 4h + (j&3), j = 0..7, and the
+// packed weights store each 16-column block with that k order (mg_qnet_pack), so no lane
+// moves and no LDS round trip between layers.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kQH1 = 224, kQH2 = 128, kQOut = 32;                 // padded 200, 100, out
+constexpr int kQS1 = 24, kQS2 = 232, kQS3 = 136;                   // row strides (bf16): every
+constexpr int kQOffW2 = kQH1 * kQS1 * 2;                           // ds_read_b128 lane group hits
+constexpr int kQOffW3 = kQOffW2 + kQH2 * kQS2 * 2;                 // 16 distinct 4-bank slots
+constexpr int kQOffB1 = kQOffW3 + kQOut * kQS3 * 2;
+constexpr int kQOffB2 = kQOffB1 + kQH1 * 4;
+constexpr int kQOffB3 = kQOffB2 + kQH2 * 4;
+constexpr int kQNetBytes = kQOffB3 + kQOut * 4;                    // 80,384 B
+constexpr int kQBlock = 512;                                       // 8 waves share one LDS copy
+static_assert(kQOffW2 % 16 == 0 && kQOffW3 % 16 == 0 && kQOffB1 % 16 == 0 && kQOffB2 % 16 == 0 &&
+                  kQOffB3 % 16 == 0 && kQNetBytes % 16 == 0,
+              "packed Q-net sections must stay 16-byte aligned");
+
+// hardware k (0..15) within a 16-block -> hidden unit within that block (see above)
+__host__ __device__ constexpr int qnet_krow(int kk) {
+  return 8 * ((kk & 7) >> 2) + 4 * (kk >> 3) + (kk & 3);
+}
+
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// Packs fp32 torch Linear weights (row-major [out][in]) into the kernel layout.
+__global__ void qnet_pack_kernel(const float* w1, const float* b1, const float* w2, const float* b2,
+                                 const float* w3, const float* b3, int in_dim, int out_dim,
+                                 uint8_t* packed) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  __bf16* pw1 = reinterpret_cast<__bf16*>(packed);
+  __bf16* pw2 = reinterpret_cast<__bf16*>(packed + kQOffW2);
+  __bf16* pw3 = reinterpret_cast<__bf16*>(packed + kQOffW3);
+  float* pb1 = reinterpret_cast<float*>(packed + kQOffB1);
+  float* pb2 = reinterpret_cast<float*>(packed + kQOffB2);
+  float* pb3 = reinterpret_cast<float*>(packed + kQOffB3);
+  int e = idx;
+  if (e < kQH1 * kQS1) {  // W1[m][k]: natural k order (the input features)
+    const int m = e / kQS1, k = e % kQS1;
+    pw1[e] = static_cast<__bf16>((m < 200 && k < in_dim) ? w1[m * in_dim + k] : 0.f);
+    return;
+  }
+  e -= kQH1 * kQS1;
+  if (e < kQH2 * kQS2) {  // W2[m][c]: columns in the accumulator's k order
+    const int m = e / kQS2, c = e % kQS2;
+    const int src = 16 * (c / 16) + qnet_krow(c % 16);
+    pw2[e] = static_cast<__bf16>((m < 100 && c < kQH1 && src < 200) ? w2[m * 200 + src] : 0.f);
+    return;
+  }
+  e -= kQH2 * kQS2;
+  if (e < kQOut * kQS3) {
+    const int m = e / kQS3, c = e % kQS3;
+    const int src = 16 * (c / 16) + qnet_krow(c % 16);
+    pw3[e] = static_cast<__bf16>((m < out_dim && c < kQH2 && src < 100) ? w3[m * 100 + src] : 0.f);
+    return;
+  }
+  e -= kQOut * kQS3;
+  if (e < kQH1) { pb1[e] = e < 200 ? b1[e] : 0.f; return; }
+  e -= kQH1;
+  if (e < kQH2) { pb2[e] = e < 100 ? b2[e] : 0.f; return; }
+  e -= kQH2;
+  if (e < kQOut) pb3[e] = e < out_dim ? b3[e] : 0.f;
+}
+
+// Cooperative copy of a packed net into LDS (all threads of the block; caller syncs).
+__device__ __forceinline__ void qnet_to_lds(const uint8_t* net, uint8_t* lds) {
+  const f32x4* src = reinterpret_cast<const f32x4*>(net);
+  f32x4* dst = reinterpret_cast<f32x4*>(lds);
+  for (int j = threadIdx.x; j < kQNetBytes / 16; j += blockDim.x) dst[j] = src[j];
+}
+
+// Q-values of this lane's env (rows 0..7) from the block's f32 observation tile in LDS.
+// row0 = tile row of this wave's lane 0. swap = the opponent's view state[5:] + state[:5]
+// (scripts/main.py:199, human_player.py:40-41). Every lane of the wave must call it.
+__device__ __forceinline__ void qnet_forward(const uint8_t* net, const float* tile, int row0,
+                                             bool swap, float (&q)[8]) {
+  const __bf16* W1 = reinterpret_cast<const __bf16*>(net);
+  const __bf16* W2 = reinterpret_cast<const __bf16*>(net + kQOffW2);
+  const __bf16* W3 = reinterpret_cast<const __bf16*>(net + kQOffW3);
+  const float* B1 = reinterpret_cast<const float*>(net + kQOffB1);
+  const float* B2 = reinterpret_cast<const float*>(net + kQOffB2);
+  const float* B3 = reinterpret_cast<const float*>(net + kQOffB3);
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+
+  // One N-tile (32 envs = lanes 32*NT .. 32*NT+31) at a time: 4 layer-2 accumulators live
+  // instead of 8 (W2 fragments are re-read from LDS per tile, which the LDS rate covers).
+  f32x16 acc3[2];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    // layer-1 B operand: X'[k = 8h + j][env 32 nt + r]
+    bf16x8 xb;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 8 * h + j;
+      const int src = swap ? (k < 5 ? k + 5 : k - 5) : k;
+      xb[j] = static_cast<__bf16>(k < kObs ? tile[(row0 + 32 * nt + r) * kObs + src] : 0.f);
+    }
+    const f32x16 zero = {};
+    f32x16 acc2[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) acc2[m] = zero;
+    // rolled on purpose: unrolled, hipcc hoists all 56 W2 fragment loads ahead of the MFMAs
+    // and runs out of registers
+#pragma unroll 1
+    for (int mt = 0; mt < kQH1 / 32; ++mt) {
+      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(W1 + (32 * mt + r) * kQS1 + 8 * h);
+      const f32x16 c = mfma32(a1, xb, zero);
+      bf16x8 hb[2];  // [k-step]
+#pragma unroll
+      for (int qq = 0; qq < 16; ++qq) {
+        const float b = B1[32 * mt + (qq & 3) + 8 * (qq >> 2) + 4 * h];
+        hb[qq >> 3][qq & 7] = static_cast<__bf16>(fmaxf(c[qq] + b, 0.f));
+      }
+#pragma unroll
+      for (int m2 = 0; m2 < kQH2 / 32; ++m2) {
+#pragma unroll
+        for (int sk = 0; sk < 2; ++sk) {
+          const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(W2 + (32 * m2 + r) * kQS2 +
+                                                             16 * (2 * mt + sk) + 8 * h);
+          acc2[m2] = mfma32(a2, hb[sk], acc2[m2]);
+        }
+      }
+    }
+    f32x16 a3acc = zero;
+#pragma unroll
+    for (int m2 = 0; m2 < kQH2 / 32; ++m2) {
+      bf16x8 hb[2];
+#pragma unroll
+      for (int qq = 0; qq < 16; ++qq) {
+        const float b = B2[32 * m2 + (qq & 3) + 8 * (qq >> 2) + 4 * h];
+        hb[qq >> 3][qq & 7] = static_cast<__bf16>(fmaxf(acc2[m2][qq] + b, 0.f));
+      }
+#pragma unroll
+      for (int sk = 0; sk < 2; ++sk) {
+        const bf16x8 a3 =
+            *reinterpret_cast<const bf16x8*>(W3 + r * kQS3 + 16 * (2 * m2 + sk) + 8 * h);
+        a3acc = mfma32(a3, hb[sk], a3acc);
+      }
+    }
+    acc3[nt] = a3acc;
+  }
+  // Column r of N-tile t is the env of lane 32t + r. Rows 0-3 sit in registers 0-3 of lane
+  // half 0, rows 4-7 in registers 0-3 of lane half 1: swap halves across the wave.
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float own = h ? acc3[1][j] : acc3[0][j];
+    const float send = h ? acc3[0][j] : acc3[1][j];
+    const float got = __shfl_xor(send, 32);
+    q[j] = (h ? got : own) + B3[j];
+    q[4 + j] = (h ? own : got) + B3[4 + j];
+  }
+}
+
+__device__ __forceinline__ int argmax_first(const float (&q)[8], int out_dim) {
+  int best = 0;
+  float v = q[0];
+#pragma unroll
+  for (int j = 1; j < 8; ++j)
+    if (j < out_dim && q[j] > v) {
+      v = q[j];
+      best = j;
+    }
+  return best;
+}
+
+// Standalone forward for tests / evaluation: q[i][0..7] for obs[i][0..9].
+__global__ __launch_bounds__(kBlock) void qnet_forward_kernel(const uint8_t* net, const float* obs,
+                                                              int swap, float* qout, int64_t n) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds_net[kQNetBytes];
+  __shared__ __attribute__((aligned(16))) float tile[kBlock * kObs];
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kBlock;
+  qnet_to_lds(net, lds_net);
+  for (int j = threadIdx.x; j < kBlock * kObs; j += kBlock) {
+    const int64_t g = base * kObs + j;
+    tile[j] = g < n * kObs ? obs[g] : 0.f;
+  }
+  __syncthreads();
+  float q[8];
+  qnet_forward(lds_net, tile, (threadIdx.x >> 6) * 64, swap != 0, q);
+  const int64_t i = base + threadIdx.x;
+  if (i < n) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qout[i * 8 + j] = q[j];
+  }
+}
+
+struct QRollout {
+  mg_params P;
+  mg_state S;
+  mg_traj T;
+  mg_stats St;
+  const uint8_t* net;
+  uint64_t seed;
+  uint64_t first_step;
+  uint64_t greedy_thr;      // greedy iff u32 draw < greedy_thr (2^32: always)
+  uint64_t opp_greedy_thr;
+  int64_t env_offset;
+  int64_t n;
+  int32_t num_steps;
+  int32_t out_dim;
+  uint32_t flags;
+};
+
+// T epsilon-greedy Q-net steps per launch. OPP: 0 = None (L0 opponent), 1 = uniform random,
+// 2 = the same net on the swapped observation (self-play, main.py:165-166 / :199).
+// Philox4x32-10 per (global env, step): u.x ego explore draw, u.y ego random action,
+// u.z opponent explore draw, u.w opponent random action.
+template <int OPP>
+__global__ __launch_bounds__(kQBlock, 2) void qnet_rollout_kernel(const QRollout R) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds_net[kQNetBytes];
+  __shared__ __attribute__((aligned(16))) float tile[kQBlock * kObs];
+
+  const mg_params& P = R.P;
+  const int tid = threadIdx.x;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kQBlock;
+  const int64_t i = base + tid;
+  const bool live = i < R.n;
+  const int64_t rem = R.n - base;
+  const int nrows = rem < kQBlock ? static_cast<int>(rem) : kQBlock;
+  const bool autoreset = (R.flags & MG_AUTORESET) != 0;
+  const int row0 = (tid >> 6) * 64;
+
+  qnet_to_lds(R.net, lds_net);
+  Env e;
+  StepOut r;
+  if (live) {
+    e = load_env(R.S, i);
+    double x1, y1, x2, y2;
+    lon2coord(P, e.p1, true, x1, y1);
+    lon2coord(P, e.p2, false, x2, y2);
+    observe(P, e.p1, e.v1, e.p2, e.v2, x1, y1, x2, y2, r.o);
+  } else {
+#pragma unroll
+    for (int k = 0; k < kObs; ++k) r.o[k] = 0.0;
+  }
+  {
+    float2* t2 = reinterpret_cast<float2*>(tile + tid * kObs);
+#pragma unroll
+    for (int k = 0; k < kObs / 2; ++k)
+      t2[k] = make_float2(static_cast<float>(r.o[2 * k]), static_cast<float>(r.o[2 * k + 1]));
+  }
+  __syncthreads();
+
+  for (int t = 0; t < R.num_steps; ++t) {
+    float q[8];
+    qnet_forward(lds_net, tile, row0, false, q);
+    const int greedy1 = argmax_first(q, R.out_dim);
+    int greedy2 = 0;
+    if constexpr (OPP == 2) {
+      qnet_forward(lds_net, tile, row0, true, q);
+      greedy2 = argmax_first(q, R.out_dim);
+    }
+    __syncthreads();  // every wave is done reading the tile before it is overwritten
+    const int64_t row = static_cast<int64_t>(t) * R.n + i;
+    if (live) {
+      const uint64_t gi = static_cast<uint64_t>(R.env_offset + i);
+      const uint64_t step = R.first_step + t;
+      const uint4 u = philox4x32_10(
+          make_uint4(static_cast<uint32_t>(gi), static_cast<uint32_t>(gi >> 32),
+                     static_cast<uint32_t>(step), static_cast<uint32_t>(step >> 32)),
+          static_cast<uint32_t>(R.seed), static_cast<uint32_t>(R.seed >> 32));
+      const int a1 = (static_cast<uint64_t>(u.x) < R.greedy_thr) ? greedy1 : action_from_u32(u.y);
+      int a2 = MG_ACTION_NONE;
+      if constexpr (OPP == 1) a2 = action_from_u32(u.w);
+      if constexpr (OPP == 2)
+        a2 = (static_cast<uint64_t>(u.z) < R.opp_greedy_thr) ? greedy2 : action_from_u32(u.w);
+      env_step(P, e, a1, a2, r);
+      if (R.T.a1) st_out(R.T.a1 + row, static_cast<int8_t>(a1));
+      if (R.T.a2) st_out(R.T.a2 + row, static_cast<int8_t>(a2));
+      if (R.T.rew)
+        st_out(reinterpret_cast<f32x2*>(R.T.rew) + row,
+               f32x2{static_cast<float>(r.r1), static_cast<float>(r.r2)});
+      if (R.T.done) st_out(R.T.done + row, static_cast<uint8_t>(r.done ? 1 : 0));
+      if (R.T.coll) st_out(R.T.coll + row, static_cast<uint8_t>(r.coll ? 1 : 0));
+      if (autoreset && r.done)
+        finish_episode(P, e, r, R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i);
+    }
+    // writes the new observations into the tile (the next step's network input) and out
+    store_obs_tile_n(tile, r.o, R.T.obs ? R.T.obs + (static_cast<int64_t>(t) * R.n + base) * kObs : nullptr,
+                     nrows, kQBlock);
   }
   if (live) store_env(R.S, i, e);
 }
@@ -785,6 +1086,94 @@ int mg_rollout_random(const mg_params* params, const mg_state* state, const mg_t
   R.opp_random = opponent_random;
   R.flags = flags;
   return launch_rollout(R, static_cast<hipStream_t>(stream));
+}
+
+size_t mg_qnet_packed_bytes(void) { return static_cast<size_t>(kQNetBytes); }
+
+int mg_qnet_pack(const float* fc1_w, const float* fc1_b, const float* fc2_w, const float* fc2_b,
+                 const float* out_w, const float* out_b, int32_t in_dim, int32_t out_dim,
+                 void* packed, void* stream) {
+  if (!fc1_w || !fc1_b || !fc2_w || !fc2_b || !out_w || !out_b || !packed)
+    return fail(hipErrorInvalidValue, "%s", "mg_qnet_pack: NULL pointer");
+  if (in_dim < 1 || in_dim > 16 || out_dim < 1 || out_dim > 8)
+    return fail(hipErrorInvalidValue, "%s", "mg_qnet_pack: need 1 <= in_dim <= 16, 1 <= out_dim <= 8");
+  if (reinterpret_cast<uintptr_t>(packed) & 15)
+    return fail(hipErrorInvalidValue, "%s", "mg_qnet_pack: packed buffer must be 16-byte aligned");
+  const int total = kQH1 * kQS1 + kQH2 * kQS2 + kQOut * kQS3 + kQH1 + kQH2 + kQOut;
+  hipLaunchKernelGGL(qnet_pack_kernel, dim3((total + 255) / 256), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), fc1_w, fc1_b, fc2_w, fc2_b, out_w, out_b,
+                     in_dim, out_dim, static_cast<uint8_t*>(packed));
+  return finish_launch("mg_qnet_pack");
+}
+
+int mg_qnet_forward(const void* packed, const float* obs, int32_t swap_halves, float* q, int64_t n,
+                    void* stream) {
+  if (!packed || !obs || !q) return fail(hipErrorInvalidValue, "%s", "mg_qnet_forward: NULL pointer");
+  if (n < 0) return fail(hipErrorInvalidValue, "%s", "n < 0");
+  if (reinterpret_cast<uintptr_t>(packed) & 15)
+    return fail(hipErrorInvalidValue, "%s", "packed net must be 16-byte aligned");
+  if (n == 0) return 0;
+  const unsigned blocks = static_cast<unsigned>((n + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(qnet_forward_kernel, dim3(blocks), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), static_cast<const uint8_t*>(packed), obs,
+                     swap_halves, q, n);
+  return finish_launch("mg_qnet_forward");
+}
+
+int mg_rollout_qnet(const mg_params* params, const mg_state* state, const mg_traj* traj,
+                    const mg_stats* stats, int64_t n, int64_t env_offset, uint64_t seed,
+                    uint64_t first_step, int32_t num_steps, const void* net, int32_t out_dim,
+                    uint64_t greedy_threshold, int32_t opponent_mode,
+                    uint64_t opp_greedy_threshold, uint32_t flags, void* stream) {
+  mg_outputs none{};
+  if (int e = check_common(params, state, &none, n)) return e;
+  if (!traj) return fail(hipErrorInvalidValue, "%s", "traj is NULL (pass a zeroed mg_traj)");
+  if (!net || (reinterpret_cast<uintptr_t>(net) & 15))
+    return fail(hipErrorInvalidValue, "%s", "net must be a 16-byte aligned packed Q-net");
+  if (num_steps < 0 || out_dim < 1 || out_dim > 8)
+    return fail(hipErrorInvalidValue, "%s", "need num_steps >= 0 and 1 <= out_dim <= 8");
+  if (opponent_mode < 0 || opponent_mode > 2)
+    return fail(hipErrorInvalidValue, "%s", "opponent_mode must be 0 (None), 1 (uniform) or 2 (same net)");
+  if ((traj->obs && (reinterpret_cast<uintptr_t>(traj->obs) & 15)) ||
+      (traj->final_obs && (reinterpret_cast<uintptr_t>(traj->final_obs) & 7)) ||
+      (traj->rew && (reinterpret_cast<uintptr_t>(traj->rew) & 7)))
+    return fail(hipErrorInvalidValue, "%s", "traj.obs must be 16-byte, rew/final_obs 8-byte aligned");
+  if (n == 0 || num_steps == 0) return 0;
+  QRollout R{};
+  R.P = *params;
+  R.S = *state;
+  R.T = *traj;
+  if (stats) R.St = *stats;
+  R.net = static_cast<const uint8_t*>(net);
+  R.seed = seed;
+  R.first_step = first_step;
+  R.greedy_thr = greedy_threshold;
+  R.opp_greedy_thr = opp_greedy_threshold;
+  R.env_offset = env_offset;
+  R.n = n;
+  R.num_steps = num_steps;
+  R.out_dim = out_dim;
+  R.flags = flags;
+  const unsigned blocks = static_cast<unsigned>((n + kQBlock - 1) / kQBlock);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  hipEvent_t ev0 = g_ev_start, ev1 = g_ev_stop;
+  g_ev_start = g_ev_stop = nullptr;
+#define MG_LAUNCH_Q(OPPV)                                                                         \
+  do {                                                                                            \
+    if (ev0 || ev1)                                                                               \
+      hipExtLaunchKernelGGL(qnet_rollout_kernel<OPPV>, dim3(blocks), dim3(kQBlock), 0, st, ev0,  \
+                            ev1, 0, R);                                                           \
+    else                                                                                          \
+      hipLaunchKernelGGL(qnet_rollout_kernel<OPPV>, dim3(blocks), dim3(kQBlock), 0, st, R);      \
+  } while (0)
+  if (opponent_mode == 0)
+    MG_LAUNCH_Q(0);
+  else if (opponent_mode == 1)
+    MG_LAUNCH_Q(1);
+  else
+    MG_LAUNCH_Q(2);
+#undef MG_LAUNCH_Q
+  return finish_launch("mg_rollout_qnet");
 }
 
 int mg_reset(const mg_params* params, const mg_state* state, const uint8_t* mask,

@@ -93,9 +93,15 @@ def _load():
     lib.mg_observe.argtypes = [PP, SP, OP, _c.c_int64, _P]
     lib.mg_rollout_random.argtypes = [PP, SP, _c.POINTER(Traj), STP, _c.c_int64, _c.c_int64,
                                       _c.c_uint64, _c.c_uint64, _c.c_int32, _c.c_int32, _c.c_uint32, _P]
+    lib.mg_qnet_packed_bytes.restype = _c.c_size_t
+    lib.mg_qnet_pack.argtypes = [_P] * 6 + [_c.c_int32, _c.c_int32, _P, _P]
+    lib.mg_qnet_forward.argtypes = [_P, _P, _c.c_int32, _P, _c.c_int64, _P]
+    lib.mg_rollout_qnet.argtypes = [PP, SP, _c.POINTER(Traj), STP, _c.c_int64, _c.c_int64, _c.c_uint64,
+                                    _c.c_uint64, _c.c_int32, _P, _c.c_int32, _c.c_uint64, _c.c_int32,
+                                    _c.c_uint64, _c.c_uint32, _P]
     lib.mg_time_next_launch.argtypes = [_P, _P]
     for f in (lib.mg_step, lib.mg_step_random, lib.mg_reset, lib.mg_observe, lib.mg_rollout_random,
-              lib.mg_time_next_launch):
+              lib.mg_time_next_launch, lib.mg_qnet_pack, lib.mg_qnet_forward, lib.mg_rollout_qnet):
         f.restype = _c.c_int
     v = lib.mg_abi_version()
     if v != ABI_VERSION:

@@ -184,9 +184,21 @@ class MergeVecEnv:
         step_random(seed, step_idx=first_step + t). Returns a dict of [T, N, ...] tensors:
         obs, rew, done (bool), collision (bool), a1, a2 and final_observation (rows where
         done). The buffers are reused by the next rollout of the same length."""
-        torch, nat = self._torch, self._nat
+        nat = self._nat
         T, n = int(num_steps), self.num_envs
         k0 = self._step_idx if first_step is None else int(first_step)
+        buf = self._traj(T, final_observation)
+        rc = nat.lib.mg_rollout_random(
+            self._p_ref, self._s_ref, ctypes.byref(buf["_traj"]), self._st_ref, n, self.env_offset,
+            seed & 0xFFFFFFFFFFFFFFFF, k0 & 0xFFFFFFFFFFFFFFFF, T, 1 if opponent_random else 0,
+            self._flags, self._stream())
+        nat.check(rc, "mg_rollout_random")
+        self._step_idx = k0 + T
+        return buf["_result"]
+
+    def _traj(self, T, final_observation):
+        """[T, N, ...] trajectory buffers, reused while T and the final-obs choice stay the same."""
+        torch, nat, n = self._torch, self._nat, self.num_envs
         buf = getattr(self, "_traj_bufs", None)
         if buf is None or buf["T"] != T or (buf["final_observation"] is None) == final_observation:
             dev = self.device
@@ -206,11 +218,27 @@ class MergeVecEnv:
                               "collision": buf["collision"].view(torch.bool), "a1": buf["a1"],
                               "a2": buf["a2"], "final_observation": buf["final_observation"]}
             self._traj_bufs = buf
-        rc = nat.lib.mg_rollout_random(
+        return buf
+
+    def rollout_qnet(self, num_steps: int, qnet, seed: int, opponent: str = "none",
+                     episilo: float = 0.7, opp_episilo: float = 0.7, first_step=None,
+                     final_observation: bool = True):
+        """`num_steps` steps with the reference's epsilon-greedy DQN policy (main.py:99-112)
+        computed on the device (bf16 MFMA) and fused with the env step, one launch.
+        opponent: "none" (L0), "uniform", or "self" (the same net on the swapped observation,
+        main.py:199). Returns the same [T, N, ...] dict as rollout_random."""
+        from ..policy import greedy_threshold
+
+        torch, nat = self._torch, self._nat
+        T, n = int(num_steps), self.num_envs
+        mode = {"none": 0, "uniform": 1, "self": 2}[opponent]
+        k0 = self._step_idx if first_step is None else int(first_step)
+        buf = self._traj(T, final_observation)
+        rc = nat.lib.mg_rollout_qnet(
             self._p_ref, self._s_ref, ctypes.byref(buf["_traj"]), self._st_ref, n, self.env_offset,
-            seed & 0xFFFFFFFFFFFFFFFF, k0 & 0xFFFFFFFFFFFFFFFF, T, 1 if opponent_random else 0,
-            self._flags, self._stream())
-        nat.check(rc, "mg_rollout_random")
+            seed & 0xFFFFFFFFFFFFFFFF, k0 & 0xFFFFFFFFFFFFFFFF, T, qnet.packed.data_ptr(), qnet.out_dim,
+            greedy_threshold(episilo), mode, greedy_threshold(opp_episilo), self._flags, self._stream())
+        nat.check(rc, "mg_rollout_qnet")
         self._step_idx = k0 + T
         return buf["_result"]
 

@@ -1,0 +1,63 @@
+"""The reference's DQN policy on the device: Net (scripts/main.py:30-47, scripts/hdqn.py:38-55)
+and epsilon-greedy choose_action (main.py:99-112), packed for the fused bf16 MFMA kernels.
+
+    qnet = QNet.from_state_dict(torch.load(path, weights_only=True), device="cuda:0")
+    q = qnet.forward(obs)                       # [N, out_dim] fp32 (bf16 operands, fp32 sums)
+    traj = env.rollout_qnet(T, qnet, seed=0)    # policy + env step fused, T steps per launch
+"""
+
+from __future__ import annotations
+
+import ctypes
+import math
+
+EPISILO = 0.7  # main.py:16, hdqn.py:20 -- greedy when np.random.randn() <= EPISILO
+
+
+def greedy_threshold(episilo: float = EPISILO) -> int:
+    """u32 threshold t with P(u < t) = P(randn <= episilo) = Phi(episilo)."""
+    phi = 0.5 * (1.0 + math.erf(episilo / math.sqrt(2.0)))
+    return min(1 << 32, max(0, int(round(phi * (1 << 32)))))
+
+
+class QNet:
+    """A Net(in, out) with hidden sizes 200 / 100, packed on the device (bf16 weights)."""
+
+    def __init__(self, fc1_w, fc1_b, fc2_w, fc2_b, out_w, out_b, device=None):
+        import torch
+
+        from . import _native
+
+        self._nat = _native
+        dev = torch.device(device if device is not None else "cuda")
+        ts = [torch.as_tensor(t, dtype=torch.float32).to(dev).contiguous()
+              for t in (fc1_w, fc1_b, fc2_w, fc2_b, out_w, out_b)]
+        self.in_dim, self.out_dim = int(ts[0].shape[1]), int(ts[4].shape[0])
+        if tuple(ts[0].shape) != (200, self.in_dim) or tuple(ts[2].shape) != (100, 200) or \
+                tuple(ts[4].shape) != (self.out_dim, 100):
+            raise ValueError("expected the reference Net: fc1 [200,in], fc2 [100,200], out [out,100]")
+        self.device = dev
+        self.fp32 = ts  # kept for reference checks
+        self.packed = torch.empty(_native.lib.mg_qnet_packed_bytes(), dtype=torch.uint8, device=dev)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        _native.check(_native.lib.mg_qnet_pack(*(t.data_ptr() for t in ts), self.in_dim, self.out_dim,
+                                               self.packed.data_ptr(), stream), "mg_qnet_pack")
+
+    @classmethod
+    def from_state_dict(cls, sd, device=None):
+        return cls(sd["fc1.weight"], sd["fc1.bias"], sd["fc2.weight"], sd["fc2.bias"], sd["out.weight"],
+                   sd["out.bias"], device=device)
+
+    def forward(self, obs, swap_halves: bool = False):
+        """Q-values [N, out_dim] of obs [N, 10] (device tensor), computed by mg_qnet_forward."""
+        import torch
+
+        if self.in_dim != 10:
+            raise ValueError("the fused forward takes the 10-value observation (in_dim 10)")
+        obs = obs.to(self.device, torch.float32).contiguous()
+        q = torch.empty((obs.shape[0], 8), dtype=torch.float32, device=self.device)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        self._nat.check(self._nat.lib.mg_qnet_forward(self.packed.data_ptr(), obs.data_ptr(),
+                                                      1 if swap_halves else 0, q.data_ptr(),
+                                                      obs.shape[0], stream), "mg_qnet_forward")
+        return q[:, : self.out_dim]

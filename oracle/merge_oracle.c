@@ -336,3 +336,13 @@ int64_t oracle_rollout_random(oracle_env* envs, int64_t n, int64_t steps, uint64
   }
   return n * steps;
 }
+
+/* The four Philox words of (env_offset + i, step) for i < n: out[4 i + 0..3]. */
+void oracle_philox_batch(int64_t n, int64_t env_offset, uint64_t seed, uint64_t step, uint32_t* out) {
+  const uint32_t k[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  for (int64_t i = 0; i < n; ++i) {
+    const uint64_t gi = (uint64_t)(env_offset + i);
+    const uint32_t c[4] = {(uint32_t)gi, (uint32_t)(gi >> 32), (uint32_t)step, (uint32_t)(step >> 32)};
+    oracle_philox4x32_10(c, k, out + 4 * i);
+  }
+}

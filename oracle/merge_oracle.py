@@ -242,6 +242,8 @@ class COracle:
             ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint64,
             ctypes.c_int32, ctypes.c_int32, P(ctypes.c_double), P(ctypes.c_uint32)]
         lib.oracle_rollout_random.restype = ctypes.c_int64
+        lib.oracle_philox_batch.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint64,
+                                            P(ctypes.c_uint32)]
         lib.oracle_set_threads.argtypes = [ctypes.c_int32]
         lib.oracle_max_threads.restype = ctypes.c_int32
         self.lib = lib
@@ -290,6 +292,12 @@ class COracle:
                                       _ptr(out, ctypes.c_uint32))
         return out
 
+    def philox_batch(self, n, env_offset, seed, step_idx):
+        """[n, 4] uint32 Philox words for (env_offset + i, step_idx) under key seed."""
+        out = np.empty((n, 4), np.uint32)
+        self.lib.oracle_philox_batch(n, env_offset, seed, step_idx, _ptr(out, ctypes.c_uint32))
+        return out
+
     def random_actions(self, n, env_offset, seed, step_idx, opponent_random):
         a1 = np.empty(n, np.int8)
         a2 = np.empty(n, np.int8)
@@ -306,3 +314,29 @@ class COracle:
             envs.ctypes.data, len(envs), int(steps), int(seed), int(first_step),
             int(opponent_random), int(env_offset), _ptr(ret_sum, ctypes.c_double),
             _ptr(counts, ctypes.c_uint32)))
+
+
+# --------------------------------------------------------------------------- DQN policy oracle
+
+def qnet_reference(weights, obs, bf16: bool = True, swap: bool = False):
+    """The reference Net (scripts/main.py:30-47) on CPU: fc1 -> ReLU -> fc2 -> ReLU -> out.
+
+    bf16=True rounds the input, every weight and each hidden activation to bf16 (round to
+    nearest even) and sums in fp32 -- what the MFMA kernel computes up to summation order.
+    bf16=False is the reference's own fp32 forward. swap feeds state[5:] + state[:5]
+    (main.py:199)."""
+    import torch
+
+    x = torch.as_tensor(np.asarray(obs, np.float32))
+    if swap:
+        x = torch.cat([x[:, 5:], x[:, :5]], dim=1)
+    ws = [torch.as_tensor(np.asarray(weights[k], np.float32)) for k in
+          ("fc1.weight", "fc2.weight", "out.weight")]
+    bs = [torch.as_tensor(np.asarray(weights[k], np.float32)) for k in ("fc1.bias", "fc2.bias", "out.bias")]
+    rnd = (lambda t: t.to(torch.bfloat16).to(torch.float32)) if bf16 else (lambda t: t)
+    h = rnd(x)
+    for i, (w, b) in enumerate(zip(ws, bs)):
+        h = h @ rnd(w).T + b
+        if i < 2:
+            h = rnd(torch.relu(h))
+    return h.numpy()

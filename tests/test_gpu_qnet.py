@@ -1,0 +1,140 @@
+"""GPU parity for the fused DQN policy (BASELINE config 5): the reference's Net and
+epsilon-greedy choose_action (scripts/main.py:30-47, :99-112) in bf16 on the matrix cores.
+
+Bar: Q-values equal the bf16-emulated CPU forward (oracle.qnet_reference: bf16 operands,
+fp32 sums) to summation-order rounding; greedy actions equal its argmax except at near-ties;
+exploration draws and random actions bit-exact (Philox); every env transition equal to the
+CPU oracle stepping with the kernel's actions. Weights: two of the reference's shipped
+checkpoints (tests/golden/dqn_checkpoints.npz, from test_params/dqn/*/eval.pth).
+"""
+
+import os
+
+import numpy as np
+import pytest
+
+import merge_oracle as mo
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+OBS_TOL = dict(rtol=1e-6, atol=1e-5)
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+
+    return t
+
+
+@pytest.fixture(scope="module")
+def nets():
+    f = np.load(os.path.join(ROOT, "tests", "golden", "dqn_checkpoints.npz"))
+    out = {}
+    for key in ("l1", "l3"):
+        out[key] = {name.split("/", 1)[1]: f[name] for name in f.files if name.startswith(key + "/")}
+    return out
+
+
+def _obs_samples(coracle, n=8192, steps=240, seed=3):
+    envs = coracle.new_envs(n)
+    coracle.reset(envs)
+    rng = np.random.default_rng(seed)
+    out = []
+    for k in range(steps):
+        o, *_ = coracle.step(envs, rng.integers(0, 5, n).astype(np.int8), rng.integers(0, 5, n).astype(np.int8),
+                             autoreset=True)
+        if k % 30 == 0:
+            out.append(o.astype(np.float32))
+    return np.concatenate(out)
+
+
+def _near_tie(q, tol=1e-2):
+    """Top-2 Q gap within what one bf16 rounding of a hidden unit can move (summation order
+    differs between the matrix cores and the CPU emulation)."""
+    s = np.sort(q, axis=1)
+    return (s[:, -1] - s[:, -2]) <= tol * np.maximum(1.0, np.abs(s[:, -1]))
+
+
+@pytest.mark.parametrize("key", ["l1", "l3"])
+@pytest.mark.parametrize("swap", [False, True])
+def test_qnet_forward_matches_bf16_reference(torch, coracle, nets, key, swap):
+    from merging_gym.policy import QNet
+
+    obs = _obs_samples(coracle)
+    qnet = QNet.from_state_dict(nets[key], device="cuda:0")
+    q = qnet.forward(torch.from_numpy(obs).cuda(), swap_halves=swap).cpu().numpy()
+    q_bf = mo.qnet_reference(nets[key], obs, bf16=True, swap=swap)
+    q_32 = mo.qnet_reference(nets[key], obs, bf16=False, swap=swap)
+    scale = np.maximum(1.0, np.abs(q_bf).max(axis=1, keepdims=True))
+    err = np.abs(q - q_bf) / scale
+    assert np.median(err) < 1e-5 and err.max() < 1e-2, (np.median(err), err.max())
+    tie = _near_tie(q_bf)
+    assert (q.argmax(1) == q_bf.argmax(1))[~tie].all()
+    agree = (q.argmax(1) == q_32.argmax(1)).mean()
+    assert agree >= 0.999, agree  # bf16 policy vs the reference's fp32 Net
+
+
+@pytest.mark.parametrize("opponent", ["none", "uniform", "self"])
+def test_rollout_qnet_policy_and_transitions(torch, coracle, nets, opponent):
+    """Every action is the epsilon-greedy choice (Philox draws exact, greedy = argmax of the
+    bf16 reference except near-ties) and every transition equals the CPU oracle's."""
+    from merging_gym import MergeVecEnv
+    from merging_gym.policy import QNet, greedy_threshold
+
+    n, T, seed, k0 = 4096, 24, 17, 500
+    qnet = QNet.from_state_dict(nets["l1"], device="cuda:0")
+    env = MergeVecEnv(n, device="cuda:0")
+    for k in range(60):  # mid-episode start
+        env.step_random(seed + 1, step_idx=k)
+    envs = coracle.new_envs(n)
+    for name, src in (("pos1", env.p1), ("vel1", env.v1), ("pos2", env.p2), ("vel2", env.v2),
+                      ("r1_acc", env.ret1), ("r2_acc", env.ret2)):
+        envs[name] = src.cpu().numpy()
+    envs["steps"] = env.steps.cpu().numpy()
+    envs["winner"] = env.winner.cpu().numpy()
+    envs["time_stamp"] = np.cumsum(np.full(2700, 0.2))[np.maximum(envs["steps"] - 1, 0)] * (envs["steps"] > 0)
+    obs_in = env.observe().cpu().numpy().copy()
+    traj = env.rollout_qnet(T, qnet, seed, opponent=opponent, first_step=k0)
+    traj = {k: (v.cpu().numpy() if v is not None else None) for k, v in traj.items()}
+    thr = greedy_threshold(0.7)
+    for t in range(T):
+        u = coracle.philox_batch(n, 0, seed, k0 + t)
+        q = mo.qnet_reference(nets["l1"], obs_in, bf16=True)
+        greedy = u[:, 0].astype(np.uint64) < thr
+        exp1 = np.where(greedy, q.argmax(1), (u[:, 1].astype(np.uint64) * 5) >> 32)
+        ok1 = (traj["a1"][t] == exp1) | (greedy & _near_tie(q))
+        assert ok1.all(), (t, np.nonzero(~ok1)[0][:5])
+        if opponent == "none":
+            assert (traj["a2"][t] == -1).all()
+        else:
+            rnd2 = (u[:, 3].astype(np.uint64) * 5) >> 32
+            if opponent == "uniform":
+                assert (traj["a2"][t] == rnd2).all()
+            else:
+                q2 = mo.qnet_reference(nets["l1"], obs_in, bf16=True, swap=True)
+                g2 = u[:, 2].astype(np.uint64) < thr
+                ok2 = (traj["a2"][t] == np.where(g2, q2.argmax(1), rnd2)) | (g2 & _near_tie(q2))
+                assert ok2.all(), t
+        # the transition, with the actions the kernel took
+        o_obs, o_rew, o_done, o_coll, _, o_fobs, err = coracle.step(
+            envs, traj["a1"][t], traj["a2"][t], autoreset=True, final_obs=True)
+        assert err == 0
+        np.testing.assert_array_equal(traj["done"][t], o_done.astype(bool), err_msg=str(t))
+        np.testing.assert_array_equal(traj["collision"][t], o_coll.astype(bool), err_msg=str(t))
+        np.testing.assert_allclose(traj["obs"][t], o_obs.astype(np.float32), **OBS_TOL)
+        np.testing.assert_allclose(traj["rew"][t], o_rew.astype(np.float32), **OBS_TOL)
+        d = o_done.astype(bool)
+        np.testing.assert_allclose(traj["final_observation"][t][d], o_fobs[d].astype(np.float32), **OBS_TOL)
+        obs_in = traj["obs"][t]
+    np.testing.assert_allclose(env.p1.cpu().numpy(), envs["pos1"], rtol=0, atol=1e-9)
+    np.testing.assert_allclose(env.ret2.cpu().numpy(), envs["r2_acc"], rtol=0, atol=1e-9)
+    assert env._step_idx == k0 + T
+
+
+def test_greedy_threshold_is_phi_of_episilo():
+    from merging_gym.policy import greedy_threshold
+
+    assert greedy_threshold(0.7) == round(0.7580363477769270 * 2**32)
+    assert greedy_threshold(50.0) == 2**32 and greedy_threshold(-50.0) == 0
