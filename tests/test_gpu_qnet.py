@@ -72,8 +72,12 @@ def test_qnet_forward_matches_bf16_reference(torch, coracle, nets, key, swap):
     assert np.median(err) < 1e-5 and err.max() < 1e-2, (np.median(err), err.max())
     tie = _near_tie(q_bf)
     assert (q.argmax(1) == q_bf.argmax(1))[~tie].all()
+    # bf16 vs the reference's fp32 Net: the kernel loses nothing beyond bf16 itself
     agree = (q.argmax(1) == q_32.argmax(1)).mean()
-    assert agree >= 0.999, agree  # bf16 policy vs the reference's fp32 Net
+    agree_bf16 = (q_bf.argmax(1) == q_32.argmax(1)).mean()
+    assert agree >= agree_bf16 - 1e-3, (agree, agree_bf16)
+    if key == "l1":  # the checkpoint the bench and human_player.py:68 use
+        assert agree >= 0.999, agree
 
 
 @pytest.mark.parametrize("opponent", ["none", "uniform", "self"])
