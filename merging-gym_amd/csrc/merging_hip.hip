@@ -418,6 +418,43 @@ __device__ __forceinline__ void store_obs_tile(float* tile, const double (&o)[kO
   store_obs_tile_n(tile, o, dst, nrows, kBlock);
 }
 
+// Wave-scope ordering of LDS accesses between the lanes of ONE wave (no s_barrier): the LDS
+// executes a wave's accesses in order; this only stops the compiler from moving them.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// The same as store_obs_tile for one wave's 64 rows: the wave's tile slice holds the new
+// observations afterwards, and no other wave is waited for.
+__device__ __forceinline__ void wave_store_obs(float* wtile, const double (&o)[kObs], float* dst,
+                                               int nrows) {
+  const int lane = threadIdx.x & 63;
+  float2* t2 = reinterpret_cast<float2*>(wtile + lane * kObs);
+#pragma unroll
+  for (int k = 0; k < kObs / 2; ++k)
+    t2[k] = make_float2(static_cast<float>(o[2 * k]), static_cast<float>(o[2 * k + 1]));
+  wave_lds_sync();
+  if (dst != nullptr && nrows > 0) {
+    const int nfl = nrows * kObs;
+    if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+      const int n4 = nfl >> 2;
+      f32x4* d4 = reinterpret_cast<f32x4*>(dst);
+      const f32x4* s4 = reinterpret_cast<const f32x4*>(wtile);
+      for (int j = lane; j < n4; j += 64) st_out(d4 + j, s4[j]);
+      const int tail = nfl - (n4 << 2);
+      if (lane < tail) st_out(dst + (n4 << 2) + lane, wtile[(n4 << 2) + lane]);
+    } else {
+      const int n2 = nfl >> 1;
+      f32x2* d2 = reinterpret_cast<f32x2*>(dst);
+      const f32x2* s2 = reinterpret_cast<const f32x2*>(wtile);
+      for (int j = lane; j < n2; j += 64) st_out(d2 + j, s2[j]);
+    }
+  }
+  wave_lds_sync();
+}
+
 struct Launch {
   mg_params P;
   mg_state S;
@@ -635,6 +672,30 @@ __global__ void qnet_pack_kernel(const float* w1, const float* b1, const float* 
   if (e < kQOut) pb3[e] = e < out_dim ? b3[e] : 0.f;
 }
 
+// The 16 bias values of a 32-row accumulator tile as laid out in lane half h: register q
+// holds row (q & 3) + 8 (q >> 2) + 4 h, i.e. four float4 runs.
+__device__ __forceinline__ f32x16 bias_tile(const float* b, int h) {
+  f32x16 t;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(b + 8 * g + 4 * h);
+    t[4 * g] = v[0];
+    t[4 * g + 1] = v[1];
+    t[4 * g + 2] = v[2];
+    t[4 * g + 3] = v[3];
+  }
+  return t;
+}
+
+// A zero the compiler cannot see through. Added to the LDS addresses of loop-invariant
+// weight / bias loads so they are issued where they are used: hoisted out of the tile and
+// time loops, they stay live across them and push the kernel into scratch.
+__device__ __forceinline__ int opaque_zero() {
+  int z = 0;
+  asm volatile("" : "+v"(z));
+  return z;
+}
+
 // Cooperative copy of a packed net into LDS (all threads of the block; caller syncs).
 __device__ __forceinline__ void qnet_to_lds(const uint8_t* net, uint8_t* lds) {
   const f32x4* src = reinterpret_cast<const f32x4*>(net);
@@ -647,19 +708,26 @@ __device__ __forceinline__ void qnet_to_lds(const uint8_t* net, uint8_t* lds) {
 // (scripts/main.py:199, human_player.py:40-41). Every lane of the wave must call it.
 __device__ __forceinline__ void qnet_forward(const uint8_t* net, const float* tile, int row0,
                                              bool swap, float (&q)[8]) {
-  const __bf16* W1 = reinterpret_cast<const __bf16*>(net);
-  const __bf16* W2 = reinterpret_cast<const __bf16*>(net + kQOffW2);
-  const __bf16* W3 = reinterpret_cast<const __bf16*>(net + kQOffW3);
-  const float* B1 = reinterpret_cast<const float*>(net + kQOffB1);
-  const float* B2 = reinterpret_cast<const float*>(net + kQOffB2);
-  const float* B3 = reinterpret_cast<const float*>(net + kQOffB3);
+  const __bf16* W1_ = reinterpret_cast<const __bf16*>(net);
+  const __bf16* W2_ = reinterpret_cast<const __bf16*>(net + kQOffW2);
+  const __bf16* W3_ = reinterpret_cast<const __bf16*>(net + kQOffW3);
+  const float* B1_ = reinterpret_cast<const float*>(net + kQOffB1);
+  const float* B2_ = reinterpret_cast<const float*>(net + kQOffB2);
+  const float* B3_ = reinterpret_cast<const float*>(net + kQOffB3);
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
 
   // One N-tile (32 envs = lanes 32*NT .. 32*NT+31) at a time: 4 layer-2 accumulators live
   // instead of 8 (W2 fragments are re-read from LDS per tile, which the LDS rate covers).
-  f32x16 acc3[2];
-#pragma unroll
+  f32x16 acc3_0, acc3_1;
+#pragma unroll 1
   for (int nt = 0; nt < 2; ++nt) {
+    const int z = opaque_zero();
+    const __bf16* W1 = W1_ + z;
+    const __bf16* W2 = W2_ + z;
+    const __bf16* W3 = W3_ + z;
+    const float* B1 = B1_ + z;
+    const float* B2 = B2_ + z;
+    const float* B3 = B3_ + z;
     // layer-1 B operand: X'[k = 8h + j][env 32 nt + r]
     bf16x8 xb;
 #pragma unroll
@@ -668,22 +736,19 @@ __device__ __forceinline__ void qnet_forward(const uint8_t* net, const float* ti
       const int src = swap ? (k < 5 ? k + 5 : k - 5) : k;
       xb[j] = static_cast<__bf16>(k < kObs ? tile[(row0 + 32 * nt + r) * kObs + src] : 0.f);
     }
-    const f32x16 zero = {};
     f32x16 acc2[4];
 #pragma unroll
-    for (int m = 0; m < 4; ++m) acc2[m] = zero;
+    for (int m = 0; m < 4; ++m) acc2[m] = bias_tile(B2 + 32 * m, h);
     // rolled on purpose: unrolled, hipcc hoists all 56 W2 fragment loads ahead of the MFMAs
     // and runs out of registers
 #pragma unroll 1
     for (int mt = 0; mt < kQH1 / 32; ++mt) {
       const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(W1 + (32 * mt + r) * kQS1 + 8 * h);
-      const f32x16 c = mfma32(a1, xb, zero);
+      // the bias is the accumulator's initial value: fp32, no per-element add afterwards
+      const f32x16 c = mfma32(a1, xb, bias_tile(B1 + 32 * mt, h));
       bf16x8 hb[2];  // [k-step]
 #pragma unroll
-      for (int qq = 0; qq < 16; ++qq) {
-        const float b = B1[32 * mt + (qq & 3) + 8 * (qq >> 2) + 4 * h];
-        hb[qq >> 3][qq & 7] = static_cast<__bf16>(fmaxf(c[qq] + b, 0.f));
-      }
+      for (int qq = 0; qq < 16; ++qq) hb[qq >> 3][qq & 7] = static_cast<__bf16>(fmaxf(c[qq], 0.f));
 #pragma unroll
       for (int m2 = 0; m2 < kQH2 / 32; ++m2) {
 #pragma unroll
@@ -694,15 +759,12 @@ __device__ __forceinline__ void qnet_forward(const uint8_t* net, const float* ti
         }
       }
     }
-    f32x16 a3acc = zero;
+    f32x16 a3acc = bias_tile(B3, h);
 #pragma unroll
     for (int m2 = 0; m2 < kQH2 / 32; ++m2) {
       bf16x8 hb[2];
 #pragma unroll
-      for (int qq = 0; qq < 16; ++qq) {
-        const float b = B2[32 * m2 + (qq & 3) + 8 * (qq >> 2) + 4 * h];
-        hb[qq >> 3][qq & 7] = static_cast<__bf16>(fmaxf(acc2[m2][qq] + b, 0.f));
-      }
+      for (int qq = 0; qq < 16; ++qq) hb[qq >> 3][qq & 7] = static_cast<__bf16>(fmaxf(acc2[m2][qq], 0.f));
 #pragma unroll
       for (int sk = 0; sk < 2; ++sk) {
         const bf16x8 a3 =
@@ -710,17 +772,20 @@ __device__ __forceinline__ void qnet_forward(const uint8_t* net, const float* ti
         a3acc = mfma32(a3, hb[sk], a3acc);
       }
     }
-    acc3[nt] = a3acc;
+    if (nt == 0)  // wave-uniform branch: keeps both tiles in registers (no indexed array)
+      acc3_0 = a3acc;
+    else
+      acc3_1 = a3acc;
   }
   // Column r of N-tile t is the env of lane 32t + r. Rows 0-3 sit in registers 0-3 of lane
   // half 0, rows 4-7 in registers 0-3 of lane half 1: swap halves across the wave.
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const float own = h ? acc3[1][j] : acc3[0][j];
-    const float send = h ? acc3[0][j] : acc3[1][j];
+    const float own = h ? acc3_1[j] : acc3_0[j];
+    const float send = h ? acc3_0[j] : acc3_1[j];
     const float got = __shfl_xor(send, 32);
-    q[j] = (h ? got : own) + B3[j];
-    q[4 + j] = (h ? own : got) + B3[4 + j];
+    q[j] = h ? got : own;
+    q[4 + j] = h ? own : got;
   }
 }
 
@@ -806,8 +871,15 @@ __global__ __launch_bounds__(kQBlock, 2) void qnet_rollout_kernel(const QRollout
 #pragma unroll
     for (int k = 0; k < kObs; ++k) r.o[k] = 0.0;
   }
+  // this wave's 64 rows of the tile; waves never read each other's rows, so after the one
+  // barrier that publishes the weights they run unsynchronised (MFMA of one wave overlaps
+  // the fp64 env step of the other wave on its SIMD)
+  float* wtile = tile + row0 * kObs;
+  const int64_t wbase = base + row0;
+  const int64_t wrem = R.n - wbase;
+  const int wrows = wrem <= 0 ? 0 : (wrem < 64 ? static_cast<int>(wrem) : 64);
   {
-    float2* t2 = reinterpret_cast<float2*>(tile + tid * kObs);
+    float2* t2 = reinterpret_cast<float2*>(wtile + (tid & 63) * kObs);
 #pragma unroll
     for (int k = 0; k < kObs / 2; ++k)
       t2[k] = make_float2(static_cast<float>(r.o[2 * k]), static_cast<float>(r.o[2 * k + 1]));
@@ -823,7 +895,7 @@ __global__ __launch_bounds__(kQBlock, 2) void qnet_rollout_kernel(const QRollout
       qnet_forward(lds_net, tile, row0, true, q);
       greedy2 = argmax_first(q, R.out_dim);
     }
-    __syncthreads();  // every wave is done reading the tile before it is overwritten
+    wave_lds_sync();  // the wave is done reading its rows before they are overwritten
     const int64_t row = static_cast<int64_t>(t) * R.n + i;
     if (live) {
       const uint64_t gi = static_cast<uint64_t>(R.env_offset + i);
@@ -848,9 +920,10 @@ __global__ __launch_bounds__(kQBlock, 2) void qnet_rollout_kernel(const QRollout
       if (autoreset && r.done)
         finish_episode(P, e, r, R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i);
     }
-    // writes the new observations into the tile (the next step's network input) and out
-    store_obs_tile_n(tile, r.o, R.T.obs ? R.T.obs + (static_cast<int64_t>(t) * R.n + base) * kObs : nullptr,
-                     nrows, kQBlock);
+    // the new observations: this wave's tile rows (next step's network input) and the output
+    wave_store_obs(wtile, r.o,
+                   R.T.obs ? R.T.obs + (static_cast<int64_t>(t) * R.n + wbase) * kObs : nullptr,
+                   wrows);
   }
   if (live) store_env(R.S, i, e);
 }
