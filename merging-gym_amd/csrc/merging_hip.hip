@@ -853,8 +853,6 @@ __global__ __launch_bounds__(kQBlock, 2) void qnet_rollout_kernel(const QRollout
   const int64_t base = static_cast<int64_t>(blockIdx.x) * kQBlock;
   const int64_t i = base + tid;
   const bool live = i < R.n;
-  const int64_t rem = R.n - base;
-  const int nrows = rem < kQBlock ? static_cast<int>(rem) : kQBlock;
   const bool autoreset = (R.flags & MG_AUTORESET) != 0;
   const int row0 = (tid >> 6) * 64;
 
