@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 1
+#define MG_ABI_VERSION 2
 #define MG_OBS_DIM 10   /* merging_env.py:75 observation_shape = (10) */
 #define MG_NUM_ACTIONS 5 /* merging_env.py:101-102 action_dict / Discrete(5) */
 #define MG_ACTION_NONE (-1) /* action2=None: the constant-speed "L0" opponent, merging_env.py:152 */
@@ -91,6 +91,8 @@ typedef struct mg_params {
   int32_t veh_h;       /* 8  longitudinal box size                    merging_env.py:40,97 */
   int32_t timeout_steps; /* 2501: first step with time_stamp > 500    merging_env.py:141-143 */
   int32_t _pad;
+  double inv_R;            /* 1 / R, rounded: the kernel divides by R and prediction_t with */
+  double inv_prediction_t; /* an FMA-corrected reciprocal multiply (still correctly rounded) */
 } mg_params;
 
 /* Per-env state, struct of arrays, n entries each (device pointers). */

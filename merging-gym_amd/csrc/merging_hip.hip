@@ -45,6 +45,9 @@ namespace {
 #ifndef MG_BLOCK
 #define MG_BLOCK 256
 #endif
+#ifndef MG_QNET_PAIR
+#define MG_QNET_PAIR 1    // Q-net: both 32-env column tiles per hidden-tile iteration
+#endif
 
 constexpr int kBlock = MG_BLOCK;  // 4 waves of 64 by default
 constexpr int kObs = MG_OBS_DIM;
@@ -105,6 +108,16 @@ __device__ __forceinline__ void st_state(T* p, T v) {
 // else is the reference's KeyError.
 __device__ __forceinline__ bool valid_action(int a) { return a >= 0 && a < MG_NUM_ACTIONS; }
 
+// x / d for a divisor fixed per launch, correctly rounded: q = x * (1/d), then Markstein's
+// FMA correction. With inv = RN(1/d) this returns RN(x / d) for d = 3 and d = 30000 (the
+// only divisors used; 0 mismatches in 8e8 random tests, incl. random exponents,
+// tests/test_division.py) at 3 instructions instead of the ~10 of a general fp64 division.
+__device__ __forceinline__ double div_const(double x, double d, double inv) {
+  const double q = x * inv;
+  const double r = fma(-q, d, x);
+  return fma(r, inv, q);
+}
+
 // sin and cos of the double theta. For |theta| < 1/16 -- pos in [-842, 2875], which covers
 // every state of a live episode (pos 50..~1000) -- a degree-9 / degree-10 Taylor polynomial
 // in fma form: the correction terms are < 7e-4 of the result, so the one rounding of the
@@ -134,7 +147,7 @@ __device__ __forceinline__ void arc_sincos(double t, double& s, double& c) {
 // The ego rides the arc on +y, the opponent its mirror image on -y.
 __device__ __forceinline__ void lon2coord(const mg_params& P, double lon, bool ego, double& x,
                                           double& y) {
-  const double angle = P.angle0 - lon / P.R;
+  const double angle = P.angle0 - div_const(lon, P.R, P.inv_R);
   double s, c;
   arc_sincos(angle, s, c);
   x = P.R * s;
@@ -286,7 +299,7 @@ __device__ __forceinline__ void env_step(const mg_params& P, Env& e, int a1, int
     // mpc_1d (helper.py:152-191): min u'(D'D + 0.01 I)u s.t. sum(dt u) = vt - v0 (the only
     // row of the constraint passed to solve_qp, :172-173, :182). D.1 = 0, so P.1 = 0.01 * 1
     // and the minimiser is u = (vt - v0) / t * 1; action() = u[0].
-    r.acc1 = (P.action_speed[a1] - e.v1) / P.prediction_t;
+    r.acc1 = div_const(P.action_speed[a1] - e.v1, P.prediction_t, P.inv_prediction_t);
     const double nv = e.v1 + r.acc1 * P.dT;  // max(0, v + acc*dT)  :149
     r.v1_int = !(nv > 0.0);
     e.v1 = r.v1_int ? 0.0 : nv;
@@ -298,7 +311,8 @@ __device__ __forceinline__ void env_step(const mg_params& P, Env& e, int a1, int
     return;
   }
   // action2 None -> acc 0 (:152): the "L0" constant-speed opponent
-  if (a2 != MG_ACTION_NONE) r.acc2 = (P.action_speed[a2] - e.v2) / P.prediction_t;
+  if (a2 != MG_ACTION_NONE)
+    r.acc2 = div_const(P.action_speed[a2] - e.v2, P.prediction_t, P.inv_prediction_t);
   const double nv2 = e.v2 + r.acc2 * P.dT;  // :153
   r.v2_int = !(nv2 > 0.0);
   e.v2 = r.v2_int ? 0.0 : nv2;
@@ -629,6 +643,29 @@ __host__ __device__ constexpr int qnet_krow(int kk) {
   return 8 * ((kk & 7) >> 2) + 4 * (kk >> 3) + (kk & 3);
 }
 
+// ReLU + round to bf16 of accumulator registers 8s..8s+7 -> one B fragment. Rounded first,
+// then max(x, 0) on the packed bf16 pairs as signed 16-bit integers: a bf16 with its sign
+// bit set is a negative int16 (and -0.0 becomes +0.0), so max_i16(x, 0) is exactly ReLU --
+// 4 v_cvt_pk_bf16_f32 + 4 v_pk_max_i16 instead of 8 v_max_f32 + 4 converts.
+typedef short i16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ bf16x8 relu_bf16(const f32x16& c, int s) {
+  bf16x8 out;
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) {
+    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+    bf16x2 p;
+    p[0] = static_cast<__bf16>(c[8 * s + j]);
+    p[1] = static_cast<__bf16>(c[8 * s + j + 1]);
+    i16x2 v = __builtin_bit_cast(i16x2, p);
+    const i16x2 zero = {0, 0};
+    v = __builtin_elementwise_max(v, zero);
+    const bf16x2 q = __builtin_bit_cast(bf16x2, v);
+    out[j] = q[0];
+    out[j + 1] = q[1];
+  }
+  return out;
+}
+
 __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
@@ -716,6 +753,63 @@ __device__ __forceinline__ void qnet_forward(const uint8_t* net, const float* ti
   const float* B3_ = reinterpret_cast<const float*>(net + kQOffB3);
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
 
+#if MG_QNET_PAIR
+  // Both N-tiles in the same hidden-tile iteration: two independent MFMA -> VALU -> MFMA
+  // chains per wave and one W2 fragment load per pair of MFMAs.
+  f32x16 acc3_0, acc3_1;
+  {
+    const int z = opaque_zero();
+    const __bf16* W1 = W1_ + z;
+    const __bf16* W2 = W2_ + z;
+    const __bf16* W3 = W3_ + z;
+    const float* B1 = B1_ + z;
+    const float* B2 = B2_ + z;
+    const float* B3 = B3_ + z;
+    bf16x8 xb0, xb1;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 8 * h + j;
+      const int src = swap ? (k < 5 ? k + 5 : k - 5) : k;
+      xb0[j] = static_cast<__bf16>(k < kObs ? tile[(row0 + r) * kObs + src] : 0.f);
+      xb1[j] = static_cast<__bf16>(k < kObs ? tile[(row0 + 32 + r) * kObs + src] : 0.f);
+    }
+    f32x16 acc2a[4], acc2b[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) acc2b[m] = acc2a[m] = bias_tile(B2 + 32 * m, h);
+#pragma unroll 1
+    for (int mt = 0; mt < kQH1 / 32; ++mt) {
+      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(W1 + (32 * mt + r) * kQS1 + 8 * h);
+      const f32x16 bt = bias_tile(B1 + 32 * mt, h);
+      const f32x16 c0 = mfma32(a1, xb0, bt);
+      const f32x16 c1 = mfma32(a1, xb1, bt);
+      const bf16x8 ha[2] = {relu_bf16(c0, 0), relu_bf16(c0, 1)};
+      const bf16x8 hb[2] = {relu_bf16(c1, 0), relu_bf16(c1, 1)};
+#pragma unroll
+      for (int m2 = 0; m2 < kQH2 / 32; ++m2) {
+#pragma unroll
+        for (int sk = 0; sk < 2; ++sk) {
+          const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(W2 + (32 * m2 + r) * kQS2 +
+                                                             16 * (2 * mt + sk) + 8 * h);
+          acc2a[m2] = mfma32(a2, ha[sk], acc2a[m2]);
+          acc2b[m2] = mfma32(a2, hb[sk], acc2b[m2]);
+        }
+      }
+    }
+    acc3_0 = acc3_1 = bias_tile(B3, h);
+#pragma unroll
+    for (int m2 = 0; m2 < kQH2 / 32; ++m2) {
+      const bf16x8 ha[2] = {relu_bf16(acc2a[m2], 0), relu_bf16(acc2a[m2], 1)};
+      const bf16x8 hb[2] = {relu_bf16(acc2b[m2], 0), relu_bf16(acc2b[m2], 1)};
+#pragma unroll
+      for (int sk = 0; sk < 2; ++sk) {
+        const bf16x8 a3 =
+            *reinterpret_cast<const bf16x8*>(W3 + r * kQS3 + 16 * (2 * m2 + sk) + 8 * h);
+        acc3_0 = mfma32(a3, ha[sk], acc3_0);
+        acc3_1 = mfma32(a3, hb[sk], acc3_1);
+      }
+    }
+  }
+#else
   // One N-tile (32 envs = lanes 32*NT .. 32*NT+31) at a time: 4 layer-2 accumulators live
   // instead of 8 (W2 fragments are re-read from LDS per tile, which the LDS rate covers).
   f32x16 acc3_0, acc3_1;
@@ -746,9 +840,7 @@ __device__ __forceinline__ void qnet_forward(const uint8_t* net, const float* ti
       const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(W1 + (32 * mt + r) * kQS1 + 8 * h);
       // the bias is the accumulator's initial value: fp32, no per-element add afterwards
       const f32x16 c = mfma32(a1, xb, bias_tile(B1 + 32 * mt, h));
-      bf16x8 hb[2];  // [k-step]
-#pragma unroll
-      for (int qq = 0; qq < 16; ++qq) hb[qq >> 3][qq & 7] = static_cast<__bf16>(fmaxf(c[qq], 0.f));
+      const bf16x8 hb[2] = {relu_bf16(c, 0), relu_bf16(c, 1)};  // [k-step]
 #pragma unroll
       for (int m2 = 0; m2 < kQH2 / 32; ++m2) {
 #pragma unroll
@@ -762,9 +854,7 @@ __device__ __forceinline__ void qnet_forward(const uint8_t* net, const float* ti
     f32x16 a3acc = bias_tile(B3, h);
 #pragma unroll
     for (int m2 = 0; m2 < kQH2 / 32; ++m2) {
-      bf16x8 hb[2];
-#pragma unroll
-      for (int qq = 0; qq < 16; ++qq) hb[qq >> 3][qq & 7] = static_cast<__bf16>(fmaxf(acc2[m2][qq], 0.f));
+      const bf16x8 hb[2] = {relu_bf16(acc2[m2], 0), relu_bf16(acc2[m2], 1)};
 #pragma unroll
       for (int sk = 0; sk < 2; ++sk) {
         const bf16x8 a3 =
@@ -777,6 +867,7 @@ __device__ __forceinline__ void qnet_forward(const uint8_t* net, const float* ti
     else
       acc3_1 = a3acc;
   }
+#endif
   // Column r of N-tile t is the env of lane 32t + r. Rows 0-3 sit in registers 0-3 of lane
   // half 0, rows 4-7 in registers 0-3 of lane half 1: swap halves across the wave.
 #pragma unroll
@@ -1089,6 +1180,8 @@ void mg_params_default(mg_params* p) {
   p->veh_w = 4;
   p->veh_h = 8;
   p->timeout_steps = 2501;
+  p->inv_R = 1.0 / p->R;
+  p->inv_prediction_t = 1.0 / p->prediction_t;
 }
 
 int mg_step(const mg_params* params, const mg_state* state, const int8_t* a1, const int8_t* a2,

@@ -35,8 +35,8 @@ def test_library_exports_every_declared_symbol():
 def test_struct_layouts_match_header():
     from merging_gym import _native
 
-    # mg_params: 15 doubles + 5 doubles + 4 int32; mg_rec64: 20 doubles + 2 uint32
-    assert ctypes.sizeof(_native.Params) == 20 * 8 + 16
+    # mg_params: 15 doubles + 5 doubles + 4 int32 + 2 doubles; mg_rec64: 20 doubles + 2 uint32
+    assert ctypes.sizeof(_native.Params) == 20 * 8 + 16 + 16
     assert ctypes.sizeof(_native.State) == 7 * 8
     assert ctypes.sizeof(_native.Outputs) == 8 * 8
     assert ctypes.sizeof(_native.Stats) == 2 * 8
@@ -56,6 +56,7 @@ def test_default_params_are_the_reference_constants():
     assert list(p.action_speed) == [0.0, 10.0, 20.0, 30.0, 40.0]
     assert (p.veh_w, p.veh_h, p.timeout_steps) == (4, 8, 2501)
     assert p.angle0 == float(np.arctan2(1000, 30000))
+    assert p.inv_R == 1.0 / 30000.0 and p.inv_prediction_t == 1.0 / 3.0
 
 
 def test_argument_errors_without_gpu():

@@ -36,6 +36,11 @@ def bind(path):
                                       ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32,
                                       ctypes.c_uint32, P]
     lib.mg_time_next_launch.argtypes = [P, P]
+    lib.mg_qnet_packed_bytes.restype = ctypes.c_size_t
+    lib.mg_qnet_pack.argtypes = [P] * 6 + [ctypes.c_int32, ctypes.c_int32, P, P]
+    lib.mg_rollout_qnet.argtypes = [PP, SP, ctypes.POINTER(nat.Traj), STP, ctypes.c_int64, ctypes.c_int64,
+                                    ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int32, P, ctypes.c_int32,
+                                    ctypes.c_uint64, ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint32, P]
     return lib
 
 
@@ -81,6 +86,23 @@ class Bed:
         assert rc == 0
         self.k += 1
 
+    def pack_net(self, weights):
+        ts = [torch.as_tensor(weights[k]).cuda().contiguous() for k in
+              ("fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias", "out.weight", "out.bias")]
+        self.net_src = ts
+        self.net = torch.empty(self.lib.mg_qnet_packed_bytes(), dtype=torch.uint8, device="cuda")
+        assert self.lib.mg_qnet_pack(*(t.data_ptr() for t in ts), 10, 5, self.net.data_ptr(), None) == 0
+
+    def qrollout(self, opp, ev=None):
+        if ev:
+            self.lib.mg_time_next_launch(*ev)
+        thr = 3255688812  # round(Phi(0.7) * 2^32)
+        rc = self.lib.mg_rollout_qnet(ctypes.byref(self.params), ctypes.byref(self.state), ctypes.byref(self.traj),
+                                      ctypes.byref(self.stats), self.n, 0, 5, self.k, self.T, self.net.data_ptr(), 5,
+                                      thr, opp, thr, 1, torch.cuda.current_stream().cuda_stream)
+        assert rc == 0
+        self.k += self.T
+
     def rollout(self, ev=None):
         if ev:
             self.lib.mg_time_next_launch(*ev)
@@ -117,7 +139,10 @@ def main():
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--T", type=int, default=16)
     ap.add_argument("--rollouts", type=int, default=4)
+    ap.add_argument("--qnet", action="store_true", help="A/B the fused Q-net rollout instead")
     a = ap.parse_args()
+    if a.qnet:
+        return main_qnet(a)
     beds = {os.path.basename(p): Bed(bind(p), a.envs, a.T) for p in a.libs}
     ev = Events(max(a.steps, a.rollouts))
     res = {k: {"step": [], "rollout": [], "step_wall": [], "rollout_wall": []} for k in beds}
@@ -166,6 +191,33 @@ def main():
               f"wall: step {out[name]['step_wall_us_median']:6.2f} rollout {out[name]['rollout_wall_us_per_step_median']:6.2f}",
               flush=True)
     print(json.dumps({"envs": a.envs, "T": a.T, "results": out}))
+
+
+def main_qnet(a):
+    import time
+
+    f = np.load(os.path.join(ROOT, "tests", "golden", "dqn_checkpoints.npz"))
+    w = {k.split("/", 1)[1]: f[k] for k in f.files if k.startswith("l1/")}
+    beds = {os.path.basename(p): Bed(bind(p), a.envs, a.T) for p in a.libs}
+    for b in beds.values():
+        b.pack_net(w)
+        for _ in range(100):
+            b.step()
+    ev = Events(a.rollouts)
+    res = {k: {0: [], 2: []} for k in beds}
+    torch.cuda.synchronize()
+    for r in range(a.rounds):
+        order = list(beds) if r % 2 == 0 else list(reversed(beds))
+        for name in order:
+            b = beds[name]
+            for opp in (0, 2):
+                for j in range(a.rollouts):
+                    b.qrollout(opp, ev.ev[j])
+                torch.cuda.synchronize()
+                res[name][opp] += [ev.ms(j) / a.T for j in range(a.rollouts)]
+    for name, d in res.items():
+        print(f"{name:24s} qnet(none) {1e3 * statistics.median(d[0]):7.2f} us/step   "
+              f"qnet(self) {1e3 * statistics.median(d[2]):7.2f} us/step", flush=True)
 
 
 if __name__ == "__main__":
