@@ -188,6 +188,40 @@ def qnet_leg(env, args, world, dist, torch, opponent):
             "frac_useful": nets * QNET_USEFUL_FLOP * per_s / 1e12 / MFMA_BF16_PEAK_TFLOPS}
 
 
+def dropin_leg(seed: int):
+    """BASELINE config 1: merging_gym.make('merging-v0') single env, 500 step() calls with
+    uniform random actions for both players, reset on done. The GPU-backed drop-in (one
+    launch + one 168-byte copy back per step) is timed next to the pure-Python restatement of
+    the reference's step (oracle.PyMergeEnv, numpy sin/cos + the QP solved per car-step) on
+    the same action sequence; the reference itself measured 5,090 steps/s in the survey
+    container."""
+    import numpy as np
+
+    import merging_gym
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import merge_oracle
+
+    rng = np.random.default_rng(seed)
+    acts = rng.integers(0, 5, (500, 2)).tolist()
+    out = {}
+    for name, env in (("gpu_dropin", merging_gym.make("merging-v0")), ("cpu_python_port", merge_oracle.PyMergeEnv())):
+        env.reset()
+        env.step(0, 0)
+        env.reset()
+        episodes = 0
+        t0 = time.perf_counter()
+        for a1, a2 in acts:
+            _, _, done, _ = env.step(a1, a2)
+            if done:
+                env.reset()
+                episodes += 1
+        dt = time.perf_counter() - t0
+        out[name] = {"steps_per_s": 500 / dt, "us_per_step": dt / 500 * 1e6, "episodes_finished": episodes}
+    out["workload"] = "config 1: one env, 500 random-action step() calls, reset on done (list API)"
+    return out
+
+
 def main():
     args = parse()
     import torch
@@ -304,6 +338,7 @@ def main():
         if qnet is not None:
             line["qnet_policy"] = qnet
         if world == 1 and not args.no_cpu_baseline:
+            line["dropin_single_env"] = dropin_leg(args.seed)
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         print(json.dumps(line), flush=True)
     if world > 1:

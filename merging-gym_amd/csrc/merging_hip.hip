@@ -550,7 +550,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const Launch L) {
     if ((tid & 63) == 0 && live) L.O.done_mask[i >> 6] = m;
   }
   if constexpr (!OUT64) {
-    if (L.O.obs) {
+    if (L.O.obs) {  // one launch per step: block staging measured as fast as per-wave staging
       const int64_t rem = L.n - base;
       store_obs_tile(obs_tile, r.o, L.O.obs + base * kObs, rem < kBlock ? static_cast<int>(rem) : kBlock);
     }
@@ -581,8 +581,9 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(const Rollout R) {
   const int64_t base = static_cast<int64_t>(blockIdx.x) * kBlock;
   const int64_t i = base + tid;
   const bool live = i < R.n;
-  const int64_t rem = R.n - base;
-  const int nrows = rem < kBlock ? static_cast<int>(rem) : kBlock;
+  const int64_t wbase = base + (tid & ~63);
+  const int64_t wrem = R.n - wbase;
+  const int wrows = wrem <= 0 ? 0 : (wrem < 64 ? static_cast<int>(wrem) : 64);
   const bool autoreset = (R.flags & MG_AUTORESET) != 0;
 
   Env e;
@@ -605,8 +606,9 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(const Rollout R) {
       if (autoreset && r.done)
         finish_episode(P, e, r, R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i);
     }
-    if (R.T.obs)
-      store_obs_tile(obs_tile, r.o, R.T.obs + (static_cast<int64_t>(t) * R.n + base) * kObs, nrows);
+    if (R.T.obs)  // staged per wave: waves never wait for each other
+      wave_store_obs(obs_tile + (tid & ~63) * kObs, r.o,
+                     R.T.obs + (static_cast<int64_t>(t) * R.n + wbase) * kObs, wrows);
   }
   if (live) store_env(R.S, i, e);
 }

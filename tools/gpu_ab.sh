@@ -4,5 +4,5 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 V=merging-gym_amd/variants
-echo "== ab qnet 2^20" && timeout -k 10 300 python tools/ab_kernels.py $V/lib_*.so --qnet --rounds 4 --rollouts 3 > gpurun_out/abq.log 2>&1; rc=$?; tail -4 gpurun_out/abq.log | cut -c1-230; [ $rc -eq 0 ] \
+true \
 && echo "== ab step/rollout 2^20" && timeout -k 10 300 python tools/ab_kernels.py $V/lib_*.so --rounds 6 > gpurun_out/ab1.log 2>&1 && tail -4 gpurun_out/ab1.log | cut -c1-230
