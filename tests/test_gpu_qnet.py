@@ -80,14 +80,16 @@ def test_qnet_forward_matches_bf16_reference(torch, coracle, nets, key, swap):
         assert agree >= 0.999, agree
 
 
-@pytest.mark.parametrize("opponent", ["none", "uniform", "self"])
-def test_rollout_qnet_policy_and_transitions(torch, coracle, nets, opponent):
+@pytest.mark.parametrize("opponent,n", [("none", 4096), ("uniform", 4096), ("self", 4096),
+                                        ("none", 1000), ("self", 577)])
+def test_rollout_qnet_policy_and_transitions(torch, coracle, nets, opponent, n):
     """Every action is the epsilon-greedy choice (Philox draws exact, greedy = argmax of the
-    bf16 reference except near-ties) and every transition equals the CPU oracle's."""
+    bf16 reference except near-ties) and every transition equals the CPU oracle's. The odd
+    sizes leave partial waves / a partial block and unaligned trajectory rows."""
     from merging_gym import MergeVecEnv
     from merging_gym.policy import QNet, greedy_threshold
 
-    n, T, seed, k0 = 4096, 24, 17, 500
+    T, seed, k0 = 24, 17, 500
     qnet = QNet.from_state_dict(nets["l1"], device="cuda:0")
     env = MergeVecEnv(n, device="cuda:0")
     for k in range(60):  # mid-episode start
