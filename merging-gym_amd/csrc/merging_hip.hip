@@ -45,6 +45,9 @@ namespace {
 #ifndef MG_BLOCK
 #define MG_BLOCK 256
 #endif
+#ifndef MG_QNET_PREFETCH
+#define MG_QNET_PREFETCH 3  // Q-net W2 fragments: 0 at use, 1/2 all up front, 3 one ahead
+#endif
 #ifndef MG_QNET_PAIR
 #define MG_QNET_PAIR 1    // Q-net: both 32-env column tiles per hidden-tile iteration
 #endif
@@ -651,13 +654,12 @@ __host__ __device__ constexpr int qnet_krow(int kk) {
 // 4 v_cvt_pk_bf16_f32 + 4 v_pk_max_i16 instead of 8 v_max_f32 + 4 converts.
 typedef short i16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ bf16x8 relu_bf16(const f32x16& c, int s) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
   bf16x8 out;
 #pragma unroll
   for (int j = 0; j < 8; j += 2) {
-    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-    bf16x2 p;
-    p[0] = static_cast<__bf16>(c[8 * s + j]);
-    p[1] = static_cast<__bf16>(c[8 * s + j + 1]);
+    // a 2-wide fptrunc selects ONE v_cvt_pk_bf16_f32 (scalar casts cost 2 converts + a perm)
+    const bf16x2 p = __builtin_convertvector(f32x2{c[8 * s + j], c[8 * s + j + 1]}, bf16x2);
     i16x2 v = __builtin_bit_cast(i16x2, p);
     const i16x2 zero = {0, 0};
     v = __builtin_elementwise_max(v, zero);
@@ -782,6 +784,24 @@ __device__ __forceinline__ void qnet_forward(const uint8_t* net, const float* ti
     for (int mt = 0; mt < kQH1 / 32; ++mt) {
       const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(W1 + (32 * mt + r) * kQS1 + 8 * h);
       const f32x16 bt = bias_tile(B1 + 32 * mt, h);
+      auto w2frag = [&](int m2, int sk) {
+        return *reinterpret_cast<const bf16x8*>(W2 + (32 * m2 + r) * kQS2 + 16 * (2 * mt + sk) +
+                                                8 * h);
+      };
+#if MG_QNET_PREFETCH == 1 || MG_QNET_PREFETCH == 2
+      // all eight W2 fragments of this hidden tile in flight before the layer-1 MFMAs, so
+      // their LDS latency hides under layer 1 and the ReLU instead of stalling each MFMA
+      bf16x8 a2f[kQH2 / 32][2];
+#pragma unroll
+      for (int m2 = 0; m2 < kQH2 / 32; ++m2)
+#pragma unroll
+        for (int sk = 0; sk < 2; ++sk) a2f[m2][sk] = w2frag(m2, sk);
+#if MG_QNET_PREFETCH == 2
+      __builtin_amdgcn_sched_barrier(0);  // keep the scheduler from sinking them to their uses
+#endif
+#elif MG_QNET_PREFETCH == 3
+      bf16x8 a2cur = w2frag(0, 0);
+#endif
       const f32x16 c0 = mfma32(a1, xb0, bt);
       const f32x16 c1 = mfma32(a1, xb1, bt);
       const bf16x8 ha[2] = {relu_bf16(c0, 0), relu_bf16(c0, 1)};
@@ -790,8 +810,16 @@ __device__ __forceinline__ void qnet_forward(const uint8_t* net, const float* ti
       for (int m2 = 0; m2 < kQH2 / 32; ++m2) {
 #pragma unroll
         for (int sk = 0; sk < 2; ++sk) {
-          const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(W2 + (32 * m2 + r) * kQS2 +
-                                                             16 * (2 * mt + sk) + 8 * h);
+#if MG_QNET_PREFETCH == 1 || MG_QNET_PREFETCH == 2
+          const bf16x8 a2 = a2f[m2][sk];
+#elif MG_QNET_PREFETCH == 3
+          // one fragment ahead: the next load is in flight under this pair of MFMAs
+          const bf16x8 a2 = a2cur;
+          if (2 * m2 + sk + 1 < kQH2 / 16) a2cur = w2frag((2 * m2 + sk + 1) >> 1, (sk + 1) & 1);
+          __builtin_amdgcn_sched_barrier(0);
+#else
+          const bf16x8 a2 = w2frag(m2, sk);
+#endif
           acc2a[m2] = mfma32(a2, ha[sk], acc2a[m2]);
           acc2b[m2] = mfma32(a2, hb[sk], acc2b[m2]);
         }
