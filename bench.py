@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--rollout-steps", type=int, default=16,
                     help="T of the fused rollout leg (mg_rollout_random); 0 disables it")
     ap.add_argument("--rollout-launches", type=int, default=60)
+    ap.add_argument("--replay-stores", type=int, default=20,
+                    help="timed mg_replay_store calls of the replay-memory leg; 0 disables it")
     ap.add_argument("--qnet-launches", type=int, default=20,
                     help="launches of the config-5 leg (fused epsilon-greedy DQN rollout); 0 disables it")
     return ap.parse_args()
@@ -188,6 +190,54 @@ def qnet_leg(env, args, world, dist, torch, opponent):
             "frac_useful": nets * QNET_USEFUL_FLOP * per_s / 1e12 / MFMA_BF16_PEAK_TFLOPS}
 
 
+REPLAY_BYTES_PER_ROW = 40 + 40 + 1 + 4 + 1 + 88  # s, s', a, r, done read; the 88-B row written
+
+
+def replay_leg(env, args, torch):
+    """BASELINE section 8(f) rank 3: the device replay memory. A config-5 rollout (T steps of the
+    fused DQN policy) is appended to a 2^24-row ring (DQN.store_transition, main.py:115-119,
+    with the :209 filter) by mg_replay_store -- count, scan, write kernels, timed together with
+    events on the stream they run on -- then a 128-row minibatch is drawn (main.py:130)."""
+    import numpy as np
+
+    from merging_gym import ReplayRing
+    from merging_gym.policy import QNet
+
+    f = np.load(os.path.join(ROOT, "tests", "golden", "dqn_checkpoints.npz"))
+    qnet = QNet.from_state_dict({k.split("/", 1)[1]: f[k] for k in f.files if k.startswith("l1/")},
+                                device=env.device)
+    T, E, L = args.rollout_steps, env.num_envs, args.replay_stores
+    obs0 = env.observe().clone()
+    traj = env.rollout_qnet(T, qnet, args.seed, first_step=30_000_000)
+    ring = ReplayRing(1 << 24, device=env.device)
+    for _ in range(2):
+        ring.store_rollout(obs0, traj)
+    torch.cuda.synchronize()
+    c0 = ring.memory_counter
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * L)]
+    for j in range(L):
+        ev[2 * j].record()
+        ring.store_rollout(obs0, traj)
+        ev[2 * j + 1].record()
+    torch.cuda.synchronize()
+    kept = (ring.memory_counter - c0) / L
+    ms = sum(ev[2 * j].elapsed_time(ev[2 * j + 1]) for j in range(L)) / L
+    achieved = (kept * REPLAY_BYTES_PER_ROW + T * E / 4) / (ms * 1e-3) / 1e9
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    s.record()
+    for j in range(100):
+        ring.sample_rows(128, seed=args.seed, draw=j)
+    e.record()
+    torch.cuda.synchronize()
+    return {"kernels": "replay_count_kernel + replay_scan_kernel + replay_write_kernel",
+            "transitions_per_store": T * E, "stored_per_store": kept, "capacity": 1 << 24,
+            "value": kept / (ms * 1e-3), "unit": "transitions/s", "ms_per_store": ms,
+            "bytes_per_stored_transition": REPLAY_BYTES_PER_ROW, "achieved": achieved,
+            "peak": HBM_PEAK_GBPS, "unit_bw": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
+            "sample_128_us": s.elapsed_time(e) / 100 * 1e3}
+
+
 def dropin_leg(seed: int):
     """BASELINE config 1: merging_gym.make('merging-v0') single env, 500 step() calls with
     uniform random actions for both players, reset on done. The GPU-backed drop-in (one
@@ -299,6 +349,9 @@ def main():
     rollout = None
     if args.rollout_steps > 0:
         rollout = rollout_leg(env, args, world, dist, torch)
+    replay = None
+    if args.replay_stores > 0 and args.rollout_steps > 0:
+        replay = replay_leg(env, args, torch)
 
     qnet = None
     if args.qnet_launches > 0 and args.rollout_steps > 0:
@@ -335,6 +388,8 @@ def main():
         }
         if rollout is not None:
             line["rollout"] = rollout
+        if replay is not None:
+            line["replay"] = replay
         if qnet is not None:
             line["qnet_policy"] = qnet
         if world == 1 and not args.no_cpu_baseline:

@@ -13,6 +13,10 @@
  *   mg_step_random  the same step, actions drawn on the device (Philox4x32-10); it replaces
  *                     the callers' env.action_space.sample() / np.random.randint(0, 5)
  *                     exploration branch (scripts/main.py:110, scripts/hdqn.py:175)
+ *   mg_replay_store / mg_replay_sample / mg_replay_scratch_bytes: the DQN replay memory on the
+ *                     device -- DQN.store_transition (scripts/main.py:115-119, hdqn.py:180-184)
+ *                     for a whole batch of transitions, and learn()'s uniform minibatch draw
+ *                     np.random.choice(MEMORY_CAPACITY, BATCH_SIZE) (main.py:130-131)
  *   mg_reset        replaces MergeEnv.reset()                        merging_env.py:208-230
  *   mg_observe      replaces MergeEnv.observe() and is_collided()    merging_env.py:118-132,
  *                     :198-206 (no state change)
@@ -45,7 +49,7 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 2
+#define MG_ABI_VERSION 3
 #define MG_OBS_DIM 10   /* merging_env.py:75 observation_shape = (10) */
 #define MG_NUM_ACTIONS 5 /* merging_env.py:101-102 action_dict / Discrete(5) */
 #define MG_ACTION_NONE (-1) /* action2=None: the constant-speed "L0" opponent, merging_env.py:152 */
@@ -131,6 +135,8 @@ typedef struct mg_outputs {
                            Such an env is advanced exactly as far as the reference gets before its
                            action_dict[...] KeyError (merging_env.py:141-147, :152): the clock
                            always, the ego too when only a2 is invalid; nothing else is written. */
+  uint64_t* won_mask;   /* [ceil(n/64)] bit = env.winner == 1 after this step (read before any
+                           autoreset): main.py:209 stores a transition only when it is 0 */
 } mg_outputs;
 
 /* Trajectory buffers of mg_rollout_random: the outputs of step t for env i sit at row
@@ -143,7 +149,23 @@ typedef struct mg_traj {
   int8_t* a1;       /* [T, n] actions drawn */
   int8_t* a2;       /* [T, n] (-1 = None) */
   float* final_obs; /* [T, n, 10] written only at rows whose env finished at that step */
+  uint64_t* won_mask; /* [T, ceil(n/64)] as mg_outputs.won_mask, one bitmask per step */
 } mg_traj;
+
+/* A batch of transitions for the replay memory, T steps of n envs in [T, n, ...] layout (the
+ * trajectory buffers of a rollout, or one step's outputs with T = 1). Transition (t, i) is
+ *   s  = obs_first[i] (t = 0) or obs[t-1, i],   a = a1[t, i],   r = rew[t, i, 0] (the ego's),
+ *   s' = final_obs[t, i] where done[t, i] (autoreset put the reset observation in obs), else obs[t, i]
+ * -- exactly what the reference's loop hands store_transition (main.py:195-211). */
+typedef struct mg_transitions {
+  const float* obs_first;   /* [n, 10] observation before step 0 */
+  const float* obs;         /* [T, n, 10] */
+  const float* final_obs;   /* [T, n, 10] or NULL (then s' = obs even where done) */
+  const int8_t* a1;         /* [T, n] */
+  const float* rew;         /* [T, n, 2] */
+  const uint8_t* done;      /* [T, n] or NULL (never done) */
+  const uint64_t* won_mask; /* [T, ceil(n/64)] or NULL (nobody has won) */
+} mg_transitions;
 
 /* Completed-episode statistics, updated only when an env finishes (MG_AUTORESET). */
 typedef struct mg_stats {
@@ -217,6 +239,29 @@ int mg_rollout_qnet(const mg_params* params, const mg_state* state, const mg_tra
                     uint64_t first_step, int32_t num_steps, const void* net, int32_t out_dim,
                     uint64_t greedy_threshold, int32_t opponent_mode,
                     uint64_t opp_greedy_threshold, uint32_t flags, void* stream);
+
+/* ---- replay memory (scripts/main.py:91-92, :115-119, :130-135) --------------------------------
+ * rows: [capacity, 22] fp32 device buffer, row = [s(10), a, r, s'(10)] like np.hstack((state,
+ * [action, reward], next_state)); counter: one device uint64, the reference's memory_counter.
+ * mg_replay_store appends the transitions of *tr in (t, i) order -- the order in which
+ * stepping env 0..n-1 at each step and calling store_transition would append them -- at
+ * slot (memory_counter + k) % capacity, skipping those whose won bit is set when
+ * skip_ego_won != 0 (main.py:209 `if env.winner is not 1`; hdqn.py:316 stores every one), and
+ * adds the number appended to *counter. When more than capacity transitions are appended only
+ * the newest capacity are written, as sequential stores would leave them. scratch: a device
+ * buffer of mg_replay_scratch_bytes(n, num_steps) bytes, 8-byte aligned. Three launches. */
+size_t mg_replay_scratch_bytes(int64_t n, int32_t num_steps);
+int mg_replay_store(float* rows, uint64_t* counter, int64_t capacity, const mg_transitions* tr,
+                    int64_t n, int32_t num_steps, int32_t skip_ego_won, void* scratch,
+                    size_t scratch_bytes, void* stream);
+
+/* out[batch, 22] = rows[idx[b]], idx[b] = floor(u0 * M / 2^32) with u = Philox4x32-10(key = seed,
+ * counter = (b, draw)) and M = capacity (np.random.choice(MEMORY_CAPACITY, BATCH_SIZE),
+ * main.py:130 -- the reference learns only once the memory is full) or, when filled_only != 0,
+ * M = min(*counter, capacity) (at least 1). idx_out[batch] (int64, may be NULL) gets the slots. */
+int mg_replay_sample(const float* rows, const uint64_t* counter, int64_t capacity, uint64_t seed,
+                     uint64_t draw, int32_t filled_only, float* out, int64_t* idx_out,
+                     int64_t batch, void* stream);
 
 /* Resets the envs whose mask byte is non-zero (mask == NULL: all n) and writes their reset
  * observation to out->obs / out->rec64 when given. Replaces MergeEnv.reset (merging_env.py:208-230). */

@@ -472,6 +472,15 @@ __device__ __forceinline__ void wave_store_obs(float* wtile, const double (&o)[k
   wave_lds_sync();
 }
 
+// Step t's won bits of one wave (every lane calls it): word t * ceil(n/64) + wbase / 64.
+__device__ __forceinline__ void store_won_mask(uint64_t* mask, bool won, int t, int64_t n,
+                                               int64_t wbase, int wrows) {
+  if (mask == nullptr) return;
+  const uint64_t m = __ballot(won);
+  if ((threadIdx.x & 63) == 0 && wrows > 0)
+    st_out(mask + static_cast<int64_t>(t) * ((n + 63) >> 6) + (wbase >> 6), m);
+}
+
 struct Launch {
   mg_params P;
   mg_state S;
@@ -501,6 +510,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const Launch L) {
   const bool live = i < L.n;
   StepOut r;
   r.done = false;
+  bool won = false;
 
   if (live) {
     int a1, a2;
@@ -542,6 +552,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const Launch L) {
       }
       if (L.O.done) st_out(L.O.done + i, static_cast<uint8_t>(r.done ? 1 : 0));
       if (L.O.coll) st_out(L.O.coll + i, static_cast<uint8_t>(r.coll ? 1 : 0));
+      won = e.winner == 1;
       if ((L.flags & MG_AUTORESET) && r.done)
         finish_episode(P, e, r, L.St, L.O.final_obs ? L.O.final_obs + i * kObs : nullptr, i);
       store_env(L.S, i, e);
@@ -551,6 +562,10 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const Launch L) {
   if (L.O.done_mask) {
     const uint64_t m = __ballot(live && r.done);
     if ((tid & 63) == 0 && live) L.O.done_mask[i >> 6] = m;
+  }
+  if (L.O.won_mask) {
+    const uint64_t m = __ballot(won);
+    if ((tid & 63) == 0 && live) L.O.won_mask[i >> 6] = m;
   }
   if constexpr (!OUT64) {
     if (L.O.obs) {  // one launch per step: block staging measured as fast as per-wave staging
@@ -592,6 +607,7 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(const Rollout R) {
   Env e;
   if (live) e = load_env(R.S, i);
   StepOut r;
+  bool won = false;
   for (int t = 0; t < R.num_steps; ++t) {
     const int64_t row = static_cast<int64_t>(t) * R.n + i;
     if (live) {
@@ -606,9 +622,11 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(const Rollout R) {
                f32x2{static_cast<float>(r.r1), static_cast<float>(r.r2)});
       if (R.T.done) st_out(R.T.done + row, static_cast<uint8_t>(r.done ? 1 : 0));
       if (R.T.coll) st_out(R.T.coll + row, static_cast<uint8_t>(r.coll ? 1 : 0));
+      won = e.winner == 1;
       if (autoreset && r.done)
         finish_episode(P, e, r, R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i);
     }
+    store_won_mask(R.T.won_mask, won, t, R.n, wbase, wrows);
     if (R.T.obs)  // staged per wave: waves never wait for each other
       wave_store_obs(obs_tile + (tid & ~63) * kObs, r.o,
                      R.T.obs + (static_cast<int64_t>(t) * R.n + wbase) * kObs, wrows);
@@ -1005,6 +1023,7 @@ __global__ __launch_bounds__(kQBlock, 2) void qnet_rollout_kernel(const QRollout
   }
   __syncthreads();
 
+  bool won = false;
   for (int t = 0; t < R.num_steps; ++t) {
     float q[8];
     qnet_forward(lds_net, tile, row0, false, q);
@@ -1036,9 +1055,11 @@ __global__ __launch_bounds__(kQBlock, 2) void qnet_rollout_kernel(const QRollout
                f32x2{static_cast<float>(r.r1), static_cast<float>(r.r2)});
       if (R.T.done) st_out(R.T.done + row, static_cast<uint8_t>(r.done ? 1 : 0));
       if (R.T.coll) st_out(R.T.coll + row, static_cast<uint8_t>(r.coll ? 1 : 0));
+      won = e.winner == 1;
       if (autoreset && r.done)
         finish_episode(P, e, r, R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i);
     }
+    store_won_mask(R.T.won_mask, won, t, R.n, wbase, wrows);
     // the new observations: this wave's tile rows (next step's network input) and the output
     wave_store_obs(wtile, r.o,
                    R.T.obs ? R.T.obs + (static_cast<int64_t>(t) * R.n + wbase) * kObs : nullptr,
@@ -1100,6 +1121,161 @@ __global__ __launch_bounds__(kBlock) void observe_kernel(const mg_params P, cons
     for (int k = 0; k < kObs; ++k) O.rec64[i].obs[k] = o[k];
   }
   if (O.coll) O.coll[i] = boxes_intersect(vehicle_box(P, y1, x1), vehicle_box(P, y2, x2)) ? 1 : 0;
+}
+
+// ============================================================================ replay memory
+// The DQN replay memory (scripts/main.py:91-92 np.zeros((MEMORY_CAPACITY, 2*NUM_STATES+2)),
+// :115-119 store_transition, :130-135 the minibatch draw). A batch of T x n transitions is
+// appended in (t, i) order with three launches: per-block keep counts, a one-block scan that
+// turns them into ring positions and advances memory_counter, and the row writes. Rows are
+// gathered into an LDS tile in ring order and written as contiguous 8-byte stores (a row is
+// 88 B, so consecutive rows alternate 16-byte alignment).
+constexpr int kRow = 2 * kObs + 2;  // 22 floats: s(10), a, r, s'(10)
+constexpr int kRBlock = 256;        // transitions per block (blockIdx.x: env slice, y: step)
+constexpr int kScanBlock = 1024;
+
+struct ReplayIn {
+  mg_transitions X;
+  int64_t n;
+  int64_t words;  // ceil(n / 64)
+  int32_t skip_won;
+};
+
+__device__ __forceinline__ bool replay_keep(const ReplayIn& R, int t, int64_t i) {
+  if (i >= R.n) return false;
+  if (!R.skip_won || R.X.won_mask == nullptr) return true;
+  const uint64_t w = R.X.won_mask[static_cast<int64_t>(t) * R.words + (i >> 6)];
+  return ((w >> (i & 63)) & 1u) == 0;
+}
+
+// Number of kept transitions of this block's threads before the calling thread (inclusive
+// of nothing) and the block total; counts in LDS per wave.
+__device__ __forceinline__ int block_rank(bool keep, int* wave_cnt, int& total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t m = __ballot(keep);
+  const int below = __popcll(m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
+  if (lane == 0) wave_cnt[wave] = __popcll(m);
+  __syncthreads();
+  int before = 0;
+  total = 0;
+#pragma unroll
+  for (int w = 0; w < kRBlock / 64; ++w) {
+    before += (w < wave) ? wave_cnt[w] : 0;
+    total += wave_cnt[w];
+  }
+  return before + below;
+}
+
+__global__ __launch_bounds__(kRBlock) void replay_count_kernel(const ReplayIn R, uint32_t* counts) {
+  __shared__ int wave_cnt[kRBlock / 64];
+  const int t = blockIdx.y;
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kRBlock + threadIdx.x;
+  int total;
+  block_rank(replay_keep(R, t, i), wave_cnt, total);
+  if (threadIdx.x == 0) counts[static_cast<int64_t>(t) * gridDim.x + blockIdx.x] = total;
+}
+
+// One block: bases[b] = counter + sum(counts[0..b)), then counter += sum(counts). Thread j
+// owns the contiguous chunk [j*per, (j+1)*per): chunk sums, one block scan, chunk walk.
+__global__ __launch_bounds__(kScanBlock) void replay_scan_kernel(const uint32_t* counts,
+                                                                 uint64_t* bases, int64_t nb,
+                                                                 uint64_t* counter) {
+  __shared__ uint64_t part[kScanBlock];
+  const int tid = threadIdx.x;
+  const int64_t per = (nb + kScanBlock - 1) / kScanBlock;
+  const int64_t lo = tid * per, hi = lo + per < nb ? lo + per : nb;
+  uint64_t sum = 0;
+  for (int64_t b = lo; b < hi; ++b) sum += counts[b];
+  part[tid] = sum;
+  __syncthreads();
+  for (int off = 1; off < kScanBlock; off <<= 1) {  // Hillis-Steele inclusive scan
+    const uint64_t add = tid >= off ? part[tid - off] : 0u;
+    __syncthreads();
+    part[tid] += add;
+    __syncthreads();
+  }
+  const uint64_t c0 = *counter;
+  uint64_t run = c0 + part[tid] - sum;
+  for (int64_t b = lo; b < hi; ++b) {
+    bases[b] = run;
+    run += counts[b];
+  }
+  __syncthreads();  // every thread has read *counter
+  if (tid == 0) *counter = c0 + part[kScanBlock - 1];
+}
+
+__global__ __launch_bounds__(kRBlock) void replay_write_kernel(const ReplayIn R,
+                                                               const uint64_t* bases,
+                                                               const uint64_t* counter,
+                                                               float* rows, int64_t cap) {
+  __shared__ __attribute__((aligned(16))) float tile[kRBlock * kRow];
+  __shared__ int wave_cnt[kRBlock / 64];
+  const int t = blockIdx.y;
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kRBlock + threadIdx.x;
+  const bool keep = replay_keep(R, t, i);
+  int total;
+  const int rank = block_rank(keep, wave_cnt, total);
+  if (total == 0) return;  // uniform across the block
+  const uint64_t base = bases[static_cast<int64_t>(t) * gridDim.x + blockIdx.x];
+  const uint64_t end = *counter;  // memory_counter after this whole store
+  if (keep) {
+    const int64_t row = static_cast<int64_t>(t) * R.n + i;
+    const float* s = t == 0 ? R.X.obs_first + i * kObs : R.X.obs + (row - R.n) * kObs;
+    const bool done = R.X.done != nullptr && R.X.done[row] != 0;
+    const float* s2 = (done && R.X.final_obs) ? R.X.final_obs + row * kObs : R.X.obs + row * kObs;
+    float* d = tile + rank * kRow;
+    const f32x2* s_2 = reinterpret_cast<const f32x2*>(s);
+    const f32x2* s2_2 = reinterpret_cast<const f32x2*>(s2);
+#pragma unroll
+    for (int k = 0; k < kObs / 2; ++k) {
+      const f32x2 a = s_2[k], b = s2_2[k];
+      d[2 * k] = a[0];
+      d[2 * k + 1] = a[1];
+      d[kObs + 2 + 2 * k] = b[0];
+      d[kObs + 2 + 2 * k + 1] = b[1];
+    }
+    d[kObs] = static_cast<float>(R.X.a1[row]);
+    d[kObs + 1] = R.X.rew[2 * row];
+  }
+  __syncthreads();
+  // Only the newest `cap` transitions of the whole store survive sequential stores; they
+  // occupy distinct slots, so no two writes of this launch collide.
+  const uint64_t first = end > static_cast<uint64_t>(cap) ? end - static_cast<uint64_t>(cap) : 0u;
+  const int skip = base >= first ? 0 : static_cast<int>(min<uint64_t>(first - base, total));
+  const uint64_t slot0 = (base + skip) % static_cast<uint64_t>(cap);
+  const int nel = (total - skip) * (kRow / 2);
+  const f32x2* src = reinterpret_cast<const f32x2*>(tile + skip * kRow);
+  for (int e2 = threadIdx.x; e2 < nel; e2 += kRBlock) {
+    const int rr = e2 / (kRow / 2), part = e2 - rr * (kRow / 2);
+    uint64_t slot = slot0 + rr;
+    if (slot >= static_cast<uint64_t>(cap)) slot %= static_cast<uint64_t>(cap);
+    st_out(reinterpret_cast<f32x2*>(rows + slot * kRow) + part, src[e2]);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void replay_sample_kernel(const float* rows,
+                                                               const uint64_t* counter, int64_t cap,
+                                                               uint64_t seed, uint64_t draw,
+                                                               int32_t filled_only, float* out,
+                                                               int64_t* idx_out, int64_t batch) {
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (b >= batch) return;
+  uint64_t m = static_cast<uint64_t>(cap);
+  if (filled_only) {
+    const uint64_t c = *counter;
+    m = c < m ? c : m;
+    if (m == 0) m = 1;
+  }
+  const uint4 u = philox4x32_10(
+      make_uint4(static_cast<uint32_t>(b), static_cast<uint32_t>(static_cast<uint64_t>(b) >> 32),
+                 static_cast<uint32_t>(draw), static_cast<uint32_t>(draw >> 32)),
+      static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32));
+  const uint64_t idx = (static_cast<uint64_t>(u.x) * m) >> 32;
+  if (idx_out) idx_out[b] = static_cast<int64_t>(idx);
+  const f32x2* src = reinterpret_cast<const f32x2*>(rows + idx * kRow);
+  f32x2* dst = reinterpret_cast<f32x2*>(out + b * kRow);
+#pragma unroll
+  for (int k = 0; k < kRow / 2; ++k) dst[k] = src[k];
 }
 
 thread_local char g_err[512] = "";
@@ -1368,6 +1544,63 @@ int mg_rollout_qnet(const mg_params* params, const mg_state* state, const mg_tra
     MG_LAUNCH_Q(2);
 #undef MG_LAUNCH_Q
   return finish_launch("mg_rollout_qnet");
+}
+
+size_t mg_replay_scratch_bytes(int64_t n, int32_t num_steps) {
+  if (n <= 0 || num_steps <= 0) return 0;
+  const int64_t nb = ((n + kRBlock - 1) / kRBlock) * num_steps;
+  return static_cast<size_t>(((nb * 4 + 7) & ~int64_t{7}) + nb * 8);
+}
+
+int mg_replay_store(float* rows, uint64_t* counter, int64_t capacity, const mg_transitions* tr,
+                    int64_t n, int32_t num_steps, int32_t skip_ego_won, void* scratch,
+                    size_t scratch_bytes, void* stream) {
+  if (!rows || !counter || !tr) return fail(hipErrorInvalidValue, "%s", "mg_replay_store: NULL pointer");
+  if (capacity < 1) return fail(hipErrorInvalidValue, "%s", "mg_replay_store: capacity < 1");
+  if (n < 0 || num_steps < 0 || num_steps > 65535)
+    return fail(hipErrorInvalidValue, "%s", "mg_replay_store: need n >= 0 and 0 <= num_steps <= 65535");
+  if (n == 0 || num_steps == 0) return 0;
+  if (!tr->obs_first || !tr->obs || !tr->a1 || !tr->rew)
+    return fail(hipErrorInvalidValue, "%s", "mg_replay_store: obs_first, obs, a1 and rew are required");
+  if ((reinterpret_cast<uintptr_t>(rows) | reinterpret_cast<uintptr_t>(tr->obs_first) |
+       reinterpret_cast<uintptr_t>(tr->obs) | reinterpret_cast<uintptr_t>(tr->final_obs) |
+       reinterpret_cast<uintptr_t>(tr->rew) | reinterpret_cast<uintptr_t>(scratch)) & 7)
+    return fail(hipErrorInvalidValue, "%s", "mg_replay_store: float buffers and scratch must be 8-byte aligned");
+  const int64_t nbx = (n + kRBlock - 1) / kRBlock;
+  if (nbx > 0x7fffffff) return fail(hipErrorInvalidValue, "%s", "mg_replay_store: n exceeds the grid limit");
+  if (!scratch || scratch_bytes < mg_replay_scratch_bytes(n, num_steps))
+    return fail(hipErrorInvalidValue, "%s", "mg_replay_store: scratch smaller than mg_replay_scratch_bytes(n, num_steps)");
+  const int64_t nb = nbx * num_steps;
+  uint32_t* counts = static_cast<uint32_t*>(scratch);
+  uint64_t* bases = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(scratch) + ((nb * 4 + 7) & ~int64_t{7}));
+  ReplayIn R{};
+  R.X = *tr;
+  R.n = n;
+  R.words = (n + 63) >> 6;
+  R.skip_won = skip_ego_won;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const dim3 grid(static_cast<unsigned>(nbx), static_cast<unsigned>(num_steps));
+  hipLaunchKernelGGL(replay_count_kernel, grid, dim3(kRBlock), 0, st, R, counts);
+  hipLaunchKernelGGL(replay_scan_kernel, dim3(1), dim3(kScanBlock), 0, st, counts, bases, nb, counter);
+  hipLaunchKernelGGL(replay_write_kernel, grid, dim3(kRBlock), 0, st, R, bases, counter, rows, capacity);
+  return finish_launch("mg_replay_store");
+}
+
+int mg_replay_sample(const float* rows, const uint64_t* counter, int64_t capacity, uint64_t seed,
+                     uint64_t draw, int32_t filled_only, float* out, int64_t* idx_out,
+                     int64_t batch, void* stream) {
+  if (!rows || !out || (filled_only && !counter))
+    return fail(hipErrorInvalidValue, "%s", "mg_replay_sample: NULL pointer");
+  if (capacity < 1 || capacity > (int64_t{1} << 32) || batch < 0)
+    return fail(hipErrorInvalidValue, "%s", "mg_replay_sample: need 1 <= capacity <= 2^32 and batch >= 0");
+  if ((reinterpret_cast<uintptr_t>(rows) | reinterpret_cast<uintptr_t>(out)) & 7)
+    return fail(hipErrorInvalidValue, "%s", "mg_replay_sample: rows and out must be 8-byte aligned");
+  if (batch == 0) return 0;
+  const unsigned blocks = static_cast<unsigned>((batch + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(replay_sample_kernel, dim3(blocks), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), rows, counter, capacity, seed, draw,
+                     filled_only, out, idx_out, batch);
+  return finish_launch("mg_replay_sample");
 }
 
 int mg_reset(const mg_params* params, const mg_state* state, const uint8_t* mask,

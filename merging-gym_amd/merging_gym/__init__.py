@@ -7,7 +7,15 @@ is importable. Without gym, `merging_gym.make(id)` builds the same envs.
 
 from .envs import MergeEnv, MergeEnvExtend, MergeVecEnv
 
-__all__ = ["MergeEnv", "MergeEnvExtend", "MergeVecEnv", "make", "ENV_IDS"]
+__all__ = ["MergeEnv", "MergeEnvExtend", "MergeVecEnv", "ReplayRing", "make", "ENV_IDS"]
+
+
+def __getattr__(name):  # ReplayRing loads the native library on first use only
+    if name == "ReplayRing":
+        from .replay import ReplayRing
+
+        return ReplayRing
+    raise AttributeError(name)
 
 ENV_IDS = {
     "merging_env-v0": "merging_gym.envs:MergeEnv",

@@ -15,7 +15,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libmerging_hip.so"
 LIB_PATH = os.environ.get("MERGING_HIP_LIB", os.path.join(_HERE, LIB_NAME))
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 OBS_DIM = 10
 NUM_ACTIONS = 5
@@ -50,11 +50,15 @@ class State(_c.Structure):
 
 class Outputs(_c.Structure):
     _fields_ = [(n, _P) for n in ("obs", "rew", "done", "coll", "done_mask", "final_obs",
-                                  "rec64", "error")]
+                                  "rec64", "error", "won_mask")]
 
 
 class Traj(_c.Structure):
-    _fields_ = [(n, _P) for n in ("obs", "rew", "done", "coll", "a1", "a2", "final_obs")]
+    _fields_ = [(n, _P) for n in ("obs", "rew", "done", "coll", "a1", "a2", "final_obs", "won_mask")]
+
+
+class Transitions(_c.Structure):
+    _fields_ = [(n, _P) for n in ("obs_first", "obs", "final_obs", "a1", "rew", "done", "won_mask")]
 
 
 class Stats(_c.Structure):
@@ -101,8 +105,15 @@ def _load():
                                     _c.c_uint64, _c.c_int32, _P, _c.c_int32, _c.c_uint64, _c.c_int32,
                                     _c.c_uint64, _c.c_uint32, _P]
     lib.mg_time_next_launch.argtypes = [_P, _P]
+    lib.mg_replay_scratch_bytes.argtypes = [_c.c_int64, _c.c_int32]
+    lib.mg_replay_scratch_bytes.restype = _c.c_size_t
+    lib.mg_replay_store.argtypes = [_P, _P, _c.c_int64, _c.POINTER(Transitions), _c.c_int64, _c.c_int32,
+                                    _c.c_int32, _P, _c.c_size_t, _P]
+    lib.mg_replay_sample.argtypes = [_P, _P, _c.c_int64, _c.c_uint64, _c.c_uint64, _c.c_int32, _P, _P,
+                                     _c.c_int64, _P]
     for f in (lib.mg_step, lib.mg_step_random, lib.mg_reset, lib.mg_observe, lib.mg_rollout_random,
-              lib.mg_time_next_launch, lib.mg_qnet_pack, lib.mg_qnet_forward, lib.mg_rollout_qnet):
+              lib.mg_time_next_launch, lib.mg_qnet_pack, lib.mg_qnet_forward, lib.mg_rollout_qnet,
+              lib.mg_replay_store, lib.mg_replay_sample):
         f.restype = _c.c_int
     v = lib.mg_abi_version()
     if v != ABI_VERSION:

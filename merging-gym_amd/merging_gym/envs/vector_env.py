@@ -35,7 +35,7 @@ class MergeVecEnv:
 
     def __init__(self, num_envs: int, device=None, autoreset: bool = True, env_offset: int = 0,
                  final_observation: bool = True, episode_stats: bool = True,
-                 done_mask: bool = False):
+                 done_mask: bool = False, won_mask: bool = False):
         import torch
 
         from .. import _native
@@ -70,6 +70,9 @@ class MergeVecEnv:
                           if final_observation else None)
         self.done_mask = (torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
                           if done_mask else None)
+        # bit i = env i's winner == 1 after the step, before autoreset (main.py:209's store filter)
+        self.won_mask = (torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
+                         if won_mask else None)
         self.error = torch.zeros(1, dtype=torch.int32, device=dev)
         self.ret_sum = torch.zeros((n, 2), dtype=torch.float64, device=dev) if episode_stats else None
         self.counts = torch.zeros((n, 4), dtype=torch.int32, device=dev) if episode_stats else None
@@ -80,7 +83,8 @@ class MergeVecEnv:
         self._state = _native.State(*(ptr(t) for t in (self.p1, self.v1, self.p2, self.v2,
                                                         self.ret1, self.ret2, self.tf)))
         self._out = _native.Outputs(ptr(self.obs), ptr(self.rew), ptr(self.done), ptr(self.coll),
-                                    ptr(self.done_mask), ptr(self.final_obs), None, ptr(self.error))
+                                    ptr(self.done_mask), ptr(self.final_obs), None, ptr(self.error),
+                                    ptr(self.won_mask))
         self._stats = _native.Stats(ptr(self.ret_sum), ptr(self.counts))
         self._flags = _native.AUTORESET if self.autoreset else 0
         self._step_idx = 0
@@ -142,7 +146,7 @@ class MergeVecEnv:
             mt = self._torch.as_tensor(mask, device=self.device).to(self._torch.uint8).contiguous()
             self._mask_keepalive = mt
             m = ctypes.c_void_p(mt.data_ptr())
-        out = self._nat.Outputs(self._out.obs, None, None, None, None, None, None, None)
+        out = self._nat.Outputs(self._out.obs)
         self._nat.check(self._nat.lib.mg_reset(ctypes.byref(self.params), ctypes.byref(self._state),
                                                m, ctypes.byref(out), self.num_envs,
                                                ctypes.c_void_p(self._stream())),
@@ -182,8 +186,10 @@ class MergeVecEnv:
         """`num_steps` steps with device-drawn actions in ONE kernel launch (the env stays in
         registers; its state is read and written once). Bit-identical to `num_steps` calls of
         step_random(seed, step_idx=first_step + t). Returns a dict of [T, N, ...] tensors:
-        obs, rew, done (bool), collision (bool), a1, a2 and final_observation (rows where
-        done). The buffers are reused by the next rollout of the same length."""
+        obs, rew, done (bool), collision (bool), a1, a2, final_observation (rows where done)
+        and won_mask ([T, ceil(N/64)] int64, bit i of step t = env i's winner == 1 after that
+        step -- ReplayRing.store_rollout's filter). The buffers are reused by the next rollout
+        of the same length."""
         nat = self._nat
         T, n = int(num_steps), self.num_envs
         k0 = self._step_idx if first_step is None else int(first_step)
@@ -210,13 +216,15 @@ class MergeVecEnv:
                    "a1": torch.empty((T, n), dtype=torch.int8, device=dev),
                    "a2": torch.empty((T, n), dtype=torch.int8, device=dev),
                    "final_observation": (torch.full((T, n, _OBS_DIM), float("nan"), dtype=torch.float32,
-                                                    device=dev) if final_observation else None)}
+                                                    device=dev) if final_observation else None),
+                   "won_mask": torch.zeros((T, (n + 63) // 64), dtype=torch.int64, device=dev)}
             ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
             buf["_traj"] = nat.Traj(*(ptr(buf[k]) for k in ("obs", "rew", "done", "collision", "a1", "a2",
-                                                             "final_observation")))
+                                                             "final_observation", "won_mask")))
             buf["_result"] = {"obs": buf["obs"], "rew": buf["rew"], "done": buf["done"].view(torch.bool),
                               "collision": buf["collision"].view(torch.bool), "a1": buf["a1"],
-                              "a2": buf["a2"], "final_observation": buf["final_observation"]}
+                              "a2": buf["a2"], "final_observation": buf["final_observation"],
+                              "won_mask": buf["won_mask"]}
             self._traj_bufs = buf
         return buf
 
@@ -244,7 +252,7 @@ class MergeVecEnv:
 
     def observe(self):
         """Observation of the current state without stepping (merging_env.py:118-132)."""
-        out = self._nat.Outputs(self._out.obs, None, None, self._out.coll, None, None, None, None)
+        out = self._nat.Outputs(self._out.obs, None, None, self._out.coll)
         self._nat.check(self._nat.lib.mg_observe(ctypes.byref(self.params), ctypes.byref(self._state),
                                                  ctypes.byref(out), self.num_envs,
                                                  ctypes.c_void_p(self._stream())),

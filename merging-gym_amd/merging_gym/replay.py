@@ -1,0 +1,163 @@
+"""ReplayRing: the DQN replay memory kept on the GPU.
+
+Device twin of the reference's memory (scripts/main.py:91-92 `np.zeros((MEMORY_CAPACITY,
+NUM_STATES * 2 + 2))`, :115-119 store_transition, :129-135 the minibatch draw in learn(); the
+same structure in scripts/hdqn.py:157-158, :180-184, :194-199). Rows are
+[s(10), a, r, s'(10)] fp32 -- the reference keeps fp64 rows and reads them back through
+torch.FloatTensor, so the values learn() sees are the same.
+
+Transitions go in straight from a MergeVecEnv's trajectory buffers (one batched store per
+rollout, three kernel launches from libmerging_hip.so) instead of one store_transition call
+per env step; the order is (step, env), i.e. what stepping env 0..N-1 and storing each in
+turn would give. The ring position lives on the device; reading `memory_counter`
+synchronises.
+
+    ring = ReplayRing(capacity=2000, device="cuda:0")
+    obs0 = env.observe().clone()
+    traj = env.rollout_qnet(16, qnet, seed)
+    ring.store_rollout(obs0, traj)                       # main.py:209 filter by default
+    s, a, r, s2 = ring.sample(128, seed=1, draw=step)    # main.py:130-135
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+from . import _native
+
+_OBS_DIM = 10
+ROW = 2 * _OBS_DIM + 2
+
+
+class ReplayRing:
+    def __init__(self, capacity: int = 2000, device=None):
+        import torch
+
+        if not torch.cuda.is_available():
+            raise RuntimeError("ReplayRing needs a ROCm GPU; there is no CPU fallback")
+        if capacity < 1:
+            raise ValueError("capacity must be >= 1")
+        self._torch = torch
+        self.capacity = int(capacity)
+        self.device = torch.device(device if device is not None else "cuda")
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self.memory = torch.zeros((self.capacity, ROW), dtype=torch.float32, device=self.device)
+        self._counter = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self._scratch = torch.empty(0, dtype=torch.int64, device=self.device)
+        self._sample_bufs = {}
+
+    # ------------------------------------------------------------------ helpers
+    def _stream(self):
+        return self._torch.cuda.current_stream(self.device).cuda_stream
+
+    def _scratch_for(self, n, T):
+        need = int(_native.lib.mg_replay_scratch_bytes(n, T))
+        if self._scratch.numel() * 8 < need:
+            self._scratch = self._torch.empty((need + 7) // 8, dtype=self._torch.int64, device=self.device)
+        return self._scratch
+
+    def _f32(self, t, shape):
+        torch = self._torch
+        t = torch.as_tensor(t, device=self.device)
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            t = t.to(torch.float32).contiguous()
+        if tuple(t.shape) != tuple(shape):
+            raise ValueError(f"expected shape {tuple(shape)}, got {tuple(t.shape)}")
+        return t
+
+    # ------------------------------------------------------------------ stores
+    @property
+    def memory_counter(self) -> int:
+        """Transitions stored so far (main.py:119). Synchronises the stream."""
+        return int(self._counter.item())
+
+    def store(self, obs_first, obs, a1, rew, done=None, final_obs=None, won_mask=None,
+              skip_ego_won: bool = True):
+        """Append T steps of N envs ([T, N, ...] tensors; obs_first [N, 10] = observation
+        before step 0). skip_ego_won drops the transitions whose won bit is set (main.py:209;
+        hdqn.py:316 stores all: pass False). Stream-ordered; nothing is synchronised."""
+        torch = self._torch
+        a1 = torch.as_tensor(a1, device=self.device)
+        if a1.dim() == 1:  # one step
+            a1 = a1[None]
+            obs = torch.as_tensor(obs, device=self.device)[None]
+            rew = torch.as_tensor(rew, device=self.device)[None]
+            done = None if done is None else torch.as_tensor(done, device=self.device)[None]
+            final_obs = None if final_obs is None else torch.as_tensor(final_obs, device=self.device)[None]
+            won_mask = None if won_mask is None else torch.as_tensor(won_mask, device=self.device)[None]
+        T, n = a1.shape
+        if a1.dtype != torch.int8:
+            a1 = a1.to(torch.int8)
+        a1 = a1.contiguous()
+        obs_first = self._f32(obs_first, (n, _OBS_DIM))
+        obs = self._f32(obs, (T, n, _OBS_DIM))
+        rew = self._f32(rew, (T, n, 2))
+        if final_obs is not None:
+            final_obs = self._f32(final_obs, (T, n, _OBS_DIM))
+        if done is not None:
+            done = torch.as_tensor(done, device=self.device)
+            if done.dtype == torch.bool:
+                done = done.view(torch.uint8)
+            done = done.to(torch.uint8).contiguous()
+            if tuple(done.shape) != (T, n):
+                raise ValueError(f"done must have shape {(T, n)}")
+        if skip_ego_won and won_mask is not None:
+            won_mask = torch.as_tensor(won_mask, device=self.device).to(torch.int64).contiguous()
+            if tuple(won_mask.shape) != (T, (n + 63) // 64):
+                raise ValueError(f"won_mask must have shape {(T, (n + 63) // 64)}")
+        elif skip_ego_won:
+            raise ValueError("skip_ego_won needs the won_mask of the step(s) (main.py:209); "
+                             "pass won_mask or skip_ego_won=False")
+        ptr = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        tr = _native.Transitions(ptr(obs_first), ptr(obs), ptr(final_obs), ptr(a1), ptr(rew),
+                                 ptr(done), ptr(won_mask) if skip_ego_won else None)
+        scratch = self._scratch_for(n, T)
+        rc = _native.lib.mg_replay_store(
+            self.memory.data_ptr(), self._counter.data_ptr(), self.capacity, ctypes.byref(tr), n, T,
+            1 if skip_ego_won else 0, scratch.data_ptr(), scratch.numel() * 8, self._stream())
+        _native.check(rc, "mg_replay_store")
+        self._keepalive = (obs_first, obs, a1, rew, done, final_obs, won_mask)
+
+    def store_rollout(self, obs_first, traj, skip_ego_won: bool = True):
+        """Append a MergeVecEnv rollout (the dict rollout_random / rollout_qnet return)."""
+        self.store(obs_first, traj["obs"], traj["a1"], traj["rew"], traj["done"],
+                   traj.get("final_observation"), traj.get("won_mask"), skip_ego_won)
+
+    def store_transition(self, state, action, reward, next_state):
+        """The reference's single-transition call (main.py:115-119), through the same kernels."""
+        torch = self._torch
+        s = torch.as_tensor([list(map(float, state))], dtype=torch.float32)
+        s2 = torch.as_tensor([[list(map(float, next_state))]], dtype=torch.float32)
+        a = torch.as_tensor([[int(action)]], dtype=torch.int8)
+        r = torch.as_tensor([[[float(reward), 0.0]]], dtype=torch.float32)
+        self.store(s.to(self.device), s2.to(self.device), a.to(self.device), r.to(self.device),
+                   skip_ego_won=False)
+
+    # ------------------------------------------------------------------ sampling
+    def sample_rows(self, batch_size: int = 128, seed: int = 0, draw: int = 0,
+                    filled_only: bool = False, return_index: bool = False):
+        """[B, 22] rows at Philox-drawn slots: np.random.choice(MEMORY_CAPACITY, BATCH_SIZE)
+        (main.py:130-131); filled_only draws from the stored rows only. The returned tensor is
+        reused by the next call with the same batch size."""
+        torch = self._torch
+        B = int(batch_size)
+        buf = self._sample_bufs.get(B)
+        if buf is None:
+            buf = (torch.empty((B, ROW), dtype=torch.float32, device=self.device),
+                   torch.empty(B, dtype=torch.int64, device=self.device))
+            self._sample_bufs[B] = buf
+        rows, idx = buf
+        rc = _native.lib.mg_replay_sample(
+            self.memory.data_ptr(), self._counter.data_ptr(), self.capacity, seed & 0xFFFFFFFFFFFFFFFF,
+            draw & 0xFFFFFFFFFFFFFFFF, 1 if filled_only else 0, rows.data_ptr(), idx.data_ptr(), B,
+            self._stream())
+        _native.check(rc, "mg_replay_sample")
+        return (rows, idx) if return_index else rows
+
+    def sample(self, batch_size: int = 128, seed: int = 0, draw: int = 0, filled_only: bool = False):
+        """(batch_state [B,10] f32, batch_action [B,1] int64, batch_reward [B,1] f32,
+        batch_next_state [B,10] f32) -- the slices of main.py:131-135."""
+        rows = self.sample_rows(batch_size, seed, draw, filled_only)
+        return (rows[:, :_OBS_DIM], rows[:, _OBS_DIM:_OBS_DIM + 1].to(self._torch.int64),
+                rows[:, _OBS_DIM + 1:_OBS_DIM + 2], rows[:, -_OBS_DIM:])

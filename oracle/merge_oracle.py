@@ -340,3 +340,60 @@ def qnet_reference(weights, obs, bf16: bool = True, swap: bool = False):
         if i < 2:
             h = rnd(torch.relu(h))
     return h.numpy()
+
+
+# --------------------------------------------------------------------------- replay memory oracle
+
+def step_with_won(coracle, envs, a1, a2=None):
+    """One autoreset step of the C oracle that also reports env.winner == 1 after the step,
+    read before the reset (the kernels' won bit; main.py:209). Returns obs (reset observation
+    where done), rew, done, coll, final_obs (NaN rows where not done), won, err."""
+    obs, rew, done, coll, _, _, err = coracle.step(envs, a1, a2, autoreset=False)
+    won = envs["winner"] == 1
+    d = done.astype(bool)
+    fobs = np.full_like(obs, np.nan)
+    fobs[d] = obs[d]
+    if d.any():
+        sub = envs[d]
+        obs[d] = coracle.reset(sub)
+        envs[d] = sub
+    return obs, rew, done, coll, fobs, won, err
+
+
+def replay_store(memory, counter, obs_first, obs, a1, rew, done=None, final_obs=None, won=None,
+                 skip_ego_won=True):
+    """DQN.store_transition (scripts/main.py:115-119) applied to T steps of n envs in (t, i)
+    order -- the order of stepping envs 0..n-1 each step and storing in turn -- with main.py:209's
+    `if env.winner is not 1` filter. Row = np.hstack((s, [a, r], s')) with s the observation
+    before the step, r the ego's reward, s' the terminal observation where done. Rows are
+    float32 (the reference's float64 memory is read back through torch.FloatTensor, main.py:131-135).
+    Vectorised; only the newest len(memory) transitions are written, as sequential stores leave
+    them. Returns the new memory_counter."""
+    a1 = np.asarray(a1)
+    T, n = a1.shape
+    cap = memory.shape[0]
+    obs = np.asarray(obs, np.float32).reshape(T, n, -1)
+    prev = np.concatenate([np.asarray(obs_first, np.float32)[None], obs[:-1]], axis=0)
+    nxt = obs.copy()
+    if done is not None and final_obs is not None:
+        d = np.asarray(done, bool).reshape(T, n)
+        nxt[d] = np.asarray(final_obs, np.float32).reshape(T, n, -1)[d]
+    keep = np.ones((T, n), bool)
+    if skip_ego_won and won is not None:
+        keep = ~np.asarray(won, bool).reshape(T, n)
+    rows = np.concatenate([prev, a1[..., None].astype(np.float32),
+                           np.asarray(rew, np.float32).reshape(T, n, 2)[..., :1], nxt], axis=2)[keep]
+    k = len(rows)
+    last = rows[max(0, k - cap):]
+    slots = (counter + np.arange(max(0, k - cap), k)) % cap
+    memory[slots] = last
+    return counter + k
+
+
+def replay_sample_index(coracle, capacity, counter, seed, draw, batch, filled_only=False):
+    """Slots of mg_replay_sample: floor(u0 * M / 2^32), u = Philox4x32-10(key seed, counter
+    (b, draw)); M = capacity (np.random.choice(MEMORY_CAPACITY, BATCH_SIZE), main.py:130) or
+    min(counter, capacity) (>= 1) when filled_only."""
+    m = capacity if not filled_only else max(1, min(counter, capacity))
+    u = coracle.philox_batch(batch, 0, seed, draw)
+    return ((u[:, 0].astype(np.uint64) * np.uint64(m)) >> np.uint64(32)).astype(np.int64)

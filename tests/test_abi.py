@@ -14,13 +14,15 @@ def _declared():
     names = set()
     for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
         text = open(h).read()
-        names |= set(re.findall(r"^\s*(?:int|void|const char\*)\s+(mg_\w+)\s*\(", text, re.M))
+        names |= set(re.findall(r"^\s*(?:int|void|size_t|const char\*)\s+(mg_\w+)\s*\(", text, re.M))
     return names
 
 
 def test_header_declares_the_step_path():
     assert {"mg_step", "mg_step_random", "mg_reset", "mg_observe", "mg_abi_version",
-            "mg_last_error", "mg_params_default"} <= _declared()
+            "mg_last_error", "mg_params_default", "mg_rollout_random", "mg_rollout_qnet",
+            "mg_qnet_pack", "mg_qnet_forward", "mg_qnet_packed_bytes", "mg_replay_store",
+            "mg_replay_sample", "mg_replay_scratch_bytes"} <= _declared()
 
 
 def test_library_exports_every_declared_symbol():
@@ -38,7 +40,9 @@ def test_struct_layouts_match_header():
     # mg_params: 15 doubles + 5 doubles + 4 int32 + 2 doubles; mg_rec64: 20 doubles + 2 uint32
     assert ctypes.sizeof(_native.Params) == 20 * 8 + 16 + 16
     assert ctypes.sizeof(_native.State) == 7 * 8
-    assert ctypes.sizeof(_native.Outputs) == 8 * 8
+    assert ctypes.sizeof(_native.Outputs) == 9 * 8
+    assert ctypes.sizeof(_native.Traj) == 8 * 8
+    assert ctypes.sizeof(_native.Transitions) == 7 * 8
     assert ctypes.sizeof(_native.Stats) == 2 * 8
     assert _native.REC64_DTYPE.itemsize == 168
 
@@ -68,6 +72,20 @@ def test_argument_errors_without_gpu():
     assert rc != 0 and b"NULL" in _native.lib.mg_last_error()
     rc = _native.lib.mg_reset(None, None, None, None, 1, None)
     assert rc != 0
+    # replay: missing buffers, bad capacity and short scratch are refused before any launch
+    tr = _native.Transitions()
+    rc = _native.lib.mg_replay_store(None, None, 16, ctypes.byref(tr), 4, 1, 0, None, 0, None)
+    assert rc != 0 and b"NULL" in _native.lib.mg_last_error()
+    fake = ctypes.c_void_p(1 << 20)  # never dereferenced: validation fails first
+    rc = _native.lib.mg_replay_store(fake, fake, 0, ctypes.byref(tr), 4, 1, 0, None, 0, None)
+    assert rc != 0 and b"capacity" in _native.lib.mg_last_error()
+    tr = _native.Transitions(fake, fake, None, fake, fake, None, None)
+    rc = _native.lib.mg_replay_store(fake, fake, 16, ctypes.byref(tr), 4, 1, 0, fake, 8, None)
+    assert rc != 0 and b"scratch" in _native.lib.mg_last_error()
+    rc = _native.lib.mg_replay_sample(fake, fake, 0, 0, 0, 0, fake, None, 4, None)
+    assert rc != 0 and b"capacity" in _native.lib.mg_last_error()
+    assert _native.lib.mg_replay_scratch_bytes(1 << 20, 16) == 4096 * 16 * 12
+    assert _native.lib.mg_replay_scratch_bytes(0, 4) == 0
 
 
 def test_timeout_step_is_2501():
