@@ -45,6 +45,12 @@ namespace {
 #ifndef MG_BLOCK
 #define MG_BLOCK 256
 #endif
+#ifndef MG_REPLAY_TCHUNK
+#define MG_REPLAY_TCHUNK 2  // replay store: steps one block walks (obs carried in registers)
+#endif
+#ifndef MG_REPLAY_PREFETCH
+#define MG_REPLAY_PREFETCH 1  // replay store: next step's obs row loaded before this step's work
+#endif
 #ifndef MG_QNET_PREFETCH
 #define MG_QNET_PREFETCH 3  // Q-net W2 fragments: 0 at use, 1/2 all up front, 3 one ahead
 #endif
@@ -1126,20 +1132,48 @@ __global__ __launch_bounds__(kBlock) void observe_kernel(const mg_params P, cons
 // ============================================================================ replay memory
 // The DQN replay memory (scripts/main.py:91-92 np.zeros((MEMORY_CAPACITY, 2*NUM_STATES+2)),
 // :115-119 store_transition, :130-135 the minibatch draw). A batch of T x n transitions is
-// appended in (t, i) order with three launches: per-block keep counts, a one-block scan that
-// turns them into ring positions and advances memory_counter, and the row writes. Rows are
-// gathered into an LDS tile in ring order and written as contiguous 8-byte stores (a row is
-// 88 B, so consecutive rows alternate 16-byte alignment).
+// appended in (t, i) order with two launches:
+//   replay_scan_kernel   one wave per 64 "write blocks" (t, 256-env slice): keep counts straight
+//                        from the won bits, a wave scan (in-group offsets), and the last wave
+//                        to finish (ticket + fences, nobody waits) scans the group totals into
+//                        ring positions and advances memory_counter;
+//   replay_write_kernel  one block per 256-env slice walking t = 0..T-1, the step's
+//                        observation kept in registers as the next transition's s (each obs row
+//                        is read once); rows gathered in LDS in ring order and written as
+//                        contiguous 8-byte stores (a row is 88 B: alignment alternates).
 constexpr int kRow = 2 * kObs + 2;  // 22 floats: s(10), a, r, s'(10)
-constexpr int kRBlock = 256;        // transitions per block (blockIdx.x: env slice, y: step)
-constexpr int kScanBlock = 1024;
+constexpr int kRBlock = 256;        // envs per write block
+constexpr int kRGroup = 64;         // write blocks per scan wave
 
 struct ReplayIn {
   mg_transitions X;
   int64_t n;
-  int64_t words;  // ceil(n / 64)
+  int64_t words;  // ceil(n / 64): won-mask words per step
+  int64_t nbx;    // ceil(n / 256): write blocks per step
+  int64_t nb;     // nbx * T
+  int32_t T;
   int32_t skip_won;
 };
+
+struct ReplayScratch {  // carved from the caller's scratch buffer
+  uint32_t* ticket;      // [1] at offset 0 whatever the sizes: zero between calls (the last
+                         //     wave resets it), so one buffer serves calls of any size
+  uint64_t* group_base;  // [ngroups] memory_counter before the group's first transition
+  uint32_t* local;       // [nb] transitions of earlier write blocks of the same group
+  uint32_t* group_total; // [ngroups]
+};
+
+__host__ __device__ inline int64_t replay_groups(int64_t nb) { return (nb + kRGroup - 1) / kRGroup; }
+
+__host__ __device__ inline ReplayScratch replay_scratch(void* base, int64_t nb) {
+  const int64_t ng = replay_groups(nb);
+  ReplayScratch S;
+  S.ticket = static_cast<uint32_t*>(base);
+  S.group_base = static_cast<uint64_t*>(base) + 1;
+  S.local = reinterpret_cast<uint32_t*>(S.group_base + ng);
+  S.group_total = S.local + nb;
+  return S;
+}
 
 __device__ __forceinline__ bool replay_keep(const ReplayIn& R, int t, int64_t i) {
   if (i >= R.n) return false;
@@ -1148,8 +1182,65 @@ __device__ __forceinline__ bool replay_keep(const ReplayIn& R, int t, int64_t i)
   return ((w >> (i & 63)) & 1u) == 0;
 }
 
-// Number of kept transitions of this block's threads before the calling thread (inclusive
-// of nothing) and the block total; counts in LDS per wave.
+// Kept transitions of write block (t, bx).
+__device__ __forceinline__ uint32_t replay_block_count(const ReplayIn& R, int t, int64_t bx) {
+  const int64_t i0 = bx * kRBlock;
+  const int64_t live = R.n - i0 < kRBlock ? R.n - i0 : kRBlock;
+  if (!R.skip_won || R.X.won_mask == nullptr) return static_cast<uint32_t>(live);
+  const uint64_t* w = R.X.won_mask + static_cast<int64_t>(t) * R.words + (i0 >> 6);
+  uint32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < kRBlock / 64; ++k) {
+    const int64_t v = live - 64 * k;  // live envs of this word
+    if (v <= 0) break;
+    const uint64_t m = v >= 64 ? ~0ull : ((1ull << v) - 1);
+    c += __popcll(~w[k] & m);
+  }
+  return c;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t u = __shfl_up(v, off);
+    if (lane >= off) v += u;
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(64) void replay_scan_kernel(const ReplayIn R, ReplayScratch S,
+                                                         uint64_t* counter) {
+  const int lane = threadIdx.x;
+  const int64_t ng = replay_groups(R.nb);
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * kRGroup + lane;
+  uint32_t c = 0;
+  if (b < R.nb) c = replay_block_count(R, static_cast<int>(b / R.nbx), b % R.nbx);
+  const uint32_t incl = wave_incl_scan(c);
+  if (b < R.nb) S.local[b] = incl - c;
+  if (lane == 63) S.group_total[blockIdx.x] = incl;
+  __threadfence();  // publish before taking a ticket
+  uint32_t ticket = 0;
+  if (lane == 0) ticket = atomicAdd(S.ticket, 1u);
+  ticket = __shfl(ticket, 0);
+  if (ticket != static_cast<uint32_t>(ng - 1)) return;  // not the last group to finish
+  __threadfence();  // acquire every group's total
+  const uint64_t c0 = *counter;
+  uint64_t carry = 0;
+  for (int64_t g0 = 0; g0 < ng; g0 += 64) {
+    const int64_t g = g0 + lane;
+    const uint32_t v = g < ng ? __atomic_load_n(S.group_total + g, __ATOMIC_RELAXED) : 0u;
+    const uint32_t gi = wave_incl_scan(v);
+    if (g < ng) S.group_base[g] = c0 + carry + (gi - v);
+    carry += __shfl(gi, 63);
+  }
+  if (lane == 0) {
+    *counter = c0 + carry;
+    *S.ticket = 0u;  // ready for the next call
+  }
+}
+
+// Rank of the calling thread among the block's kept threads, and the block total.
 __device__ __forceinline__ int block_rank(bool keep, int* wave_cnt, int& total) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t m = __ballot(keep);
@@ -1166,90 +1257,87 @@ __device__ __forceinline__ int block_rank(bool keep, int* wave_cnt, int& total) 
   return before + below;
 }
 
-__global__ __launch_bounds__(kRBlock) void replay_count_kernel(const ReplayIn R, uint32_t* counts) {
-  __shared__ int wave_cnt[kRBlock / 64];
-  const int t = blockIdx.y;
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * kRBlock + threadIdx.x;
-  int total;
-  block_rank(replay_keep(R, t, i), wave_cnt, total);
-  if (threadIdx.x == 0) counts[static_cast<int64_t>(t) * gridDim.x + blockIdx.x] = total;
+__device__ __forceinline__ void load_row10(const float* src, float (&v)[kObs]) {
+  const f32x2* s2 = reinterpret_cast<const f32x2*>(src);
+#pragma unroll
+  for (int k = 0; k < kObs / 2; ++k) {
+    const f32x2 a = s2[k];
+    v[2 * k] = a[0];
+    v[2 * k + 1] = a[1];
+  }
 }
 
-// One block: bases[b] = counter + sum(counts[0..b)), then counter += sum(counts). Thread j
-// owns the contiguous chunk [j*per, (j+1)*per): chunk sums, one block scan, chunk walk.
-__global__ __launch_bounds__(kScanBlock) void replay_scan_kernel(const uint32_t* counts,
-                                                                 uint64_t* bases, int64_t nb,
-                                                                 uint64_t* counter) {
-  __shared__ uint64_t part[kScanBlock];
-  const int tid = threadIdx.x;
-  const int64_t per = (nb + kScanBlock - 1) / kScanBlock;
-  const int64_t lo = tid * per, hi = lo + per < nb ? lo + per : nb;
-  uint64_t sum = 0;
-  for (int64_t b = lo; b < hi; ++b) sum += counts[b];
-  part[tid] = sum;
-  __syncthreads();
-  for (int off = 1; off < kScanBlock; off <<= 1) {  // Hillis-Steele inclusive scan
-    const uint64_t add = tid >= off ? part[tid - off] : 0u;
-    __syncthreads();
-    part[tid] += add;
-    __syncthreads();
-  }
-  const uint64_t c0 = *counter;
-  uint64_t run = c0 + part[tid] - sum;
-  for (int64_t b = lo; b < hi; ++b) {
-    bases[b] = run;
-    run += counts[b];
-  }
-  __syncthreads();  // every thread has read *counter
-  if (tid == 0) *counter = c0 + part[kScanBlock - 1];
-}
-
-__global__ __launch_bounds__(kRBlock) void replay_write_kernel(const ReplayIn R,
-                                                               const uint64_t* bases,
-                                                               const uint64_t* counter,
-                                                               float* rows, int64_t cap) {
+__global__ __launch_bounds__(kRBlock) void replay_write_kernel(const ReplayIn R, const ReplayScratch S,
+                                                               const uint64_t* counter, float* rows,
+                                                               int64_t cap) {
   __shared__ __attribute__((aligned(16))) float tile[kRBlock * kRow];
   __shared__ int wave_cnt[kRBlock / 64];
-  const int t = blockIdx.y;
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * kRBlock + threadIdx.x;
-  const bool keep = replay_keep(R, t, i);
-  int total;
-  const int rank = block_rank(keep, wave_cnt, total);
-  if (total == 0) return;  // uniform across the block
-  const uint64_t base = bases[static_cast<int64_t>(t) * gridDim.x + blockIdx.x];
+  const int64_t bx = blockIdx.x;
+  const int64_t i = bx * kRBlock + threadIdx.x;
+  const bool live = i < R.n;
+  const int t0 = blockIdx.y * MG_REPLAY_TCHUNK;
+  const int t1 = t0 + MG_REPLAY_TCHUNK < R.T ? t0 + MG_REPLAY_TCHUNK : R.T;
   const uint64_t end = *counter;  // memory_counter after this whole store
-  if (keep) {
-    const int64_t row = static_cast<int64_t>(t) * R.n + i;
-    const float* s = t == 0 ? R.X.obs_first + i * kObs : R.X.obs + (row - R.n) * kObs;
-    const bool done = R.X.done != nullptr && R.X.done[row] != 0;
-    const float* s2 = (done && R.X.final_obs) ? R.X.final_obs + row * kObs : R.X.obs + row * kObs;
-    float* d = tile + rank * kRow;
-    const f32x2* s_2 = reinterpret_cast<const f32x2*>(s);
-    const f32x2* s2_2 = reinterpret_cast<const f32x2*>(s2);
-#pragma unroll
-    for (int k = 0; k < kObs / 2; ++k) {
-      const f32x2 a = s_2[k], b = s2_2[k];
-      d[2 * k] = a[0];
-      d[2 * k + 1] = a[1];
-      d[kObs + 2 + 2 * k] = b[0];
-      d[kObs + 2 + 2 * k + 1] = b[1];
-    }
-    d[kObs] = static_cast<float>(R.X.a1[row]);
-    d[kObs + 1] = R.X.rew[2 * row];
-  }
-  __syncthreads();
-  // Only the newest `cap` transitions of the whole store survive sequential stores; they
-  // occupy distinct slots, so no two writes of this launch collide.
+  // Only the newest `cap` transitions survive sequential stores; they occupy distinct slots,
+  // so no two writes of this launch collide.
   const uint64_t first = end > static_cast<uint64_t>(cap) ? end - static_cast<uint64_t>(cap) : 0u;
-  const int skip = base >= first ? 0 : static_cast<int>(min<uint64_t>(first - base, total));
-  const uint64_t slot0 = (base + skip) % static_cast<uint64_t>(cap);
-  const int nel = (total - skip) * (kRow / 2);
-  const f32x2* src = reinterpret_cast<const f32x2*>(tile + skip * kRow);
-  for (int e2 = threadIdx.x; e2 < nel; e2 += kRBlock) {
-    const int rr = e2 / (kRow / 2), part = e2 - rr * (kRow / 2);
-    uint64_t slot = slot0 + rr;
-    if (slot >= static_cast<uint64_t>(cap)) slot %= static_cast<uint64_t>(cap);
-    st_out(reinterpret_cast<f32x2*>(rows + slot * kRow) + part, src[e2]);
+  float s[kObs], o[kObs];
+  if (live) {
+    load_row10(t0 == 0 ? R.X.obs_first + i * kObs : R.X.obs + ((t0 - 1) * R.n + i) * kObs, s);
+#if MG_REPLAY_PREFETCH
+    load_row10(R.X.obs + (t0 * R.n + i) * kObs, o);
+#endif
+  }
+  for (int t = t0; t < t1; ++t) {
+    const int64_t row = static_cast<int64_t>(t) * R.n + i;
+    const bool keep = replay_keep(R, t, i);
+#if MG_REPLAY_PREFETCH
+    float on[kObs];  // next step's row in flight while this step is gathered and written
+    if (live && t + 1 < t1) load_row10(R.X.obs + (row + R.n) * kObs, on);
+#else
+    if (live) load_row10(R.X.obs + row * kObs, o);
+#endif
+    int total;
+    const int rank = block_rank(keep, wave_cnt, total);
+    if (total > 0) {  // uniform across the block
+      const int64_t b = static_cast<int64_t>(t) * R.nbx + bx;
+      const uint64_t base = S.group_base[b / kRGroup] + S.local[b];
+      if (keep) {
+        float* d = tile + rank * kRow;
+        const bool done = R.X.done != nullptr && R.X.done[row] != 0;
+        float s2[kObs];
+        if (done && R.X.final_obs)
+          load_row10(R.X.final_obs + row * kObs, s2);
+        else
+#pragma unroll
+          for (int k = 0; k < kObs; ++k) s2[k] = o[k];
+#pragma unroll
+        for (int k = 0; k < kObs; ++k) {
+          d[k] = s[k];
+          d[kObs + 2 + k] = s2[k];
+        }
+        d[kObs] = static_cast<float>(R.X.a1[row]);
+        d[kObs + 1] = R.X.rew[2 * row];
+      }
+      __syncthreads();
+      const int skip = base >= first ? 0 : static_cast<int>(min<uint64_t>(first - base, total));
+      const uint64_t slot0 = (base + skip) % static_cast<uint64_t>(cap);
+      const int nel = (total - skip) * (kRow / 2);
+      const f32x2* src = reinterpret_cast<const f32x2*>(tile + skip * kRow);
+      for (int e2 = threadIdx.x; e2 < nel; e2 += kRBlock) {
+        const int rr = e2 / (kRow / 2), part = e2 - rr * (kRow / 2);
+        uint64_t slot = slot0 + rr;
+        if (slot >= static_cast<uint64_t>(cap)) slot %= static_cast<uint64_t>(cap);
+        st_out(reinterpret_cast<f32x2*>(rows + slot * kRow) + part, src[e2]);
+      }
+    }
+    __syncthreads();  // tile and wave counts are reused by the next step
+#pragma unroll
+    for (int k = 0; k < kObs; ++k) s[k] = o[k];
+#if MG_REPLAY_PREFETCH
+#pragma unroll
+    for (int k = 0; k < kObs; ++k) o[k] = on[k];
+#endif
   }
 }
 
@@ -1549,7 +1637,8 @@ int mg_rollout_qnet(const mg_params* params, const mg_state* state, const mg_tra
 size_t mg_replay_scratch_bytes(int64_t n, int32_t num_steps) {
   if (n <= 0 || num_steps <= 0) return 0;
   const int64_t nb = ((n + kRBlock - 1) / kRBlock) * num_steps;
-  return static_cast<size_t>(((nb * 4 + 7) & ~int64_t{7}) + nb * 8);
+  const int64_t ng = replay_groups(nb);
+  return static_cast<size_t>((8 + ng * 8 + nb * 4 + ng * 4 + 7) & ~int64_t{7});
 }
 
 int mg_replay_store(float* rows, uint64_t* counter, int64_t capacity, const mg_transitions* tr,
@@ -1557,8 +1646,7 @@ int mg_replay_store(float* rows, uint64_t* counter, int64_t capacity, const mg_t
                     size_t scratch_bytes, void* stream) {
   if (!rows || !counter || !tr) return fail(hipErrorInvalidValue, "%s", "mg_replay_store: NULL pointer");
   if (capacity < 1) return fail(hipErrorInvalidValue, "%s", "mg_replay_store: capacity < 1");
-  if (n < 0 || num_steps < 0 || num_steps > 65535)
-    return fail(hipErrorInvalidValue, "%s", "mg_replay_store: need n >= 0 and 0 <= num_steps <= 65535");
+  if (n < 0 || num_steps < 0) return fail(hipErrorInvalidValue, "%s", "mg_replay_store: n < 0 or num_steps < 0");
   if (n == 0 || num_steps == 0) return 0;
   if (!tr->obs_first || !tr->obs || !tr->a1 || !tr->rew)
     return fail(hipErrorInvalidValue, "%s", "mg_replay_store: obs_first, obs, a1 and rew are required");
@@ -1567,22 +1655,27 @@ int mg_replay_store(float* rows, uint64_t* counter, int64_t capacity, const mg_t
        reinterpret_cast<uintptr_t>(tr->rew) | reinterpret_cast<uintptr_t>(scratch)) & 7)
     return fail(hipErrorInvalidValue, "%s", "mg_replay_store: float buffers and scratch must be 8-byte aligned");
   const int64_t nbx = (n + kRBlock - 1) / kRBlock;
-  if (nbx > 0x7fffffff) return fail(hipErrorInvalidValue, "%s", "mg_replay_store: n exceeds the grid limit");
+  const int64_t nb = nbx * num_steps;
+  if (nbx > 0x7fffffff || replay_groups(nb) > 0x7fffffff)
+    return fail(hipErrorInvalidValue, "%s", "mg_replay_store: n * num_steps exceeds the grid limit");
   if (!scratch || scratch_bytes < mg_replay_scratch_bytes(n, num_steps))
     return fail(hipErrorInvalidValue, "%s", "mg_replay_store: scratch smaller than mg_replay_scratch_bytes(n, num_steps)");
-  const int64_t nb = nbx * num_steps;
-  uint32_t* counts = static_cast<uint32_t*>(scratch);
-  uint64_t* bases = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(scratch) + ((nb * 4 + 7) & ~int64_t{7}));
+  const unsigned chunks = static_cast<unsigned>((num_steps + MG_REPLAY_TCHUNK - 1) / MG_REPLAY_TCHUNK);
+  if (chunks > 65535) return fail(hipErrorInvalidValue, "%s", "mg_replay_store: num_steps too large");
   ReplayIn R{};
   R.X = *tr;
   R.n = n;
   R.words = (n + 63) >> 6;
+  R.nbx = nbx;
+  R.nb = nb;
+  R.T = num_steps;
   R.skip_won = skip_ego_won;
+  const ReplayScratch S = replay_scratch(scratch, nb);
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const dim3 grid(static_cast<unsigned>(nbx), static_cast<unsigned>(num_steps));
-  hipLaunchKernelGGL(replay_count_kernel, grid, dim3(kRBlock), 0, st, R, counts);
-  hipLaunchKernelGGL(replay_scan_kernel, dim3(1), dim3(kScanBlock), 0, st, counts, bases, nb, counter);
-  hipLaunchKernelGGL(replay_write_kernel, grid, dim3(kRBlock), 0, st, R, bases, counter, rows, capacity);
+  hipLaunchKernelGGL(replay_scan_kernel, dim3(static_cast<unsigned>(replay_groups(nb))), dim3(64), 0, st,
+                     R, S, counter);
+  hipLaunchKernelGGL(replay_write_kernel, dim3(static_cast<unsigned>(nbx), chunks), dim3(kRBlock), 0, st, R,
+                     S, counter, rows, capacity);
   return finish_launch("mg_replay_store");
 }
 

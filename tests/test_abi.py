@@ -84,7 +84,8 @@ def test_argument_errors_without_gpu():
     assert rc != 0 and b"scratch" in _native.lib.mg_last_error()
     rc = _native.lib.mg_replay_sample(fake, fake, 0, 0, 0, 0, fake, None, 4, None)
     assert rc != 0 and b"capacity" in _native.lib.mg_last_error()
-    assert _native.lib.mg_replay_scratch_bytes(1 << 20, 16) == 4096 * 16 * 12
+    # 65536 write blocks in 1024 scan groups: ticket (8) + bases u64 + offsets u32 + totals u32
+    assert _native.lib.mg_replay_scratch_bytes(1 << 20, 16) == 8 + 1024 * 8 + 65536 * 4 + 1024 * 4
     assert _native.lib.mg_replay_scratch_bytes(0, 4) == 0
 
 

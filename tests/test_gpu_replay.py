@@ -156,3 +156,31 @@ def test_sample_rows_are_memory_at_oracle_slots(torch, coracle, filled_only):
     s, a, r, s2 = ring.sample(128, seed=9, draw=77, filled_only=filled_only)
     assert s.shape == (128, 10) and a.shape == (128, 1) and a.dtype == torch.int64
     assert r.shape == (128, 1) and s2.shape == (128, 10)
+
+
+def test_mixed_size_stores_share_scratch(torch):
+    """Stores of different shapes through one ring (the scratch buffer is reused, its ticket
+    must stay at zero between calls); random won words, including bits past n that must be
+    ignored; random done rows taking s' from final_obs."""
+    from merging_gym import ReplayRing
+
+    rng = np.random.default_rng(42)
+    cap = 20_000
+    ring = ReplayRing(cap, device="cuda:0")
+    mem = np.zeros((cap, 22), np.float32)
+    c = 0
+    for n, T in ((3000, 7), (5, 1), (700, 33), (1, 2), (3000, 7), (257, 64)):
+        obs0 = rng.standard_normal((n, 10)).astype(np.float32)
+        obs = rng.standard_normal((T, n, 10)).astype(np.float32)
+        fobs = rng.standard_normal((T, n, 10)).astype(np.float32)
+        a1 = rng.integers(0, 5, (T, n)).astype(np.int8)
+        rew = rng.standard_normal((T, n, 2)).astype(np.float32)
+        done = (rng.random((T, n)) < 0.1).astype(np.uint8)
+        words = rng.integers(0, 2**63, (T, (n + 63) // 64), dtype=np.int64)
+        words &= rng.integers(0, 2**63, words.shape, dtype=np.int64)  # ~25% of bits set
+        dev = lambda a: torch.from_numpy(a).cuda()  # noqa: E731
+        ring.store(dev(obs0), dev(obs), dev(a1), dev(rew), dev(done), dev(fobs), dev(words))
+        c = mo.replay_store(mem, c, obs0, obs, a1, rew, done, fobs, _unpack(words, n))
+        assert ring.memory_counter == c, (n, T)
+        np.testing.assert_array_equal(ring.memory.cpu().numpy(), mem, err_msg=str((n, T)))
+    assert int(ring._scratch[0].item()) == 0  # the ticket word

@@ -140,9 +140,12 @@ def main():
     ap.add_argument("--T", type=int, default=16)
     ap.add_argument("--rollouts", type=int, default=4)
     ap.add_argument("--qnet", action="store_true", help="A/B the fused Q-net rollout instead")
+    ap.add_argument("--replay", action="store_true", help="A/B mg_replay_store instead")
     a = ap.parse_args()
     if a.qnet:
         return main_qnet(a)
+    if a.replay:
+        return main_replay(a)
     beds = {os.path.basename(p): Bed(bind(p), a.envs, a.T) for p in a.libs}
     ev = Events(max(a.steps, a.rollouts))
     res = {k: {"step": [], "rollout": [], "step_wall": [], "rollout_wall": []} for k in beds}
@@ -218,6 +221,58 @@ def main_qnet(a):
     for name, d in res.items():
         print(f"{name:24s} qnet(none) {1e3 * statistics.median(d[0]):7.2f} us/step   "
               f"qnet(self) {1e3 * statistics.median(d[2]):7.2f} us/step", flush=True)
+
+
+def main_replay(a):
+    """mg_replay_store of one rollout's trajectory (T x envs transitions, made once with the
+    default library) into a 2^24-row ring, per variant; events on the current stream."""
+    from merging_gym import MergeVecEnv
+
+    env = MergeVecEnv(a.envs, device="cuda")
+    for k in range(230):
+        env.step_random(5, step_idx=k)
+    obs0 = env.observe().clone()
+    traj = env.rollout_random(a.T, 5, first_step=230)
+    ptr = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    tr = nat.Transitions(ptr(obs0), ptr(traj["obs"]), ptr(traj["final_observation"]), ptr(traj["a1"]),
+                         ptr(traj["rew"]), ptr(traj["done"].view(torch.uint8)), ptr(traj["won_mask"]))
+    cap = 1 << 24
+    beds = {}
+    for p in a.libs:
+        lib = ctypes.CDLL(p)
+        lib.mg_replay_scratch_bytes.argtypes = [ctypes.c_int64, ctypes.c_int32]
+        lib.mg_replay_scratch_bytes.restype = ctypes.c_size_t
+        lib.mg_replay_store.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                        ctypes.POINTER(nat.Transitions), ctypes.c_int64, ctypes.c_int32,
+                                        ctypes.c_int32, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+        nbytes = lib.mg_replay_scratch_bytes(a.envs, a.T)
+        beds[os.path.basename(p)] = (lib, torch.zeros((cap, 22), device="cuda"),
+                                     torch.zeros(1, dtype=torch.int64, device="cuda"),
+                                     torch.zeros(nbytes // 8 + 1, dtype=torch.int64, device="cuda"), nbytes)
+
+    def store(b):
+        lib, ring, ctr, scr, nbytes = b
+        rc = lib.mg_replay_store(ring.data_ptr(), ctr.data_ptr(), cap, ctypes.byref(tr), a.envs, a.T, 1,
+                                 scr.data_ptr(), nbytes, torch.cuda.current_stream().cuda_stream)
+        assert rc == 0
+
+    for b in beds.values():
+        store(b)
+    torch.cuda.synchronize()
+    res = {k: [] for k in beds}
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.rollouts)]
+    for r in range(a.rounds):
+        for name in (list(beds) if r % 2 == 0 else list(reversed(beds))):
+            for j in range(a.rollouts):
+                ev[2 * j].record()
+                store(beds[name])
+                ev[2 * j + 1].record()
+            torch.cuda.synchronize()
+            res[name] += [ev[2 * j].elapsed_time(ev[2 * j + 1]) for j in range(a.rollouts)]
+    kept = int(beds[next(iter(beds))][2].item()) // (1 + a.rounds * a.rollouts)
+    for name, d in res.items():
+        print(f"{name:28s} store {1e3 * statistics.median(d):8.1f} us (min {1e3 * min(d):8.1f})  "
+              f"{kept / (statistics.median(d) * 1e-3):.3e} transitions/s", flush=True)
 
 
 if __name__ == "__main__":
