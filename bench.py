@@ -110,7 +110,7 @@ def rollout_leg(env, args, world, dist, torch):
     T, L, E = args.rollout_steps, args.rollout_launches, env.num_envs
     k = 10_000_000
     for _ in range(3):
-        env.rollout_random(T, args.seed, first_step=k, final_observation=False)
+        env.rollout_random(T, args.seed, first_step=k, final_observation=False, won_mask=False)
         k += T
     timer = KernelTimer(L)
     torch.cuda.synchronize()
@@ -119,7 +119,7 @@ def rollout_leg(env, args, world, dist, torch):
     t0 = time.perf_counter()
     for j in range(L):
         timer.arm(j)
-        env.rollout_random(T, args.seed, first_step=k, final_observation=False)
+        env.rollout_random(T, args.seed, first_step=k, final_observation=False, won_mask=False)
         k += T
     torch.cuda.synchronize()
     if world > 1:
@@ -160,7 +160,8 @@ def qnet_leg(env, args, world, dist, torch, opponent):
     T, L, E = args.rollout_steps, args.qnet_launches, env.num_envs
     k = 20_000_000
     for _ in range(2):
-        env.rollout_qnet(T, qnet, args.seed, opponent=opponent, first_step=k, final_observation=False)
+        env.rollout_qnet(T, qnet, args.seed, opponent=opponent, first_step=k, final_observation=False,
+                         won_mask=False)
         k += T
     timer = KernelTimer(L)
     torch.cuda.synchronize()
@@ -169,7 +170,8 @@ def qnet_leg(env, args, world, dist, torch, opponent):
     t0 = time.perf_counter()
     for j in range(L):
         timer.arm(j)
-        env.rollout_qnet(T, qnet, args.seed, opponent=opponent, first_step=k, final_observation=False)
+        env.rollout_qnet(T, qnet, args.seed, opponent=opponent, first_step=k, final_observation=False,
+                         won_mask=False)
         k += T
     torch.cuda.synchronize()
     if world > 1:
@@ -180,6 +182,15 @@ def qnet_leg(env, args, world, dist, torch, opponent):
     kernel_ms = sum(durs) / len(durs)
     nets = 2 if opponent == "self" else 1
     per_s = E * T / (kernel_ms * 1e-3)
+    # BASELINE config 5: greedy-action agreement with the reference's fp32 Net on the CPU
+    # (main.py:30-47, re-declared here with torch) over the envs' current observations
+    sample = env.observe()[: 1 << 16].clone()
+    greedy_gpu = qnet.forward(sample).argmax(1).cpu()
+    w = {k.split("/", 1)[1]: torch.from_numpy(f[k]) for k in f.files if k.startswith("l1/")}
+    x = sample.cpu()
+    h = torch.relu(x @ w["fc1.weight"].T + w["fc1.bias"])
+    h = torch.relu(h @ w["fc2.weight"].T + w["fc2.bias"])
+    greedy_cpu = (h @ w["out.weight"].T + w["out.bias"]).argmax(1)
     return {"kernel": f"qnet_rollout_kernel<{ {'none': 0, 'uniform': 1, 'self': 2}[opponent] }>",
             "opponent": opponent, "steps_per_launch": T, "launches": L, "dtype": "bf16 (fp32 accumulate)",
             "value": world * E * T * L / elapsed, "unit": "env-steps/s",
@@ -187,7 +198,9 @@ def qnet_leg(env, args, world, dist, torch, opponent):
             "useful_tflops": nets * QNET_USEFUL_FLOP * per_s / 1e12,
             "mfma_tflops": nets * QNET_MFMA_FLOP * per_s / 1e12,
             "peak_tflops": MFMA_BF16_PEAK_TFLOPS,
-            "frac_useful": nets * QNET_USEFUL_FLOP * per_s / 1e12 / MFMA_BF16_PEAK_TFLOPS}
+            "frac_useful": nets * QNET_USEFUL_FLOP * per_s / 1e12 / MFMA_BF16_PEAK_TFLOPS,
+            "greedy_agreement_vs_fp32_cpu": float((greedy_gpu == greedy_cpu).double().mean()),
+            "agreement_sample": int(x.shape[0])}
 
 
 def replay_algorithmic_bytes(n, T, kept, done_rows):

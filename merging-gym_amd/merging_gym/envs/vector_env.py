@@ -182,18 +182,19 @@ class MergeVecEnv:
         return self._outputs()
 
     def rollout_random(self, num_steps: int, seed: int, opponent_random: bool = True,
-                       first_step=None, final_observation: bool = True):
+                       first_step=None, final_observation: bool = True, won_mask: bool = True):
         """`num_steps` steps with device-drawn actions in ONE kernel launch (the env stays in
         registers; its state is read and written once). Bit-identical to `num_steps` calls of
         step_random(seed, step_idx=first_step + t). Returns a dict of [T, N, ...] tensors:
         obs, rew, done (bool), collision (bool), a1, a2, final_observation (rows where done)
         and won_mask ([T, ceil(N/64)] int64, bit i of step t = env i's winner == 1 after that
-        step -- ReplayRing.store_rollout's filter). The buffers are reused by the next rollout
-        of the same length."""
+        step -- ReplayRing.store_rollout's filter; None with won_mask=False, which saves a
+        ballot and a store per wave-step). The buffers are reused by the next rollout with the
+        same T and output choices."""
         nat = self._nat
         T, n = int(num_steps), self.num_envs
         k0 = self._step_idx if first_step is None else int(first_step)
-        buf = self._traj(T, final_observation)
+        buf = self._traj(T, final_observation, won_mask)
         rc = nat.lib.mg_rollout_random(
             self._p_ref, self._s_ref, ctypes.byref(buf["_traj"]), self._st_ref, n, self.env_offset,
             seed & 0xFFFFFFFFFFFFFFFF, k0 & 0xFFFFFFFFFFFFFFFF, T, 1 if opponent_random else 0,
@@ -202,11 +203,12 @@ class MergeVecEnv:
         self._step_idx = k0 + T
         return buf["_result"]
 
-    def _traj(self, T, final_observation):
-        """[T, N, ...] trajectory buffers, reused while T and the final-obs choice stay the same."""
+    def _traj(self, T, final_observation, won_mask=True):
+        """[T, N, ...] trajectory buffers, reused while T and the output choices stay the same."""
         torch, nat, n = self._torch, self._nat, self.num_envs
         buf = getattr(self, "_traj_bufs", None)
-        if buf is None or buf["T"] != T or (buf["final_observation"] is None) == final_observation:
+        if (buf is None or buf["T"] != T or (buf["final_observation"] is None) == final_observation
+                or (buf["won_mask"] is None) == won_mask):
             dev = self.device
             buf = {"T": T,
                    "obs": torch.empty((T, n, _OBS_DIM), dtype=torch.float32, device=dev),
@@ -217,7 +219,8 @@ class MergeVecEnv:
                    "a2": torch.empty((T, n), dtype=torch.int8, device=dev),
                    "final_observation": (torch.full((T, n, _OBS_DIM), float("nan"), dtype=torch.float32,
                                                     device=dev) if final_observation else None),
-                   "won_mask": torch.zeros((T, (n + 63) // 64), dtype=torch.int64, device=dev)}
+                   "won_mask": (torch.zeros((T, (n + 63) // 64), dtype=torch.int64, device=dev)
+                                if won_mask else None)}
             ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
             buf["_traj"] = nat.Traj(*(ptr(buf[k]) for k in ("obs", "rew", "done", "collision", "a1", "a2",
                                                              "final_observation", "won_mask")))
@@ -230,7 +233,7 @@ class MergeVecEnv:
 
     def rollout_qnet(self, num_steps: int, qnet, seed: int, opponent: str = "none",
                      episilo: float = 0.7, opp_episilo: float = 0.7, first_step=None,
-                     final_observation: bool = True):
+                     final_observation: bool = True, won_mask: bool = True):
         """`num_steps` steps with the reference's epsilon-greedy DQN policy (main.py:99-112)
         computed on the device (bf16 MFMA) and fused with the env step, one launch.
         opponent: "none" (L0), "uniform", or "self" (the same net on the swapped observation,
@@ -241,7 +244,7 @@ class MergeVecEnv:
         T, n = int(num_steps), self.num_envs
         mode = {"none": 0, "uniform": 1, "self": 2}[opponent]
         k0 = self._step_idx if first_step is None else int(first_step)
-        buf = self._traj(T, final_observation)
+        buf = self._traj(T, final_observation, won_mask)
         rc = nat.lib.mg_rollout_qnet(
             self._p_ref, self._s_ref, ctypes.byref(buf["_traj"]), self._st_ref, n, self.env_offset,
             seed & 0xFFFFFFFFFFFFFFFF, k0 & 0xFFFFFFFFFFFFFFFF, T, qnet.packed.data_ptr(), qnet.out_dim,

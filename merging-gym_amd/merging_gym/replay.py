@@ -107,8 +107,8 @@ class ReplayRing:
             if tuple(won_mask.shape) != (T, (n + 63) // 64):
                 raise ValueError(f"won_mask must have shape {(T, (n + 63) // 64)}")
         elif skip_ego_won:
-            raise ValueError("skip_ego_won needs the won_mask of the step(s) (main.py:209); "
-                             "pass won_mask or skip_ego_won=False")
+            raise ValueError("skip_ego_won needs the won_mask of the step(s) (main.py:209): roll out "
+                             "with won_mask=True / MergeVecEnv(won_mask=True), or pass skip_ego_won=False")
         ptr = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
         tr = _native.Transitions(ptr(obs_first), ptr(obs), ptr(final_obs), ptr(a1), ptr(rew),
                                  ptr(done), ptr(won_mask) if skip_ego_won else None)

@@ -72,8 +72,10 @@ class Bed:
         self.out = nat.Outputs(self.obs.data_ptr(), self.rew.data_ptr(), self.done.data_ptr(),
                                self.coll.data_ptr(), None, self.fobs.data_ptr(), None, None)
         self.stats = nat.Stats(self.ret_sum.data_ptr(), self.counts.data_ptr())
+        self.twon = torch.zeros((T, (n + 63) // 64), dtype=torch.int64, device=dev)
+        won = self.twon.data_ptr() if os.environ.get("MG_AB_WON") == "1" else None
         self.traj = nat.Traj(self.tobs.data_ptr(), self.trew.data_ptr(), self.tdone.data_ptr(),
-                             self.tcoll.data_ptr(), self.ta[0].data_ptr(), self.ta[1].data_ptr(), None)
+                             self.tcoll.data_ptr(), self.ta[0].data_ptr(), self.ta[1].data_ptr(), None, won)
         self.k = 0
         assert lib.mg_reset(ctypes.byref(self.params), ctypes.byref(self.state), None, None, n, None) == 0
 
@@ -139,6 +141,7 @@ def main():
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--T", type=int, default=16)
     ap.add_argument("--rollouts", type=int, default=4)
+    ap.add_argument("--warm", type=int, default=200, help="single steps before timing (1000+: steady state)")
     ap.add_argument("--qnet", action="store_true", help="A/B the fused Q-net rollout instead")
     ap.add_argument("--replay", action="store_true", help="A/B mg_replay_store instead")
     a = ap.parse_args()
@@ -151,7 +154,7 @@ def main():
     res = {k: {"step": [], "rollout": [], "step_wall": [], "rollout_wall": []} for k in beds}
     import time
     for b in beds.values():  # warm up (and get into mixed episode phases)
-        for _ in range(200):
+        for _ in range(a.warm):
             b.step()
         b.rollout()
     torch.cuda.synchronize()
@@ -204,7 +207,7 @@ def main_qnet(a):
     beds = {os.path.basename(p): Bed(bind(p), a.envs, a.T) for p in a.libs}
     for b in beds.values():
         b.pack_net(w)
-        for _ in range(100):
+        for _ in range(a.warm):
             b.step()
     ev = Events(a.rollouts)
     res = {k: {0: [], 2: []} for k in beds}
