@@ -105,29 +105,26 @@ def rollout_leg(env, args, world, dist, torch):
     """The fused T-step kernel (mg_rollout_random): same per-step work and outputs, the env's
     state read and written once per launch. Algorithmic bytes per env-step:
     52 (obs 40 + rew 8 + done 1 + coll 1 + actions 2) + 104 / T (state in and out)."""
-    from merging_gym.profiling import KernelTimer
-
     T, L, E = args.rollout_steps, args.rollout_launches, env.num_envs
     k = 10_000_000
     for _ in range(3):
         env.rollout_random(T, args.seed, first_step=k, final_observation=False, won_mask=False)
         k += T
-    timer = KernelTimer(L)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
+    ev0.record()
     for j in range(L):
-        timer.arm(j)
         env.rollout_random(T, args.seed, first_step=k, final_observation=False, won_mask=False)
         k += T
+    ev1.record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    durs = timer.durations_ms()
-    timer.close()
-    kernel_ms = sum(durs) / len(durs)
+    kernel_ms = ev0.elapsed_time(ev1) / L
     t = torch.tensor([elapsed], dtype=torch.float64,
                      device="cpu" if args.dist_backend != "nccl" else env.device)
     if world > 1:
@@ -152,7 +149,6 @@ def qnet_leg(env, args, world, dist, torch, opponent):
     import numpy as np
 
     from merging_gym.policy import QNet
-    from merging_gym.profiling import KernelTimer
 
     f = np.load(os.path.join(ROOT, "tests", "golden", "dqn_checkpoints.npz"))
     qnet = QNet.from_state_dict({k.split("/", 1)[1]: f[k] for k in f.files if k.startswith("l1/")},
@@ -163,23 +159,22 @@ def qnet_leg(env, args, world, dist, torch, opponent):
         env.rollout_qnet(T, qnet, args.seed, opponent=opponent, first_step=k, final_observation=False,
                          won_mask=False)
         k += T
-    timer = KernelTimer(L)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
+    ev0.record()
     for j in range(L):
-        timer.arm(j)
         env.rollout_qnet(T, qnet, args.seed, opponent=opponent, first_step=k, final_observation=False,
                          won_mask=False)
         k += T
+    ev1.record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    durs = timer.durations_ms()
-    timer.close()
-    kernel_ms = sum(durs) / len(durs)
+    kernel_ms = ev0.elapsed_time(ev1) / L
     nets = 2 if opponent == "self" else 1
     per_s = E * T / (kernel_ms * 1e-3)
     # BASELINE config 5: greedy-action agreement with the reference's fp32 Net on the CPU
@@ -319,33 +314,41 @@ def main():
     env.clear_statistics()
     torch.cuda.synchronize()
 
-    # per-launch kernel time: HIP events recorded by each dispatch packet (hipExtLaunchKernel)
-    use_events = not args.no_events
-    every = max(1, args.event_every)
-    if use_events:
-        from merging_gym.profiling import KernelTimer
-
-        timer = KernelTimer((args.steps + every - 1) // every)
+    # Timed region: K launches back to back, bracketed by a barrier + synchronize, with one HIP
+    # event pair recorded on the stream the kernels run on (torch's current stream, which
+    # MergeVecEnv launches on). Average launch duration = region / K (launch gaps included).
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev0.record()
     for k in range(args.steps):
-        if use_events and k % every == 0:
-            timer.arm(k // every)
         step(args.warmup + k)
+    ev1.record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kernel_ms = None
-    if use_events:
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps
+
+    # untimed: per-dispatch durations (events written by the dispatch packets themselves,
+    # hipExtLaunchKernel via mg_time_next_launch) for a sample of launches, for reference
+    dispatch_ms = None
+    if not args.no_events:
+        from merging_gym.profiling import KernelTimer
+
+        nsamp = max(1, min(64, args.steps // max(1, args.event_every)))
+        timer = KernelTimer(nsamp)
+        for j in range(nsamp):
+            timer.arm(j)
+            step(args.warmup + args.steps + j)
+        torch.cuda.synchronize()
         durs = timer.durations_ms()
-        kernel_ms = sum(durs) / len(durs)
+        dispatch_ms = sum(durs) / len(durs)
         timer.close()
 
-    t = torch.tensor([elapsed, kernel_ms or 0.0], dtype=torch.float64,
-                     device="cpu" if host_coll else device)
+    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cpu" if host_coll else device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kernel_ms_max = float(t[0]), float(t[1])
@@ -401,7 +404,9 @@ def main():
                          "frac": (achieved / HBM_PEAK_GBPS) if achieved else None,
                          "traffic": pmc, "kernel": KERNEL_NAME,
                          "bytes_per_env_step": BYTES_PER_ENV_STEP,
-                         "kernel_ms_mean": kernel_ms, "kernel_ms_mean_max_rank": kernel_ms_max},
+                         "kernel_ms_mean": kernel_ms, "kernel_ms_mean_max_rank": kernel_ms_max,
+                         "timing": "HIP events recorded on the launch stream around the K timed launches, / K",
+                         "kernel_ms_dispatch_sample": dispatch_ms},
             "episodes": episodes,
         }
         if rollout is not None:

@@ -71,7 +71,8 @@ class Bed:
         self.state = nat.State(*(x.data_ptr() for x in self.t))
         self.out = nat.Outputs(self.obs.data_ptr(), self.rew.data_ptr(), self.done.data_ptr(),
                                self.coll.data_ptr(), None, self.fobs.data_ptr(), None, None)
-        self.stats = nat.Stats(self.ret_sum.data_ptr(), self.counts.data_ptr())
+        self.stats = (nat.Stats() if os.environ.get("MG_AB_NOSTATS") == "1"
+                      else nat.Stats(self.ret_sum.data_ptr(), self.counts.data_ptr()))
         self.twon = torch.zeros((T, (n + 63) // 64), dtype=torch.int64, device=dev)
         won = self.twon.data_ptr() if os.environ.get("MG_AB_WON") == "1" else None
         self.traj = nat.Traj(self.tobs.data_ptr(), self.trew.data_ptr(), self.tdone.data_ptr(),
