@@ -51,6 +51,18 @@ namespace {
 #ifndef MG_REPLAY_PREFETCH
 #define MG_REPLAY_PREFETCH 1  // replay store: next step's obs row loaded before this step's work
 #endif
+#ifndef MG_SINCOS_COLD
+#define MG_SINCOS_COLD 1  // the |t| >= 1/16 sincos fallback as an out-of-line call
+#endif
+#ifndef MG_QNET_BIAS_RELOAD
+#define MG_QNET_BIAS_RELOAD 1  // Q-net: both column tiles load the layer-2 bias from LDS
+#endif
+#ifndef MG_QNET_PRIO
+#define MG_QNET_PRIO 0  // Q-net rollout: s_setprio 1 for waves 4-7
+#endif
+#ifndef MG_QNET_STAGGER
+#define MG_QNET_STAGGER 0  // Q-net rollout: waves 4-7 sleep STAGGER x 8128 cycles at the start
+#endif
 #ifndef MG_QNET_PREFETCH
 #define MG_QNET_PREFETCH 3  // Q-net W2 fragments: 0 at use, 1/2 all up front, 3 one ahead
 #endif
@@ -132,6 +144,17 @@ __device__ __forceinline__ double div_const(double x, double d, double inv) {
 // in fma form: the correction terms are < 7e-4 of the result, so the one rounding of the
 // final fma dominates and the result agrees with libm's sin/cos to <= 1 ulp (identical in
 // 99.98 % of 2e7 samples vs glibc). Larger |theta| takes the device library's sincos.
+// The device library's sincos for |t| >= 1/16 (only reached off the live-episode range, e.g.
+// stepping far past done). Kept out of line: inlined, the compiler hoists its polynomial
+// constants into VGPRs for the whole step loop of the T-step kernels, which then spill.
+#if MG_SINCOS_COLD
+__device__ __attribute__((noinline)) void sincos_cold(double t, double* s, double* c) {
+  sincos(t, s, c);
+}
+#else
+__device__ __forceinline__ void sincos_cold(double t, double* s, double* c) { sincos(t, s, c); }
+#endif
+
 __device__ __forceinline__ void arc_sincos(double t, double& s, double& c) {
 #if MG_FAST_SINCOS
   if (fabs(t) < 0.0625) {
@@ -148,8 +171,10 @@ __device__ __forceinline__ void arc_sincos(double t, double& s, double& c) {
     c = fma(t2, pc, 1.0);
     return;
   }
-#endif
+  sincos_cold(t, &s, &c);
+#else
   sincos(t, &s, &c);
+#endif
 }
 
 // lon2coord (merging_env.py:48-58): position along the arc -> (x longitudinal, y lateral).
@@ -760,6 +785,30 @@ __device__ __forceinline__ bf16x8 relu_bf16(const f32x16& c, int s) {
   return out;
 }
 
+// Layer-1 B fragment of one env: features k = 8h .. 8h+7 of its observation row (zero past
+// 10), in the swapped order state[5:] + state[:5] when swap (main.py:199). The row is read
+// with five unconditional ds_read_b64 and converted pairwise; the lane half picks its pairs
+// with selects (per-element conditional loads cost a full LDS wait each).
+__device__ __forceinline__ bf16x8 qnet_input(const float* row, bool swap, int h) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  float v[kObs];
+#pragma unroll
+  for (int k = 0; k < kObs / 2; ++k) {
+    const f32x2 t = reinterpret_cast<const f32x2*>(row)[k];
+    v[2 * k] = t[0];
+    v[2 * k + 1] = t[1];
+  }
+  uint32_t pr[kObs / 2];
+#pragma unroll
+  for (int k = 0; k < kObs / 2; ++k) {
+    const int a = swap ? (2 * k + 5) % kObs : 2 * k, b = swap ? (2 * k + 6) % kObs : 2 * k + 1;
+    pr[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{v[a], v[b]}, bf16x2));
+  }
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 w = h ? u32x4{pr[4], 0u, 0u, 0u} : u32x4{pr[0], pr[1], pr[2], pr[3]};
+  return __builtin_bit_cast(bf16x8, w);
+}
+
 __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
@@ -859,17 +908,21 @@ __device__ __forceinline__ void qnet_forward(const uint8_t* net, const float* ti
     const float* B1 = B1_ + z;
     const float* B2 = B2_ + z;
     const float* B3 = B3_ + z;
-    bf16x8 xb0, xb1;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = 8 * h + j;
-      const int src = swap ? (k < 5 ? k + 5 : k - 5) : k;
-      xb0[j] = static_cast<__bf16>(k < kObs ? tile[(row0 + r) * kObs + src] : 0.f);
-      xb1[j] = static_cast<__bf16>(k < kObs ? tile[(row0 + 32 + r) * kObs + src] : 0.f);
-    }
+    const bf16x8 xb0 = qnet_input(tile + (row0 + r) * kObs, swap, h);
+    const bf16x8 xb1 = qnet_input(tile + (row0 + 32 + r) * kObs, swap, h);
     f32x16 acc2a[4], acc2b[4];
+#if MG_QNET_BIAS_RELOAD
+    // each accumulator loads its bias from LDS itself: sharing one load costs 16 v_mov per tile
+    const int zb = opaque_zero();
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      acc2a[m] = bias_tile(B2 + 32 * m, h);
+      acc2b[m] = bias_tile(B2 + 32 * m + zb, h);
+    }
+#else
 #pragma unroll
     for (int m = 0; m < 4; ++m) acc2b[m] = acc2a[m] = bias_tile(B2 + 32 * m, h);
+#endif
 #pragma unroll 1
     for (int mt = 0; mt < kQH1 / 32; ++mt) {
       const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(W1 + (32 * mt + r) * kQS1 + 8 * h);
@@ -943,13 +996,7 @@ __device__ __forceinline__ void qnet_forward(const uint8_t* net, const float* ti
     const float* B2 = B2_ + z;
     const float* B3 = B3_ + z;
     // layer-1 B operand: X'[k = 8h + j][env 32 nt + r]
-    bf16x8 xb;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = 8 * h + j;
-      const int src = swap ? (k < 5 ? k + 5 : k - 5) : k;
-      xb[j] = static_cast<__bf16>(k < kObs ? tile[(row0 + 32 * nt + r) * kObs + src] : 0.f);
-    }
+    const bf16x8 xb = qnet_input(tile + (row0 + 32 * nt + r) * kObs, swap, h);
     f32x16 acc2[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) acc2[m] = bias_tile(B2 + 32 * m, h);
@@ -1094,6 +1141,16 @@ __global__ __launch_bounds__(kQBlock, 2) void qnet_rollout_kernel(const QRollout
       t2[k] = make_float2(static_cast<float>(r.o[2 * k]), static_cast<float>(r.o[2 * k + 1]));
   }
   __syncthreads();
+#if MG_QNET_PRIO
+  // the second-dispatched half loses VALU arbitration on every segment: raise it once
+  if ((tid >> 6) >= kQBlock / 128) __builtin_amdgcn_s_setprio(1);
+#endif
+#if MG_QNET_STAGGER
+  // waves 4-7 start late, so each SIMD pairs one wave's MFMA phase with its partner's
+  // fp64 env step instead of running both in lockstep
+  if ((tid >> 6) >= kQBlock / 128)
+    for (int k = 0; k < MG_QNET_STAGGER; ++k) __builtin_amdgcn_s_sleep(127);
+#endif
 
   bool won = false;
   for (int t = 0; t < R.num_steps; ++t) {
