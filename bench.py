@@ -243,7 +243,7 @@ def replay_leg(env, args, torch):
         ring.sample_rows(128, seed=args.seed, draw=j)
     e.record()
     torch.cuda.synchronize()
-    return {"kernels": "replay_scan_kernel + replay_write_kernel",
+    return {"kernels": "replay_scan_kernel + replay_group_scan_kernel + replay_write_kernel",
             "transitions_per_store": T * E, "stored_per_store": kept, "capacity": 1 << 24,
             "value": kept / (ms * 1e-3), "unit": "transitions/s", "ms_per_store": ms,
             "bytes_per_store": nbytes, "achieved": achieved,

@@ -249,9 +249,8 @@ int mg_rollout_qnet(const mg_params* params, const mg_state* state, const mg_tra
  * skip_ego_won != 0 (main.py:209 `if env.winner is not 1`; hdqn.py:316 stores every one), and
  * adds the number appended to *counter. When more than capacity transitions are appended only
  * the newest capacity are written, as sequential stores would leave them. scratch: a device
- * buffer of at least mg_replay_scratch_bytes(n, num_steps) bytes, 8-byte aligned and zero-filled
- * before its first use (every call leaves it ready for the next); one scratch buffer per
- * stream. Two launches, stream-ordered, no host synchronisation. */
+ * buffer of at least mg_replay_scratch_bytes(n, num_steps) bytes, 8-byte aligned, any contents;
+ * one scratch buffer per stream. Three launches, stream-ordered, no host synchronisation. */
 size_t mg_replay_scratch_bytes(int64_t n, int32_t num_steps);
 int mg_replay_store(float* rows, uint64_t* counter, int64_t capacity, const mg_transitions* tr,
                     int64_t n, int32_t num_steps, int32_t skip_ego_won, void* scratch,

@@ -1255,15 +1255,16 @@ __global__ __launch_bounds__(kBlock) void observe_kernel(const mg_params P, cons
 // ============================================================================ replay memory
 // The DQN replay memory (scripts/main.py:91-92 np.zeros((MEMORY_CAPACITY, 2*NUM_STATES+2)),
 // :115-119 store_transition, :130-135 the minibatch draw). A batch of T x n transitions is
-// appended in (t, i) order with two launches:
-//   replay_scan_kernel   one wave per 64 "write blocks" (t, 256-env slice): keep counts straight
-//                        from the won bits, a wave scan (in-group offsets), and the last wave
-//                        to finish (ticket + fences, nobody waits) scans the group totals into
-//                        ring positions and advances memory_counter;
-//   replay_write_kernel  one block per 256-env slice walking t = 0..T-1, the step's
-//                        observation kept in registers as the next transition's s (each obs row
-//                        is read once); rows gathered in LDS in ring order and written as
-//                        contiguous 8-byte stores (a row is 88 B: alignment alternates).
+// appended in (t, i) order with three launches (kernel boundaries publish the partial sums;
+// a last-arriver ticket with device-scope fences measured 8 % slower for the whole store):
+//   replay_scan_kernel        one wave per 64 "write blocks" (t, 256-env slice): keep counts
+//                             straight from the won bits, a wave scan (in-group offsets), the
+//                             group's total;
+//   replay_group_scan_kernel  one wave: group totals -> ring positions, memory_counter advanced;
+//   replay_write_kernel       one block per 256 envs x MG_REPLAY_TCHUNK steps, the step's
+//                             observation kept in registers as the next transition's s; rows
+//                             gathered in LDS in ring order and written as contiguous 8-byte
+//                             stores (a row is 88 B: 16-byte alignment alternates).
 constexpr int kRow = 2 * kObs + 2;  // 22 floats: s(10), a, r, s'(10)
 constexpr int kRBlock = 256;        // envs per write block
 constexpr int kRGroup = 64;         // write blocks per scan wave
@@ -1278,9 +1279,7 @@ struct ReplayIn {
   int32_t skip_won;
 };
 
-struct ReplayScratch {  // carved from the caller's scratch buffer
-  uint32_t* ticket;      // [1] at offset 0 whatever the sizes: zero between calls (the last
-                         //     wave resets it), so one buffer serves calls of any size
+struct ReplayScratch {  // carved from the caller's scratch buffer (8-byte header reserved)
   uint64_t* group_base;  // [ngroups] memory_counter before the group's first transition
   uint32_t* local;       // [nb] transitions of earlier write blocks of the same group
   uint32_t* group_total; // [ngroups]
@@ -1291,7 +1290,6 @@ __host__ __device__ inline int64_t replay_groups(int64_t nb) { return (nb + kRGr
 __host__ __device__ inline ReplayScratch replay_scratch(void* base, int64_t nb) {
   const int64_t ng = replay_groups(nb);
   ReplayScratch S;
-  S.ticket = static_cast<uint32_t*>(base);
   S.group_base = static_cast<uint64_t*>(base) + 1;
   S.local = reinterpret_cast<uint32_t*>(S.group_base + ng);
   S.group_total = S.local + nb;
@@ -1311,13 +1309,15 @@ __device__ __forceinline__ uint32_t replay_block_count(const ReplayIn& R, int t,
   const int64_t live = R.n - i0 < kRBlock ? R.n - i0 : kRBlock;
   if (!R.skip_won || R.X.won_mask == nullptr) return static_cast<uint32_t>(live);
   const uint64_t* w = R.X.won_mask + static_cast<int64_t>(t) * R.words + (i0 >> 6);
+  uint64_t wk[kRBlock / 64];
+#pragma unroll
+  for (int k = 0; k < kRBlock / 64; ++k) wk[k] = live > 64 * k ? w[k] : ~0ull;  // loads issued together
   uint32_t c = 0;
 #pragma unroll
   for (int k = 0; k < kRBlock / 64; ++k) {
     const int64_t v = live - 64 * k;  // live envs of this word
-    if (v <= 0) break;
-    const uint64_t m = v >= 64 ? ~0ull : ((1ull << v) - 1);
-    c += __popcll(~w[k] & m);
+    const uint64_t m = v >= 64 ? ~0ull : (v <= 0 ? 0ull : ((1ull << v) - 1));
+    c += __popcll(~wk[k] & m);
   }
   return c;
 }
@@ -1332,35 +1332,43 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   return v;
 }
 
-__global__ __launch_bounds__(64) void replay_scan_kernel(const ReplayIn R, ReplayScratch S,
-                                                         uint64_t* counter) {
+// One wave: group_base[g] = counter + sum(group_total[0..g)), then counter += sum.
+__device__ __forceinline__ void replay_group_scan(const ReplayScratch& S, int64_t ng, uint64_t* counter) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t c0 = *counter;
+  uint64_t carry = 0;
+  constexpr int kBatch = 16;  // loads issued together, then scanned: one memory wait per batch
+  for (int64_t g0 = 0; g0 < ng; g0 += 64 * kBatch) {
+    uint32_t v[kBatch];
+#pragma unroll
+    for (int b = 0; b < kBatch; ++b) {
+      const int64_t g = g0 + 64 * b + lane;
+      v[b] = g < ng ? __atomic_load_n(S.group_total + g, __ATOMIC_RELAXED) : 0u;
+    }
+#pragma unroll
+    for (int b = 0; b < kBatch; ++b) {
+      const int64_t g = g0 + 64 * b + lane;
+      const uint32_t gi = wave_incl_scan(v[b]);
+      if (g < ng) S.group_base[g] = c0 + carry + (gi - v[b]);
+      carry += __shfl(gi, 63);
+    }
+  }
+  if (lane == 0) *counter = c0 + carry;
+}
+
+__global__ __launch_bounds__(64) void replay_group_scan_kernel(const ReplayScratch S, int64_t ng,
+                                                               uint64_t* counter) {
+  replay_group_scan(S, ng, counter);
+}
+
+__global__ __launch_bounds__(64) void replay_scan_kernel(const ReplayIn R, ReplayScratch S) {
   const int lane = threadIdx.x;
-  const int64_t ng = replay_groups(R.nb);
   const int64_t b = static_cast<int64_t>(blockIdx.x) * kRGroup + lane;
   uint32_t c = 0;
   if (b < R.nb) c = replay_block_count(R, static_cast<int>(b / R.nbx), b % R.nbx);
   const uint32_t incl = wave_incl_scan(c);
   if (b < R.nb) S.local[b] = incl - c;
   if (lane == 63) S.group_total[blockIdx.x] = incl;
-  __threadfence();  // publish before taking a ticket
-  uint32_t ticket = 0;
-  if (lane == 0) ticket = atomicAdd(S.ticket, 1u);
-  ticket = __shfl(ticket, 0);
-  if (ticket != static_cast<uint32_t>(ng - 1)) return;  // not the last group to finish
-  __threadfence();  // acquire every group's total
-  const uint64_t c0 = *counter;
-  uint64_t carry = 0;
-  for (int64_t g0 = 0; g0 < ng; g0 += 64) {
-    const int64_t g = g0 + lane;
-    const uint32_t v = g < ng ? __atomic_load_n(S.group_total + g, __ATOMIC_RELAXED) : 0u;
-    const uint32_t gi = wave_incl_scan(v);
-    if (g < ng) S.group_base[g] = c0 + carry + (gi - v);
-    carry += __shfl(gi, 63);
-  }
-  if (lane == 0) {
-    *counter = c0 + carry;
-    *S.ticket = 0u;  // ready for the next call
-  }
 }
 
 // Rank of the calling thread among the block's kept threads, and the block total.
@@ -1796,7 +1804,8 @@ int mg_replay_store(float* rows, uint64_t* counter, int64_t capacity, const mg_t
   const ReplayScratch S = replay_scratch(scratch, nb);
   hipStream_t st = static_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(replay_scan_kernel, dim3(static_cast<unsigned>(replay_groups(nb))), dim3(64), 0, st,
-                     R, S, counter);
+                     R, S);
+  hipLaunchKernelGGL(replay_group_scan_kernel, dim3(1), dim3(64), 0, st, S, replay_groups(nb), counter);
   hipLaunchKernelGGL(replay_write_kernel, dim3(static_cast<unsigned>(nbx), chunks), dim3(kRBlock), 0, st, R,
                      S, counter, rows, capacity);
   return finish_launch("mg_replay_store");

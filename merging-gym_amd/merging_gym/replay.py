@@ -7,7 +7,7 @@ same structure in scripts/hdqn.py:157-158, :180-184, :194-199). Rows are
 torch.FloatTensor, so the values learn() sees are the same.
 
 Transitions go in straight from a MergeVecEnv's trajectory buffers (one batched store per
-rollout, two kernel launches from libmerging_hip.so) instead of one store_transition call
+rollout, three kernel launches from libmerging_hip.so) instead of one store_transition call
 per env step; the order is (step, env), i.e. what stepping env 0..N-1 and storing each in
 turn would give. The ring position lives on the device; reading `memory_counter`
 synchronises.
@@ -53,8 +53,8 @@ class ReplayRing:
 
     def _scratch_for(self, n, T):
         need = int(_native.lib.mg_replay_scratch_bytes(n, T))
-        if self._scratch.numel() * 8 < need:  # zero-filled: the kernels keep it that way
-            self._scratch = self._torch.zeros((need + 7) // 8, dtype=self._torch.int64, device=self.device)
+        if self._scratch.numel() * 8 < need:
+            self._scratch = self._torch.empty((need + 7) // 8, dtype=self._torch.int64, device=self.device)
         return self._scratch
 
     def _f32(self, t, shape):

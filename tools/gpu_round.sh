@@ -12,4 +12,5 @@ echo "== smoke" && timeout -k 10 400 python -c "import __graft_entry__ as g; g.s
 && echo "== pmc fetch" && timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o pmc -- python tools/profile_pmc.py > gpurun_out/pmc_fetch.log 2>&1 \
 && echo "== pmc write" && timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o pmc -- python tools/profile_pmc.py > gpurun_out/pmc_write.log 2>&1 \
 && echo "== bench 2^22" && timeout -k 10 300 python bench.py --envs 4194304 --steps 300 --no-cpu-baseline > gpurun_out/bench_4m.log 2>&1 && tail -1 gpurun_out/bench_4m.log | cut -c1-400 \
-&& echo "== 2-rank rehearsal (gloo, shared GPU)" && timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 100 --warmup 10 --envs 262144 --dist-backend gloo --rollout-launches 5 > gpurun_out/bench_2rank.log 2>&1 && tail -1 gpurun_out/bench_2rank.log | cut -c1-600
+&& echo "== 2-rank rehearsal (gloo, shared GPU)" && timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 100 --warmup 10 --envs 262144 --dist-backend gloo --rollout-launches 5 > gpurun_out/bench_2rank.log 2>&1 && tail -1 gpurun_out/bench_2rank.log | cut -c1-600 \
+&& echo "== pmc qnet" && bash tools/pmc_qnet.sh
