@@ -57,14 +57,20 @@ namespace {
 #ifndef MG_QNET_BIAS_RELOAD
 #define MG_QNET_BIAS_RELOAD 1  // Q-net: both column tiles load the layer-2 bias from LDS
 #endif
-#ifndef MG_QNET_PRIO
-#define MG_QNET_PRIO 0  // Q-net rollout: s_setprio 1 for waves 4-7
+#ifndef MG_QNET_SWP
+#define MG_QNET_SWP 1  // Q-net waves of the specialised kernel: software-pipelined hidden tiles
 #endif
-#ifndef MG_QNET_STAGGER
-#define MG_QNET_STAGGER 0  // Q-net rollout: waves 4-7 sleep STAGGER x 8128 cycles at the start
+#ifndef MG_QNET_WS
+#define MG_QNET_WS 1  // Q-net rollout: specialised waves (4 Q-net + 4 env) instead of uniform ones
 #endif
 #ifndef MG_QNET_PREFETCH
 #define MG_QNET_PREFETCH 3  // Q-net W2 fragments: 0 at use, 1/2 all up front, 3 one ahead
+#endif
+#ifndef MG_QNET_BLOCK
+#define MG_QNET_BLOCK 512  // Q-net rollout: threads per block (one LDS copy of the net each)
+#endif
+#ifndef MG_QNET_WAVES_PER_EU
+#define MG_QNET_WAVES_PER_EU 2  // Q-net rollout: waves per SIMD the register budget is cut for
 #endif
 #ifndef MG_QNET_PAIR
 #define MG_QNET_PAIR 1    // Q-net: both 32-env column tiles per hidden-tile iteration
@@ -308,12 +314,19 @@ struct StepOut {
   int bad;  // 1: action1 invalid, 2: action2 invalid (the reference's KeyError)
 };
 
+// opaque_key: a uniform key the compiler cannot hoist. In a multi-step loop the 20 round keys
+// are then scalar adds at each use instead of loop invariants spilled into VGPR lanes (one
+// v_readlane, a vector instruction, per round): -2 % per rollout step (A/B); the one-step
+// kernel is better without it.
 __device__ __forceinline__ void draw_actions(uint64_t gi, uint64_t step, uint64_t seed,
-                                             int opp_random, int& a1, int& a2) {
+                                             int opp_random, int& a1, int& a2,
+                                             bool opaque_key = false) {
+  uint32_t k0 = static_cast<uint32_t>(seed), k1 = static_cast<uint32_t>(seed >> 32);
+  if (opaque_key) asm volatile("" : "+s"(k0), "+s"(k1));
   const uint4 u = philox4x32_10(
       make_uint4(static_cast<uint32_t>(gi), static_cast<uint32_t>(gi >> 32),
                  static_cast<uint32_t>(step), static_cast<uint32_t>(step >> 32)),
-      static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32));
+      k0, k1);
   a1 = action_from_u32(u.x);
   a2 = opp_random ? action_from_u32(u.y) : MG_ACTION_NONE;
 }
@@ -691,7 +704,7 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(const Rollout R) {
     if (live) {
       int a1, a2;
       draw_actions(static_cast<uint64_t>(R.env_offset + i), R.first_step + t, R.seed, R.opp_random,
-                   a1, a2);
+                   a1, a2, /*opaque_key=*/true);
       env_step(P, e, a1, a2, r);  // Philox actions are always valid
 #if !MG_ABL_NO_BYTES
       if (R.T.a1) st_out(R.T.a1 + row, static_cast<int8_t>(a1));
@@ -753,7 +766,7 @@ constexpr int kQOffB1 = kQOffW3 + kQOut * kQS3 * 2;
 constexpr int kQOffB2 = kQOffB1 + kQH1 * 4;
 constexpr int kQOffB3 = kQOffB2 + kQH2 * 4;
 constexpr int kQNetBytes = kQOffB3 + kQOut * 4;                    // 80,384 B
-constexpr int kQBlock = 512;                                       // 8 waves share one LDS copy
+constexpr int kQBlock = MG_QNET_BLOCK;                             // waves sharing one LDS copy
 static_assert(kQOffW2 % 16 == 0 && kQOffW3 % 16 == 0 && kQOffB1 % 16 == 0 && kQOffB2 % 16 == 0 &&
                   kQOffB3 % 16 == 0 && kQNetBytes % 16 == 0,
               "packed Q-net sections must stay 16-byte aligned");
@@ -1047,6 +1060,119 @@ __device__ __forceinline__ void qnet_forward(const uint8_t* net, const float* ti
   }
 }
 
+// ReLU + bf16 pack of two accumulator values: one v_cvt_pk_bf16_f32 + one v_pk_max_i16.
+__device__ __forceinline__ uint32_t relu_pair(float x, float y) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  i16x2 v = __builtin_bit_cast(i16x2, __builtin_convertvector(f32x2{x, y}, bf16x2));
+  const i16x2 zero = {0, 0};
+  v = __builtin_elementwise_max(v, zero);
+  return __builtin_bit_cast(uint32_t, v);
+}
+
+// qnet_forward (pair mode) software-pipelined over the hidden tiles, for a wave that runs
+// only the Q-net (qnet_rollout_ws_kernel has the registers for it): layer 1 of hidden tile
+// mt + 1 is issued ahead of layer 2 of tile mt, and its ReLU is computed in pieces between
+// tile mt's layer-2 MFMAs, so the vector work runs while the matrix pipe is busy instead of
+// between dependent MFMAs.
+__device__ __forceinline__ void qnet_forward_swp(const uint8_t* net, const float* tile, int row0,
+                                                 bool swap, float (&q)[8]) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int z = opaque_zero();
+  const __bf16* W1 = reinterpret_cast<const __bf16*>(net) + z;
+  const __bf16* W2 = reinterpret_cast<const __bf16*>(net + kQOffW2) + z;
+  const __bf16* W3 = reinterpret_cast<const __bf16*>(net + kQOffW3) + z;
+  const float* B1 = reinterpret_cast<const float*>(net + kQOffB1) + z;
+  const float* B2 = reinterpret_cast<const float*>(net + kQOffB2) + z;
+  const float* B3 = reinterpret_cast<const float*>(net + kQOffB3) + z;
+  const bf16x8 xb0 = qnet_input(tile + (row0 + r) * kObs, swap, h);
+  const bf16x8 xb1 = qnet_input(tile + (row0 + 32 + r) * kObs, swap, h);
+  f32x16 acc2a[4], acc2b[4];
+  const int zb = opaque_zero();
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    acc2a[m] = bias_tile(B2 + 32 * m, h);
+    acc2b[m] = bias_tile(B2 + 32 * m + zb, h);
+  }
+  auto layer1 = [&](int mt, f32x16& c0, f32x16& c1) {
+    const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(W1 + (32 * mt + r) * kQS1 + 8 * h);
+    const f32x16 bt = bias_tile(B1 + 32 * mt, h);
+    c0 = mfma32(a1, xb0, bt);
+    c1 = mfma32(a1, xb1, bt);
+  };
+  // hb[f]: f = 0, 1 -> column tile 0 k-steps 0, 1; f = 2, 3 -> column tile 1
+  auto relu_all = [&](const f32x16& c0, const f32x16& c1, bf16x8 (&hb)[4]) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const f32x16& c = f < 2 ? c0 : c1;
+      const int b = 8 * (f & 1);
+      hb[f] = __builtin_bit_cast(bf16x8, u32x4{relu_pair(c[b], c[b + 1]), relu_pair(c[b + 2], c[b + 3]),
+                                               relu_pair(c[b + 4], c[b + 5]), relu_pair(c[b + 6], c[b + 7])});
+    }
+  };
+  f32x16 c0, c1;
+  bf16x8 hb[4];
+  layer1(0, c0, c1);
+  relu_all(c0, c1, hb);
+  auto w2frag = [&](int mt, int j) {
+    return *reinterpret_cast<const bf16x8*>(W2 + (32 * (j >> 1) + r) * kQS2 + 16 * (2 * mt + (j & 1)) + 8 * h);
+  };
+  // one hidden tile: its layer 2, with the next tile's layer 1 + ReLU folded in when `more`
+  // (a constant at both call sites: the last tile is peeled, so no branch per ReLU piece)
+  auto tile_step = [&](int mt, bool more) __attribute__((always_inline)) {
+    bf16x8 a2n = w2frag(mt, 0);
+    if (more) layer1(mt + 1, c0, c1);
+    uint32_t nx[16];  // next tile's packed ReLU pairs, built between this tile's MFMAs
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int m2 = j >> 1, sk = j & 1;
+      // one fragment ahead: the next load is in flight under this pair of MFMAs
+      const bf16x8 a2 = a2n;
+      if (j + 1 < 8) a2n = w2frag(mt, j + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      acc2a[m2] = mfma32(a2, hb[sk], acc2a[m2]);
+      acc2b[m2] = mfma32(a2, hb[2 + sk], acc2b[m2]);
+      if (more) {
+#pragma unroll
+        for (int pp = 2 * j; pp < 2 * j + 2; ++pp) {
+          const int f = pp >> 2, b = 8 * (f & 1) + 2 * (pp & 3);
+          const f32x16& c = f < 2 ? c0 : c1;
+          nx[pp] = relu_pair(c[b], c[b + 1]);
+        }
+      }
+    }
+    if (more) {
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+        hb[f] = __builtin_bit_cast(bf16x8, u32x4{nx[4 * f], nx[4 * f + 1], nx[4 * f + 2], nx[4 * f + 3]});
+    }
+  };
+#pragma unroll 1
+  for (int mt = 0; mt < kQH1 / 32 - 1; ++mt) tile_step(mt, true);
+  tile_step(kQH1 / 32 - 1, false);
+  f32x16 acc3_0 = bias_tile(B3, h), acc3_1 = bias_tile(B3 + zb, h);
+#pragma unroll
+  for (int m2 = 0; m2 < kQH2 / 32; ++m2) {
+    const bf16x8 ha[2] = {relu_bf16(acc2a[m2], 0), relu_bf16(acc2a[m2], 1)};
+    const bf16x8 hbb[2] = {relu_bf16(acc2b[m2], 0), relu_bf16(acc2b[m2], 1)};
+#pragma unroll
+    for (int sk = 0; sk < 2; ++sk) {
+      const bf16x8 a3 = *reinterpret_cast<const bf16x8*>(W3 + r * kQS3 + 16 * (2 * m2 + sk) + 8 * h);
+      acc3_0 = mfma32(a3, ha[sk], acc3_0);
+      acc3_1 = mfma32(a3, hbb[sk], acc3_1);
+    }
+  }
+  // rows 0-3 of the env of lane 32t + r sit in lane half 0 of tile t, rows 4-7 in half 1
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float own = h ? acc3_1[j] : acc3_0[j];
+    const float send = h ? acc3_0[j] : acc3_1[j];
+    const float got = __shfl_xor(send, 32);
+    q[j] = h ? got : own;
+    q[4 + j] = h ? own : got;
+  }
+}
+
 __device__ __forceinline__ int argmax_first(const float (&q)[8], int out_dim) {
   int best = 0;
   float v = q[0];
@@ -1097,60 +1223,92 @@ struct QRollout {
   uint32_t flags;
 };
 
-// T epsilon-greedy Q-net steps per launch. OPP: 0 = None (L0 opponent), 1 = uniform random,
-// 2 = the same net on the swapped observation (self-play, main.py:165-166 / :199).
-// Philox4x32-10 per (global env, step): u.x ego explore draw, u.y ego random action,
-// u.z opponent explore draw, u.w opponent random action.
+__device__ __forceinline__ void qnet_forward_ws(const uint8_t* net, const float* tile, int row0,
+                                                bool swap, float (&q)[8]) {
+#if MG_QNET_SWP
+  qnet_forward_swp(net, tile, row0, swap, q);
+#else
+  qnet_forward(net, tile, row0, swap, q);
+#endif
+}
+
+// One epsilon-greedy step of env i given the greedy actions (main.py:99-112): Philox4x32-10
+// per (global env, step): u.x ego explore draw, u.y ego random action, u.z opponent explore
+// draw, u.w opponent random action. Then the env step and its trajectory outputs.
 template <int OPP>
-__global__ __launch_bounds__(kQBlock, 2) void qnet_rollout_kernel(const QRollout R) {
+__device__ __forceinline__ void qnet_policy_step(const QRollout& R, Env& e, StepOut& r, int64_t i,
+                                                 int t, int greedy1, int greedy2, bool& won) {
+  const int64_t row = static_cast<int64_t>(t) * R.n + i;
+  const uint64_t gi = static_cast<uint64_t>(R.env_offset + i);
+  const uint64_t step = R.first_step + t;
+  const uint4 u = philox4x32_10(
+      make_uint4(static_cast<uint32_t>(gi), static_cast<uint32_t>(gi >> 32),
+                 static_cast<uint32_t>(step), static_cast<uint32_t>(step >> 32)),
+      static_cast<uint32_t>(R.seed), static_cast<uint32_t>(R.seed >> 32));
+  const int a1 = (static_cast<uint64_t>(u.x) < R.greedy_thr) ? greedy1 : action_from_u32(u.y);
+  int a2 = MG_ACTION_NONE;
+  if constexpr (OPP == 1) a2 = action_from_u32(u.w);
+  if constexpr (OPP == 2)
+    a2 = (static_cast<uint64_t>(u.z) < R.opp_greedy_thr) ? greedy2 : action_from_u32(u.w);
+  env_step(R.P, e, a1, a2, r);
+  if (R.T.a1) st_out(R.T.a1 + row, static_cast<int8_t>(a1));
+  if (R.T.a2) st_out(R.T.a2 + row, static_cast<int8_t>(a2));
+  if (R.T.rew)
+    st_out(reinterpret_cast<f32x2*>(R.T.rew) + row, f32x2{static_cast<float>(r.r1), static_cast<float>(r.r2)});
+  if (R.T.done) st_out(R.T.done + row, static_cast<uint8_t>(r.done ? 1 : 0));
+  if (R.T.coll) st_out(R.T.coll + row, static_cast<uint8_t>(r.coll ? 1 : 0));
+  won = e.winner == 1;
+  if ((R.flags & MG_AUTORESET) && r.done)
+    finish_episode(R.P, e, r, R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i);
+}
+
+// Observation of env i (or zeros past n) into its fp32 tile row; returns live.
+__device__ __forceinline__ bool qnet_load_env(const QRollout& R, int64_t i, Env& e, float* row) {
+  double o[kObs];
+  const bool live = i < R.n;
+  if (live) {
+    e = load_env(R.S, i);
+    double x1, y1, x2, y2;
+    lon2coord(R.P, e.p1, true, x1, y1);
+    lon2coord(R.P, e.p2, false, x2, y2);
+    observe(R.P, e.p1, e.v1, e.p2, e.v2, x1, y1, x2, y2, o);
+  } else {
+#pragma unroll
+    for (int k = 0; k < kObs; ++k) o[k] = 0.0;
+  }
+  float2* t2 = reinterpret_cast<float2*>(row);
+#pragma unroll
+  for (int k = 0; k < kObs / 2; ++k)
+    t2[k] = make_float2(static_cast<float>(o[2 * k]), static_cast<float>(o[2 * k + 1]));
+  return live;
+}
+
+// T epsilon-greedy Q-net steps per launch, every wave doing both jobs for its own 64 envs.
+// OPP: 0 = None (L0 opponent), 1 = uniform random, 2 = the same net on the swapped observation
+// (self-play, main.py:165-166 / :199).
+template <int OPP>
+__global__ __launch_bounds__(kQBlock, MG_QNET_WAVES_PER_EU) void qnet_rollout_kernel(const QRollout R) {
   __shared__ __attribute__((aligned(16))) uint8_t lds_net[kQNetBytes];
   __shared__ __attribute__((aligned(16))) float tile[kQBlock * kObs];
 
-  const mg_params& P = R.P;
   const int tid = threadIdx.x;
   const int64_t base = static_cast<int64_t>(blockIdx.x) * kQBlock;
   const int64_t i = base + tid;
-  const bool live = i < R.n;
-  const bool autoreset = (R.flags & MG_AUTORESET) != 0;
   const int row0 = (tid >> 6) * 64;
 
   qnet_to_lds(R.net, lds_net);
   Env e;
   StepOut r;
-  if (live) {
-    e = load_env(R.S, i);
-    double x1, y1, x2, y2;
-    lon2coord(P, e.p1, true, x1, y1);
-    lon2coord(P, e.p2, false, x2, y2);
-    observe(P, e.p1, e.v1, e.p2, e.v2, x1, y1, x2, y2, r.o);
-  } else {
-#pragma unroll
-    for (int k = 0; k < kObs; ++k) r.o[k] = 0.0;
-  }
+  const bool live = qnet_load_env(R, i, e, tile + tid * kObs);
   // this wave's 64 rows of the tile; waves never read each other's rows, so after the one
-  // barrier that publishes the weights they run unsynchronised (MFMA of one wave overlaps
-  // the fp64 env step of the other wave on its SIMD)
+  // barrier that publishes the weights they run unsynchronised
   float* wtile = tile + row0 * kObs;
   const int64_t wbase = base + row0;
   const int64_t wrem = R.n - wbase;
   const int wrows = wrem <= 0 ? 0 : (wrem < 64 ? static_cast<int>(wrem) : 64);
-  {
-    float2* t2 = reinterpret_cast<float2*>(wtile + (tid & 63) * kObs);
 #pragma unroll
-    for (int k = 0; k < kObs / 2; ++k)
-      t2[k] = make_float2(static_cast<float>(r.o[2 * k]), static_cast<float>(r.o[2 * k + 1]));
-  }
+  for (int k = 0; k < kObs; ++k) r.o[k] = 0.0;
   __syncthreads();
-#if MG_QNET_PRIO
-  // the second-dispatched half loses VALU arbitration on every segment: raise it once
-  if ((tid >> 6) >= kQBlock / 128) __builtin_amdgcn_s_setprio(1);
-#endif
-#if MG_QNET_STAGGER
-  // waves 4-7 start late, so each SIMD pairs one wave's MFMA phase with its partner's
-  // fp64 env step instead of running both in lockstep
-  if ((tid >> 6) >= kQBlock / 128)
-    for (int k = 0; k < MG_QNET_STAGGER; ++k) __builtin_amdgcn_s_sleep(127);
-#endif
 
   bool won = false;
   for (int t = 0; t < R.num_steps; ++t) {
@@ -1163,31 +1321,7 @@ __global__ __launch_bounds__(kQBlock, 2) void qnet_rollout_kernel(const QRollout
       greedy2 = argmax_first(q, R.out_dim);
     }
     wave_lds_sync();  // the wave is done reading its rows before they are overwritten
-    const int64_t row = static_cast<int64_t>(t) * R.n + i;
-    if (live) {
-      const uint64_t gi = static_cast<uint64_t>(R.env_offset + i);
-      const uint64_t step = R.first_step + t;
-      const uint4 u = philox4x32_10(
-          make_uint4(static_cast<uint32_t>(gi), static_cast<uint32_t>(gi >> 32),
-                     static_cast<uint32_t>(step), static_cast<uint32_t>(step >> 32)),
-          static_cast<uint32_t>(R.seed), static_cast<uint32_t>(R.seed >> 32));
-      const int a1 = (static_cast<uint64_t>(u.x) < R.greedy_thr) ? greedy1 : action_from_u32(u.y);
-      int a2 = MG_ACTION_NONE;
-      if constexpr (OPP == 1) a2 = action_from_u32(u.w);
-      if constexpr (OPP == 2)
-        a2 = (static_cast<uint64_t>(u.z) < R.opp_greedy_thr) ? greedy2 : action_from_u32(u.w);
-      env_step(P, e, a1, a2, r);
-      if (R.T.a1) st_out(R.T.a1 + row, static_cast<int8_t>(a1));
-      if (R.T.a2) st_out(R.T.a2 + row, static_cast<int8_t>(a2));
-      if (R.T.rew)
-        st_out(reinterpret_cast<f32x2*>(R.T.rew) + row,
-               f32x2{static_cast<float>(r.r1), static_cast<float>(r.r2)});
-      if (R.T.done) st_out(R.T.done + row, static_cast<uint8_t>(r.done ? 1 : 0));
-      if (R.T.coll) st_out(R.T.coll + row, static_cast<uint8_t>(r.coll ? 1 : 0));
-      won = e.winner == 1;
-      if (autoreset && r.done)
-        finish_episode(P, e, r, R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i);
-    }
+    if (live) qnet_policy_step<OPP>(R, e, r, i, t, greedy1, greedy2, won);
     store_won_mask(R.T.won_mask, won, t, R.n, wbase, wrows);
     // the new observations: this wave's tile rows (next step's network input) and the output
     wave_store_obs(wtile, r.o,
@@ -1195,6 +1329,87 @@ __global__ __launch_bounds__(kQBlock, 2) void qnet_rollout_kernel(const QRollout
                    wrows);
   }
   if (live) store_env(R.S, i, e);
+}
+
+// The same T steps with the waves specialised: waves 0-3 run only the Q-net (matrix cores +
+// ReLU), waves 4-7 only the fp64 env step, so each SIMD pairs a matrix-heavy wave with a
+// vector-heavy one (waves w and w + 4 share a SIMD). The block's 512 envs are two groups
+// of 256, pipelined over 2T + 1 barrier-separated phases:
+//   Q(A,0) | Q(B,0) + step(A,0) | Q(A,1) + step(B,0) | ... | step(B,T-1)
+// Greedy actions go to the env waves through LDS; the new observations come back through the
+// tile rows. Each env-wave lane holds the two envs (one per group) it steps.
+template <int OPP>
+__global__ __launch_bounds__(kQBlock, 2) void qnet_rollout_ws_kernel(const QRollout R) {
+  static_assert(kQBlock == 512, "8 waves: 4 Q-net waves + 4 env waves");
+  constexpr int kHalf = kQBlock / 2;
+  __shared__ __attribute__((aligned(16))) uint8_t lds_net[kQNetBytes];
+  __shared__ __attribute__((aligned(16))) float tile[kQBlock * kObs];
+  __shared__ uint8_t greedy[2][kQBlock];
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kQBlock;
+  const bool qwave = wave < 4;
+  const int ew = wave - 4;
+
+  qnet_to_lds(R.net, lds_net);
+  const int phases = 2 * R.num_steps + 1;
+  if (qwave) {
+    // Q-net waves: the barrier count matches the env waves' loop below, phase for phase
+    // (roles are whole waves, so s_barrier pairs up; the two loops keep each role's live
+    // registers apart -- in one loop the env state sat beside the accumulators and spilled)
+    __syncthreads();
+    for (int p = 0; p < phases; ++p) {
+      if (p < 2 * R.num_steps) {
+        const int row0 = (p & 1) * kHalf + wave * 64;
+        float q[8];
+        qnet_forward_ws(lds_net, tile, row0, false, q);
+        greedy[0][row0 + lane] = static_cast<uint8_t>(argmax_first(q, R.out_dim));
+        if constexpr (OPP == 2) {
+          qnet_forward_ws(lds_net, tile, row0, true, q);
+          greedy[1][row0 + lane] = static_cast<uint8_t>(argmax_first(q, R.out_dim));
+        }
+      }
+      __syncthreads();
+    }
+    return;
+  }
+  Env e0, e1;
+  StepOut r;
+  bool won0 = false, won1 = false;
+  const bool live0 = qnet_load_env(R, base + ew * 64 + lane, e0, tile + (ew * 64 + lane) * kObs);
+  const bool live1 =
+      qnet_load_env(R, base + kHalf + ew * 64 + lane, e1, tile + (kHalf + ew * 64 + lane) * kObs);
+#pragma unroll
+  for (int k = 0; k < kObs; ++k) r.o[k] = 0.0;
+  __syncthreads();
+  for (int p = 0; p < phases; ++p) {
+    if (p > 0) {
+      const int g = (p - 1) & 1, t = (p - 1) >> 1;
+      const int local0 = g * kHalf + ew * 64;
+      const int local = local0 + lane;
+      const int64_t i = base + local;
+      const int greedy1 = greedy[0][local];
+      const int greedy2 = OPP == 2 ? greedy[1][local] : 0;
+      bool won;
+      if (g == 0) {  // wave-uniform: the two envs stay in named registers
+        if (live0) qnet_policy_step<OPP>(R, e0, r, i, t, greedy1, greedy2, won0);
+        won = won0;
+      } else {
+        if (live1) qnet_policy_step<OPP>(R, e1, r, i, t, greedy1, greedy2, won1);
+        won = won1;
+      }
+      const int64_t wbase = base + local0;
+      const int64_t wrem = R.n - wbase;
+      const int wrows = wrem <= 0 ? 0 : (wrem < 64 ? static_cast<int>(wrem) : 64);
+      store_won_mask(R.T.won_mask, won, t, R.n, wbase, wrows);
+      wave_store_obs(tile + local0 * kObs, r.o,
+                     R.T.obs ? R.T.obs + (static_cast<int64_t>(t) * R.n + wbase) * kObs : nullptr,
+                     wrows);
+    }
+    __syncthreads();
+  }
+  if (live0) store_env(R.S, base + ew * 64 + lane, e0);
+  if (live1) store_env(R.S, base + kHalf + ew * 64 + lane, e1);
 }
 
 __global__ __launch_bounds__(kBlock) void reset_kernel(const mg_params P, const mg_state S,
@@ -1747,13 +1962,17 @@ int mg_rollout_qnet(const mg_params* params, const mg_state* state, const mg_tra
   hipStream_t st = static_cast<hipStream_t>(stream);
   hipEvent_t ev0 = g_ev_start, ev1 = g_ev_stop;
   g_ev_start = g_ev_stop = nullptr;
+#if MG_QNET_WS
+#define MG_QKERNEL qnet_rollout_ws_kernel
+#else
+#define MG_QKERNEL qnet_rollout_kernel
+#endif
 #define MG_LAUNCH_Q(OPPV)                                                                         \
   do {                                                                                            \
     if (ev0 || ev1)                                                                               \
-      hipExtLaunchKernelGGL(qnet_rollout_kernel<OPPV>, dim3(blocks), dim3(kQBlock), 0, st, ev0,  \
-                            ev1, 0, R);                                                           \
+      hipExtLaunchKernelGGL(MG_QKERNEL<OPPV>, dim3(blocks), dim3(kQBlock), 0, st, ev0, ev1, 0, R); \
     else                                                                                          \
-      hipLaunchKernelGGL(qnet_rollout_kernel<OPPV>, dim3(blocks), dim3(kQBlock), 0, st, R);      \
+      hipLaunchKernelGGL(MG_QKERNEL<OPPV>, dim3(blocks), dim3(kQBlock), 0, st, R);               \
   } while (0)
   if (opponent_mode == 0)
     MG_LAUNCH_Q(0);
@@ -1762,6 +1981,7 @@ int mg_rollout_qnet(const mg_params* params, const mg_state* state, const mg_tra
   else
     MG_LAUNCH_Q(2);
 #undef MG_LAUNCH_Q
+#undef MG_QKERNEL
   return finish_launch("mg_rollout_qnet");
 }
 
