@@ -60,6 +60,12 @@ namespace {
 #ifndef MG_QNET_SWP
 #define MG_QNET_SWP 1  // Q-net waves of the specialised kernel: software-pipelined hidden tiles
 #endif
+#ifndef MG_QNET_WS_ENV_WAVES
+// specialised kernel: env waves per block. 4 = 512-env blocks (shipped); 8 = 1024-env blocks,
+// 3 waves per SIMD, which needs a Q-net wave within 168 VGPRs -- measured 19 % slower with the
+// unpaired forward that fits
+#define MG_QNET_WS_ENV_WAVES 4
+#endif
 #ifndef MG_QNET_WS
 #define MG_QNET_WS 1  // Q-net rollout: specialised waves (4 Q-net + 4 env) instead of uniform ones
 #endif
@@ -767,6 +773,11 @@ constexpr int kQOffB2 = kQOffB1 + kQH1 * 4;
 constexpr int kQOffB3 = kQOffB2 + kQH2 * 4;
 constexpr int kQNetBytes = kQOffB3 + kQOut * 4;                    // 80,384 B
 constexpr int kQBlock = MG_QNET_BLOCK;                             // waves sharing one LDS copy
+// specialised kernel: 4 Q-net waves + MG_QNET_WS_ENV_WAVES env waves; each env lane steps one
+// env per phase, so a group is 64 x env waves envs and a block holds two groups
+constexpr int kQWsThreads = 64 * (4 + MG_QNET_WS_ENV_WAVES);
+constexpr int kQWsWavesPerSimd = (4 + MG_QNET_WS_ENV_WAVES) / 4;
+constexpr int kQWsEnvs = 2 * 64 * MG_QNET_WS_ENV_WAVES;
 static_assert(kQOffW2 % 16 == 0 && kQOffW3 % 16 == 0 && kQOffB1 % 16 == 0 && kQOffB2 % 16 == 0 &&
                   kQOffB3 % 16 == 0 && kQNetBytes % 16 == 0,
               "packed Q-net sections must stay 16-byte aligned");
@@ -1339,15 +1350,17 @@ __global__ __launch_bounds__(kQBlock, MG_QNET_WAVES_PER_EU) void qnet_rollout_ke
 // Greedy actions go to the env waves through LDS; the new observations come back through the
 // tile rows. Each env-wave lane holds the two envs (one per group) it steps.
 template <int OPP>
-__global__ __launch_bounds__(kQBlock, 2) void qnet_rollout_ws_kernel(const QRollout R) {
-  static_assert(kQBlock == 512, "8 waves: 4 Q-net waves + 4 env waves");
-  constexpr int kHalf = kQBlock / 2;
+__global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws_kernel(const QRollout R) {
+  constexpr int kHalf = kQWsEnvs / 2;   // envs per group
+  constexpr int kTiles = kHalf / 256;   // 64-env tiles each Q-net wave computes per phase
+  constexpr int kEnvWaves = MG_QNET_WS_ENV_WAVES;
+  static_assert(kTiles >= 1 && kHalf == 64 * kEnvWaves, "group = 4 Q-net waves x kTiles x 64 envs");
   __shared__ __attribute__((aligned(16))) uint8_t lds_net[kQNetBytes];
-  __shared__ __attribute__((aligned(16))) float tile[kQBlock * kObs];
-  __shared__ uint8_t greedy[2][kQBlock];
+  __shared__ __attribute__((aligned(16))) float tile[kQWsEnvs * kObs];
+  __shared__ uint8_t greedy[2][kQWsEnvs];
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int64_t base = static_cast<int64_t>(blockIdx.x) * kQBlock;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kQWsEnvs;
   const bool qwave = wave < 4;
   const int ew = wave - 4;
 
@@ -1360,25 +1373,29 @@ __global__ __launch_bounds__(kQBlock, 2) void qnet_rollout_ws_kernel(const QRoll
     __syncthreads();
     for (int p = 0; p < phases; ++p) {
       if (p < 2 * R.num_steps) {
-        const int row0 = (p & 1) * kHalf + wave * 64;
-        float q[8];
-        qnet_forward_ws(lds_net, tile, row0, false, q);
-        greedy[0][row0 + lane] = static_cast<uint8_t>(argmax_first(q, R.out_dim));
-        if constexpr (OPP == 2) {
-          qnet_forward_ws(lds_net, tile, row0, true, q);
-          greedy[1][row0 + lane] = static_cast<uint8_t>(argmax_first(q, R.out_dim));
+#pragma unroll 1
+        for (int tt = 0; tt < kTiles; ++tt) {
+          const int row0 = (p & 1) * kHalf + (4 * tt + wave) * 64;
+          float q[8];
+          qnet_forward_ws(lds_net, tile, row0, false, q);
+          greedy[0][row0 + lane] = static_cast<uint8_t>(argmax_first(q, R.out_dim));
+          if constexpr (OPP == 2) {
+            qnet_forward_ws(lds_net, tile, row0, true, q);
+            greedy[1][row0 + lane] = static_cast<uint8_t>(argmax_first(q, R.out_dim));
+          }
         }
       }
       __syncthreads();
     }
     return;
   }
+  // env lane: env ew * 64 + lane of group 0 (e0) and of group 1 (e1)
+  const int local_a = ew * 64 + lane, local_b = kHalf + ew * 64 + lane;
   Env e0, e1;
   StepOut r;
   bool won0 = false, won1 = false;
-  const bool live0 = qnet_load_env(R, base + ew * 64 + lane, e0, tile + (ew * 64 + lane) * kObs);
-  const bool live1 =
-      qnet_load_env(R, base + kHalf + ew * 64 + lane, e1, tile + (kHalf + ew * 64 + lane) * kObs);
+  const bool live0 = qnet_load_env(R, base + local_a, e0, tile + local_a * kObs);
+  const bool live1 = qnet_load_env(R, base + local_b, e1, tile + local_b * kObs);
 #pragma unroll
   for (int k = 0; k < kObs; ++k) r.o[k] = 0.0;
   __syncthreads();
@@ -1390,7 +1407,10 @@ __global__ __launch_bounds__(kQBlock, 2) void qnet_rollout_ws_kernel(const QRoll
       const int64_t i = base + local;
       const int greedy1 = greedy[0][local];
       const int greedy2 = OPP == 2 ? greedy[1][local] : 0;
-      bool won;
+      bool won = false;
+#if MG_ABL_WS_NOENV  // timing ablation only: the env waves skip the step
+      if (greedy1 + greedy2 == 1000) R.T.done[0] = 0;
+#else
       if (g == 0) {  // wave-uniform: the two envs stay in named registers
         if (live0) qnet_policy_step<OPP>(R, e0, r, i, t, greedy1, greedy2, won0);
         won = won0;
@@ -1398,6 +1418,7 @@ __global__ __launch_bounds__(kQBlock, 2) void qnet_rollout_ws_kernel(const QRoll
         if (live1) qnet_policy_step<OPP>(R, e1, r, i, t, greedy1, greedy2, won1);
         won = won1;
       }
+#endif
       const int64_t wbase = base + local0;
       const int64_t wrem = R.n - wbase;
       const int wrows = wrem <= 0 ? 0 : (wrem < 64 ? static_cast<int>(wrem) : 64);
@@ -1408,8 +1429,8 @@ __global__ __launch_bounds__(kQBlock, 2) void qnet_rollout_ws_kernel(const QRoll
     }
     __syncthreads();
   }
-  if (live0) store_env(R.S, base + ew * 64 + lane, e0);
-  if (live1) store_env(R.S, base + kHalf + ew * 64 + lane, e1);
+  if (live0) store_env(R.S, base + local_a, e0);
+  if (live1) store_env(R.S, base + local_b, e1);
 }
 
 __global__ __launch_bounds__(kBlock) void reset_kernel(const mg_params P, const mg_state S,
@@ -1958,21 +1979,24 @@ int mg_rollout_qnet(const mg_params* params, const mg_state* state, const mg_tra
   R.num_steps = num_steps;
   R.out_dim = out_dim;
   R.flags = flags;
-  const unsigned blocks = static_cast<unsigned>((n + kQBlock - 1) / kQBlock);
+  unsigned blocks = static_cast<unsigned>((n + kQBlock - 1) / kQBlock);
   hipStream_t st = static_cast<hipStream_t>(stream);
   hipEvent_t ev0 = g_ev_start, ev1 = g_ev_stop;
   g_ev_start = g_ev_stop = nullptr;
 #if MG_QNET_WS
 #define MG_QKERNEL qnet_rollout_ws_kernel
+  const unsigned threads = kQWsThreads;
+  blocks = static_cast<unsigned>((n + kQWsEnvs - 1) / kQWsEnvs);
 #else
 #define MG_QKERNEL qnet_rollout_kernel
+  const unsigned threads = kQBlock;
 #endif
 #define MG_LAUNCH_Q(OPPV)                                                                         \
   do {                                                                                            \
     if (ev0 || ev1)                                                                               \
-      hipExtLaunchKernelGGL(MG_QKERNEL<OPPV>, dim3(blocks), dim3(kQBlock), 0, st, ev0, ev1, 0, R); \
+      hipExtLaunchKernelGGL(MG_QKERNEL<OPPV>, dim3(blocks), dim3(threads), 0, st, ev0, ev1, 0, R); \
     else                                                                                          \
-      hipLaunchKernelGGL(MG_QKERNEL<OPPV>, dim3(blocks), dim3(kQBlock), 0, st, R);               \
+      hipLaunchKernelGGL(MG_QKERNEL<OPPV>, dim3(blocks), dim3(threads), 0, st, R);               \
   } while (0)
   if (opponent_mode == 0)
     MG_LAUNCH_Q(0);
