@@ -320,7 +320,7 @@ int32_t oracle_step_batch(oracle_env* envs, int64_t n, const int8_t* a1, const i
 
 /* `steps` autoreset steps with Philox actions: the CPU baseline of the bench workload. */
 int64_t oracle_rollout_random(oracle_env* envs, int64_t n, int64_t steps, uint64_t seed,
-                              uint64_t first_step, int32_t opp_random, int32_t env_offset,
+                              uint64_t first_step, int32_t opp_random, int64_t env_offset,
                               double* ret_sum, uint32_t* counts) {
 #pragma omp parallel for schedule(static)
   for (int64_t i = 0; i < n; ++i) {

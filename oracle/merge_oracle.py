@@ -239,8 +239,8 @@ class COracle:
                                               ctypes.c_uint64, ctypes.c_int32, P(ctypes.c_int8),
                                               P(ctypes.c_int8)]
         lib.oracle_rollout_random.argtypes = [
-            ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint64,
-            ctypes.c_int32, ctypes.c_int32, P(ctypes.c_double), P(ctypes.c_uint32)]
+            ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_uint64,
+            ctypes.c_uint64, ctypes.c_int32, ctypes.c_int64, P(ctypes.c_double), P(ctypes.c_uint32)]
         lib.oracle_rollout_random.restype = ctypes.c_int64
         lib.oracle_philox_batch.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint64,
                                             P(ctypes.c_uint32)]

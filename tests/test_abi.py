@@ -89,6 +89,29 @@ def test_argument_errors_without_gpu():
     assert _native.lib.mg_replay_scratch_bytes(0, 4) == 0
 
 
+def test_empty_batches_are_no_ops_without_gpu():
+    """n == 0 (or num_steps == 0) returns success before any launch, for every entry point."""
+    from merging_gym import _native
+
+    lib, P = _native.lib, ctypes.byref(_native.default_params())
+    fake = ctypes.c_void_p(1 << 20)  # never dereferenced
+    st = _native.State(*([fake] * 7))
+    out = ctypes.byref(_native.Outputs())
+    traj = ctypes.byref(_native.Traj())
+    assert lib.mg_step(P, ctypes.byref(st), fake, None, out, None, 0, 0, None) == 0
+    assert lib.mg_step_random(P, ctypes.byref(st), None, None, out, None, 0, 0, 1, 0, 1, 0, None) == 0
+    assert lib.mg_rollout_random(P, ctypes.byref(st), traj, None, 0, 0, 1, 0, 16, 1, 0, None) == 0
+    assert lib.mg_rollout_random(P, ctypes.byref(st), traj, None, 64, 0, 1, 0, 0, 1, 0, None) == 0
+    assert lib.mg_rollout_qnet(P, ctypes.byref(st), traj, None, 0, 0, 1, 0, 16, fake, 5, 0, 0, 0, 0,
+                               None) == 0
+    assert lib.mg_reset(P, ctypes.byref(st), None, out, 0, None) == 0
+    assert lib.mg_observe(P, ctypes.byref(st), out, 0, None) == 0
+    assert lib.mg_qnet_forward(fake, fake, 0, fake, 0, None) == 0
+    tr = _native.Transitions(fake, fake, None, fake, fake, None, None)
+    assert lib.mg_replay_store(fake, fake, 16, ctypes.byref(tr), 0, 4, 1, None, 0, None) == 0
+    assert lib.mg_replay_sample(fake, fake, 16, 0, 0, 0, fake, None, 0, None) == 0
+
+
 def test_timeout_step_is_2501():
     """time_stamp += 0.2 in fp64 first exceeds 500 at step 2501 (merging_env.py:141-143)."""
     t, k = 0.0, 0

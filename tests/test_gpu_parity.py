@@ -287,3 +287,37 @@ def test_rollout_equals_step_sequence(torch, n, T):
     for name in ("p1", "v1", "p2", "v2", "ret1", "ret2", "tf", "ret_sum", "counts"):
         assert torch.equal(getattr(a, name), getattr(b, name)), name
     assert b._step_idx == 180 + T
+
+
+def test_config4_size_and_64bit_env_index(torch, coracle):
+    """Config 4's global batch (2^23 envs) stepped on one GPU: step-count bookkeeping over the
+    whole batch and oracle replays at both ends of the index range; then a small shard whose
+    global env indices exceed 2^32 (Philox counter high word) against the oracle."""
+    from merging_gym import MergeVecEnv
+
+    n, steps, seed = 1 << 23, 96, 4040
+    env = MergeVecEnv(n, device="cuda:0", final_observation=False)
+    for k in range(steps):
+        env.step_random(seed, step_idx=k, record_actions=False)
+    counts = env.counts.cpu().numpy().astype(np.int64)
+    np.testing.assert_array_equal(counts[:, 3] + env.steps.cpu().numpy(), steps)
+    idx = np.array([0, 1, 63, 64, 1 << 22, n - 65, n - 2, n - 1])
+    p1, r2 = env.p1.cpu().numpy()[idx], env.ret2.cpu().numpy()[idx]
+    del env
+    for j, gi in enumerate(idx):
+        e = coracle.new_envs(1)
+        coracle.reset(e)
+        coracle.rollout_random(e, steps, seed, 0, True, env_offset=int(gi))
+        assert abs(e["pos1"][0] - p1[j]) <= 1e-9 and abs(e["r2_acc"][0] - r2[j]) <= 1e-9, gi
+
+    off = (1 << 33) + 5
+    small = MergeVecEnv(300, device="cuda:0", env_offset=off)
+    for k in range(40):
+        small.step_random(seed, step_idx=k)
+    a1, a2 = coracle.random_actions(300, off, seed, 39, True)
+    np.testing.assert_array_equal(small.a1_buf.cpu().numpy(), a1)
+    np.testing.assert_array_equal(small.a2_buf.cpu().numpy(), a2)
+    e = coracle.new_envs(300)
+    coracle.reset(e)
+    coracle.rollout_random(e, 40, seed, 0, True, env_offset=off)
+    np.testing.assert_allclose(small.p2.cpu().numpy(), e["pos2"], rtol=0, atol=1e-9)
