@@ -45,6 +45,9 @@ namespace {
 #ifndef MG_BLOCK
 #define MG_BLOCK 256
 #endif
+#ifndef MG_REPLAY_WIDE_STORES
+#define MG_REPLAY_WIDE_STORES 1  // replay store: 16-byte stores over each contiguous run of rows
+#endif
 #ifndef MG_REPLAY_TCHUNK
 #define MG_REPLAY_TCHUNK 2  // replay store: steps one block walks (obs carried in registers)
 #endif
@@ -1689,7 +1692,33 @@ __global__ __launch_bounds__(kRBlock) void replay_write_kernel(const ReplayIn R,
       __syncthreads();
       const int skip = base >= first ? 0 : static_cast<int>(min<uint64_t>(first - base, total));
       const uint64_t slot0 = (base + skip) % static_cast<uint64_t>(cap);
-      const int nel = (total - skip) * (kRow / 2);
+      const int cnt = total - skip;  // <= cap: at most one wrap
+#if MG_REPLAY_WIDE_STORES
+      // the kept rows are one contiguous byte run of the ring (two at a wrap): an 8-byte head
+      // when the run starts off 16-byte alignment, then 16-byte stores, then an 8-byte tail
+      const int n_a = static_cast<int>(min<uint64_t>(static_cast<uint64_t>(cnt), static_cast<uint64_t>(cap) - slot0));
+#pragma unroll
+      for (int run = 0; run < 2; ++run) {
+        const int r0 = run == 0 ? 0 : n_a, nr = run == 0 ? n_a : cnt - n_a;
+        if (nr <= 0) continue;  // uniform
+        float* d = rows + (run == 0 ? slot0 : 0) * kRow;
+        const float* sp = tile + (skip + r0) * kRow;
+        const int nf = nr * kRow;
+        const int hd = (reinterpret_cast<uintptr_t>(d) & 15) ? 2 : 0;
+        const int nb = (nf - hd) >> 2;
+        const int tl = nf - hd - 4 * nb;  // 0 or 2
+        if (threadIdx.x == 0 && hd) st_out(reinterpret_cast<f32x2*>(d), *reinterpret_cast<const f32x2*>(sp));
+        if (threadIdx.x == 1 && tl)
+          st_out(reinterpret_cast<f32x2*>(d + nf - 2), *reinterpret_cast<const f32x2*>(sp + nf - 2));
+        const f32x2* s2 = reinterpret_cast<const f32x2*>(sp + hd);  // 8-byte aligned in LDS
+        f32x4* d4 = reinterpret_cast<f32x4*>(d + hd);
+        for (int k = threadIdx.x; k < nb; k += kRBlock) {
+          const f32x2 lo = s2[2 * k], hi = s2[2 * k + 1];
+          st_out(d4 + k, f32x4{lo[0], lo[1], hi[0], hi[1]});
+        }
+      }
+#else
+      const int nel = cnt * (kRow / 2);
       const f32x2* src = reinterpret_cast<const f32x2*>(tile + skip * kRow);
       for (int e2 = threadIdx.x; e2 < nel; e2 += kRBlock) {
         const int rr = e2 / (kRow / 2), part = e2 - rr * (kRow / 2);
@@ -1697,6 +1726,7 @@ __global__ __launch_bounds__(kRBlock) void replay_write_kernel(const ReplayIn R,
         if (slot >= static_cast<uint64_t>(cap)) slot %= static_cast<uint64_t>(cap);
         st_out(reinterpret_cast<f32x2*>(rows + slot * kRow) + part, src[e2]);
       }
+#endif
     }
     __syncthreads();  // tile and wave counts are reused by the next step
 #pragma unroll
