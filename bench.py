@@ -254,7 +254,8 @@ def replay_leg(env, args, torch):
 def dropin_leg(seed: int):
     """BASELINE config 1: merging_gym.make('merging-v0') single env, 500 step() calls with
     uniform random actions for both players, reset on done. The GPU-backed drop-in (one
-    launch + one 168-byte copy back per step) is timed next to the pure-Python restatement of
+    launch + one stream sync per step: the kernel reads the actions from and writes its
+    168-byte record to pinned host memory) is timed next to the pure-Python restatement of
     the reference's step (oracle.PyMergeEnv, numpy sin/cos + the QP solved per car-step) on
     the same action sequence; the reference itself measured 5,090 steps/s in the survey
     container."""

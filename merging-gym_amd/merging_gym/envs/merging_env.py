@@ -61,7 +61,7 @@ except Exception:  # noqa: BLE001
 class MergeEnv(_EnvBase):
     """GPU-backed single MergeEnv with the reference's list API."""
 
-    def __init__(self, device=None):
+    def __init__(self, device=None, zero_copy: bool = True):
         super().__init__()
         import torch
 
@@ -100,6 +100,16 @@ class MergeEnv(_EnvBase):
         self._stats = _native.Stats(None, None)
         self._a1 = ctypes.c_void_p(self._a_dev.data_ptr())
         self._a2 = ctypes.c_void_p(self._a_dev.data_ptr() + 1)
+        # zero_copy: the kernel reads the two actions from, and writes its 168-byte record to,
+        # pinned host memory (device-addressable on ROCm) -- one launch and one stream sync
+        # per step instead of two copies around the launch
+        self._zero_copy = bool(zero_copy)
+        if self._zero_copy:
+            self._a1 = ctypes.c_void_p(self._a_host.data_ptr())
+            self._a2 = ctypes.c_void_p(self._a_host.data_ptr() + 1)
+            self._out_zc = _native.Outputs(None, None, None, None, None, None,
+                                           ctypes.c_void_p(self._rec_host.data_ptr()),
+                                           ctypes.c_void_p(self._err.data_ptr()))
 
         self._time, self._steps, self._dirty = 0, 0, False
         self.reset()
@@ -211,15 +221,28 @@ class MergeEnv(_EnvBase):
         c1 = _ACTION_CODE.get(action1, nat.ACTION_INVALID)
         c2 = nat.ACTION_NONE if action2 is None else _ACTION_CODE.get(action2, nat.ACTION_INVALID)
         self._time += dT
-        self._a_host[0], self._a_host[1] = c1, c2
-        self._a_dev.copy_(self._a_host, non_blocking=True)
+        stream = self._stream()
+        if self._zero_copy:
+            stream.synchronize()  # the previous launch has read the host action bytes
+            a = self._a_host.numpy()
+            a[0], a[1] = c1, c2
+            out = self._out_zc
+        else:
+            self._a_host[0], self._a_host[1] = c1, c2
+            self._a_dev.copy_(self._a_host, non_blocking=True)
+            out = self._out
         nat.check(nat.lib.mg_step(ctypes.byref(self.params), ctypes.byref(self._state), self._a1,
-                                  self._a2, ctypes.byref(self._out), ctypes.byref(self._stats), 1, 0,
-                                  ctypes.c_void_p(self._stream().cuda_stream)), "mg_step")
+                                  self._a2, ctypes.byref(out), ctypes.byref(self._stats), 1, 0,
+                                  ctypes.c_void_p(stream.cuda_stream)), "mg_step")
         if c1 == nat.ACTION_INVALID or c2 == nat.ACTION_INVALID:
             self._sync_after_error()
             raise KeyError(action1 if c1 == nat.ACTION_INVALID else action2)
-        obs, rewards, done, info = self._apply(self._fetch())
+        if self._zero_copy:
+            stream.synchronize()
+            rec = self._rec_host.numpy().view(self._nat.REC64_DTYPE)[0]
+        else:
+            rec = self._fetch()
+        obs, rewards, done, info = self._apply(rec)
         return obs, rewards, done, info
 
     def _sync_after_error(self):
