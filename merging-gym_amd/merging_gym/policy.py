@@ -8,7 +8,6 @@ and epsilon-greedy choose_action (main.py:99-112), packed for the fused bf16 MFM
 
 from __future__ import annotations
 
-import ctypes
 import math
 
 EPISILO = 0.7  # main.py:16, hdqn.py:20 -- greedy when np.random.randn() <= EPISILO

@@ -25,7 +25,6 @@ through the reference's call sites ("Oracle").
 from __future__ import annotations
 
 import ctypes
-import math
 import os
 import subprocess
 

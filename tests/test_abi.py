@@ -5,8 +5,6 @@ import glob
 import os
 import re
 
-import pytest
-
 from conftest import ROOT
 
 

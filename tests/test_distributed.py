@@ -2,8 +2,6 @@
 
 import os
 
-import numpy as np
-import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp

@@ -11,7 +11,6 @@ import ctypes
 import numpy as np
 import pytest
 
-import merge_oracle as mo
 
 pytestmark = pytest.mark.gpu
 

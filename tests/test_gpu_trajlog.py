@@ -15,7 +15,6 @@ import os
 import numpy as np
 import pytest
 
-from conftest import ROOT
 from test_trajlog import CSV_DIR, assert_csv_equivalent
 
 pytestmark = pytest.mark.gpu

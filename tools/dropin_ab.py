@@ -1,8 +1,14 @@
-import sys, time
-sys.path.insert(0, "merging-gym_amd")
-import numpy as np
-import torch
-from merging_gym.envs.merging_env import MergeEnv
+"""Drop-in single env (config 1): per-step latency with device copies vs zero-copy pinned host
+memory, and that both give identical outputs.   python tools/dropin_ab.py   (on an MI355X)"""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "merging-gym_amd"))
+
+import numpy as np  # noqa: E402
+
+from merging_gym.envs.merging_env import MergeEnv  # noqa: E402
 rng = np.random.default_rng(0)
 acts = rng.integers(0, 5, (3000, 2)).tolist()
 res = {}
