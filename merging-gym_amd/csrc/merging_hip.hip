@@ -57,9 +57,6 @@ namespace {
 #ifndef MG_SINCOS_COLD
 #define MG_SINCOS_COLD 1  // the |t| >= 1/16 sincos fallback as an out-of-line call
 #endif
-#ifndef MG_QNET_BIAS_RELOAD
-#define MG_QNET_BIAS_RELOAD 1  // Q-net: both column tiles load the layer-2 bias from LDS
-#endif
 #ifndef MG_QNET_SWP
 #define MG_QNET_SWP 1  // Q-net waves of the specialised kernel: software-pipelined hidden tiles
 #endif
@@ -72,17 +69,11 @@ namespace {
 #ifndef MG_QNET_WS
 #define MG_QNET_WS 1  // Q-net rollout: specialised waves (4 Q-net + 4 env) instead of uniform ones
 #endif
-#ifndef MG_QNET_PREFETCH
-#define MG_QNET_PREFETCH 3  // Q-net W2 fragments: 0 at use, 1/2 all up front, 3 one ahead
-#endif
 #ifndef MG_QNET_BLOCK
 #define MG_QNET_BLOCK 512  // Q-net rollout: threads per block (one LDS copy of the net each)
 #endif
 #ifndef MG_QNET_WAVES_PER_EU
 #define MG_QNET_WAVES_PER_EU 2  // Q-net rollout: waves per SIMD the register budget is cut for
-#endif
-#ifndef MG_QNET_PAIR
-#define MG_QNET_PAIR 1    // Q-net: both 32-env column tiles per hidden-tile iteration
 #endif
 
 constexpr int kBlock = MG_BLOCK;  // 4 waves of 64 by default
@@ -923,9 +914,9 @@ __device__ __forceinline__ void qnet_forward(const uint8_t* net, const float* ti
   const float* B3_ = reinterpret_cast<const float*>(net + kQOffB3);
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
 
-#if MG_QNET_PAIR
   // Both N-tiles in the same hidden-tile iteration: two independent MFMA -> VALU -> MFMA
-  // chains per wave and one W2 fragment load per pair of MFMAs.
+  // chains per wave and one W2 fragment load per pair of MFMAs (one N-tile at a time, with 4
+  // accumulators instead of 8, measured 7-12 % slower).
   f32x16 acc3_0, acc3_1;
   {
     const int z = opaque_zero();
@@ -938,7 +929,6 @@ __device__ __forceinline__ void qnet_forward(const uint8_t* net, const float* ti
     const bf16x8 xb0 = qnet_input(tile + (row0 + r) * kObs, swap, h);
     const bf16x8 xb1 = qnet_input(tile + (row0 + 32 + r) * kObs, swap, h);
     f32x16 acc2a[4], acc2b[4];
-#if MG_QNET_BIAS_RELOAD
     // each accumulator loads its bias from LDS itself: sharing one load costs 16 v_mov per tile
     const int zb = opaque_zero();
 #pragma unroll
@@ -946,10 +936,6 @@ __device__ __forceinline__ void qnet_forward(const uint8_t* net, const float* ti
       acc2a[m] = bias_tile(B2 + 32 * m, h);
       acc2b[m] = bias_tile(B2 + 32 * m + zb, h);
     }
-#else
-#pragma unroll
-    for (int m = 0; m < 4; ++m) acc2b[m] = acc2a[m] = bias_tile(B2 + 32 * m, h);
-#endif
 #pragma unroll 1
     for (int mt = 0; mt < kQH1 / 32; ++mt) {
       const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(W1 + (32 * mt + r) * kQS1 + 8 * h);
@@ -958,20 +944,7 @@ __device__ __forceinline__ void qnet_forward(const uint8_t* net, const float* ti
         return *reinterpret_cast<const bf16x8*>(W2 + (32 * m2 + r) * kQS2 + 16 * (2 * mt + sk) +
                                                 8 * h);
       };
-#if MG_QNET_PREFETCH == 1 || MG_QNET_PREFETCH == 2
-      // all eight W2 fragments of this hidden tile in flight before the layer-1 MFMAs, so
-      // their LDS latency hides under layer 1 and the ReLU instead of stalling each MFMA
-      bf16x8 a2f[kQH2 / 32][2];
-#pragma unroll
-      for (int m2 = 0; m2 < kQH2 / 32; ++m2)
-#pragma unroll
-        for (int sk = 0; sk < 2; ++sk) a2f[m2][sk] = w2frag(m2, sk);
-#if MG_QNET_PREFETCH == 2
-      __builtin_amdgcn_sched_barrier(0);  // keep the scheduler from sinking them to their uses
-#endif
-#elif MG_QNET_PREFETCH == 3
       bf16x8 a2cur = w2frag(0, 0);
-#endif
       const f32x16 c0 = mfma32(a1, xb0, bt);
       const f32x16 c1 = mfma32(a1, xb1, bt);
       const bf16x8 ha[2] = {relu_bf16(c0, 0), relu_bf16(c0, 1)};
@@ -980,16 +953,11 @@ __device__ __forceinline__ void qnet_forward(const uint8_t* net, const float* ti
       for (int m2 = 0; m2 < kQH2 / 32; ++m2) {
 #pragma unroll
         for (int sk = 0; sk < 2; ++sk) {
-#if MG_QNET_PREFETCH == 1 || MG_QNET_PREFETCH == 2
-          const bf16x8 a2 = a2f[m2][sk];
-#elif MG_QNET_PREFETCH == 3
-          // one fragment ahead: the next load is in flight under this pair of MFMAs
+          // one fragment ahead: the next load is in flight under this pair of MFMAs (loaded at
+          // its use, each pair waited on LDS; all eight up front spilled: +17 %)
           const bf16x8 a2 = a2cur;
           if (2 * m2 + sk + 1 < kQH2 / 16) a2cur = w2frag((2 * m2 + sk + 1) >> 1, (sk + 1) & 1);
           __builtin_amdgcn_sched_barrier(0);
-#else
-          const bf16x8 a2 = w2frag(m2, sk);
-#endif
           acc2a[m2] = mfma32(a2, ha[sk], acc2a[m2]);
           acc2b[m2] = mfma32(a2, hb[sk], acc2b[m2]);
         }
@@ -1009,59 +977,7 @@ __device__ __forceinline__ void qnet_forward(const uint8_t* net, const float* ti
       }
     }
   }
-#else
-  // One N-tile (32 envs = lanes 32*NT .. 32*NT+31) at a time: 4 layer-2 accumulators live
-  // instead of 8 (W2 fragments are re-read from LDS per tile, which the LDS rate covers).
-  f32x16 acc3_0, acc3_1;
-#pragma unroll 1
-  for (int nt = 0; nt < 2; ++nt) {
-    const int z = opaque_zero();
-    const __bf16* W1 = W1_ + z;
-    const __bf16* W2 = W2_ + z;
-    const __bf16* W3 = W3_ + z;
-    const float* B1 = B1_ + z;
-    const float* B2 = B2_ + z;
-    const float* B3 = B3_ + z;
-    // layer-1 B operand: X'[k = 8h + j][env 32 nt + r]
-    const bf16x8 xb = qnet_input(tile + (row0 + 32 * nt + r) * kObs, swap, h);
-    f32x16 acc2[4];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) acc2[m] = bias_tile(B2 + 32 * m, h);
-    // rolled on purpose: unrolled, hipcc hoists all 56 W2 fragment loads ahead of the MFMAs
-    // and runs out of registers
-#pragma unroll 1
-    for (int mt = 0; mt < kQH1 / 32; ++mt) {
-      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(W1 + (32 * mt + r) * kQS1 + 8 * h);
-      // the bias is the accumulator's initial value: fp32, no per-element add afterwards
-      const f32x16 c = mfma32(a1, xb, bias_tile(B1 + 32 * mt, h));
-      const bf16x8 hb[2] = {relu_bf16(c, 0), relu_bf16(c, 1)};  // [k-step]
-#pragma unroll
-      for (int m2 = 0; m2 < kQH2 / 32; ++m2) {
-#pragma unroll
-        for (int sk = 0; sk < 2; ++sk) {
-          const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(W2 + (32 * m2 + r) * kQS2 +
-                                                             16 * (2 * mt + sk) + 8 * h);
-          acc2[m2] = mfma32(a2, hb[sk], acc2[m2]);
-        }
-      }
-    }
-    f32x16 a3acc = bias_tile(B3, h);
-#pragma unroll
-    for (int m2 = 0; m2 < kQH2 / 32; ++m2) {
-      const bf16x8 hb[2] = {relu_bf16(acc2[m2], 0), relu_bf16(acc2[m2], 1)};
-#pragma unroll
-      for (int sk = 0; sk < 2; ++sk) {
-        const bf16x8 a3 =
-            *reinterpret_cast<const bf16x8*>(W3 + r * kQS3 + 16 * (2 * m2 + sk) + 8 * h);
-        a3acc = mfma32(a3, hb[sk], a3acc);
-      }
-    }
-    if (nt == 0)  // wave-uniform branch: keeps both tiles in registers (no indexed array)
-      acc3_0 = a3acc;
-    else
-      acc3_1 = a3acc;
-  }
-#endif
+
   // Column r of N-tile t is the env of lane 32t + r. Rows 0-3 sit in registers 0-3 of lane
   // half 0, rows 4-7 in registers 0-3 of lane half 1: swap halves across the wave.
 #pragma unroll
