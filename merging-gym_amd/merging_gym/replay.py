@@ -120,9 +120,14 @@ class ReplayRing:
         self._keepalive = (obs_first, obs, a1, rew, done, final_obs, won_mask)
 
     def store_rollout(self, obs_first, traj, skip_ego_won: bool = True):
-        """Append a MergeVecEnv rollout (the dict rollout_random / rollout_qnet return)."""
+        """Append a MergeVecEnv rollout (the dict rollout_random / rollout_qnet return). With
+        autoreset the obs row of a finished env is already the reset observation, so the
+        terminal one must come from final_observation (roll out with final_observation=True)."""
+        if traj.get("final_observation") is None:
+            raise ValueError("the rollout has no final_observation: episode ends would store the "
+                             "reset observation as next_state; roll out with final_observation=True")
         self.store(obs_first, traj["obs"], traj["a1"], traj["rew"], traj["done"],
-                   traj.get("final_observation"), traj.get("won_mask"), skip_ego_won)
+                   traj["final_observation"], traj.get("won_mask"), skip_ego_won)
 
     def store_transition(self, state, action, reward, next_state):
         """The reference's single-transition call (main.py:115-119), through the same kernels."""

@@ -96,6 +96,10 @@ class TrajectoryCSVLogger:
     def log(self, obs_first, traj):
         import torch
 
+        if traj.get("won_mask") is None:
+            raise ValueError("the rollout has no won_mask (human_player.py:180's filter needs it): "
+                             "roll out with won_mask=True")
+
         ids = torch.as_tensor(self.env_ids, dtype=torch.long, device=traj["obs"].device)
         sel = lambda t: t.index_select(1, ids).cpu().numpy()  # noqa: E731  [T, k, ...]
         obs = sel(traj["obs"])

@@ -121,6 +121,12 @@ def test_store_without_filter_and_single_transition(torch):
         ring.store(torch.zeros((2, 10), device="cuda:0"), torch.zeros((1, 2, 10), device="cuda:0"),
                    torch.zeros((1, 2), dtype=torch.int8, device="cuda:0"),
                    torch.zeros((1, 2, 2), device="cuda:0"))  # filter asked for, no won bits
+    from merging_gym import MergeVecEnv
+
+    env = MergeVecEnv(64, device="cuda:0")
+    traj = env.rollout_random(4, 1, final_observation=False)
+    with pytest.raises(ValueError):  # episode ends need the terminal observation
+        ring.store_rollout(env.obs.clone(), traj)
 
 
 def test_step_won_mask_matches_oracle(torch, coracle):
