@@ -11,8 +11,8 @@ scripts/hdqn.py, scripts/main.py and scripts/human_player.py's list arithmetic
 
 The step itself runs on the GPU: a batch of one env in the same kernel as MergeVecEnv,
 writing a packed fp64 record (mg_rec64) that is copied back once per call. The pygame UI
-methods (render / plot / intro / prepare / feedback / finish) are out of scope for this
-build and raise NotImplementedError.
+methods (render / plot / intro / prepare / feedback / finish) draw that state through
+envs/ui.py, importing pygame at the first UI call.
 """
 
 from __future__ import annotations
@@ -112,6 +112,7 @@ class MergeEnv(_EnvBase):
                                            ctypes.c_void_p(self._err.data_ptr()))
 
         self._time, self._steps, self._dirty = 0, 0, False
+        self._ui = None
         self.reset()
 
     # ------------------------------------------------------------------ plumbing
@@ -272,15 +273,50 @@ class MergeEnv(_EnvBase):
         self.observe()
         return bool(self._coll_dev[0].item())
 
-    # ------------------------------------------------------------------ UI: out of scope
-    def _ui(self, *a, **k):
-        raise NotImplementedError("pygame rendering (merging_env.py:241-395) is out of scope for the "
-                                  "MI355X build; see DESIGN.md")
+    # ------------------------------------------------------------------ UI (pygame, lazy)
+    @property
+    def ui(self):
+        """The pygame window (envs/ui.py MergeUI), created at the first UI call -- the
+        reference opens it in __init__ (:83-108); here the step path never touches pygame."""
+        if self._ui is None:
+            from .ui import MergeUI
 
-    render = plot = intro = prepare = feedback = finish = _ui
+            self._ui = MergeUI()
+        return self._ui
+
+    @ui.setter
+    def ui(self, value):
+        self._ui = value
+
+    def render_view(self):
+        """The state render() draws: the host mirror of the device step record (or what a
+        caller assigned to state1 / state2 / r*_accumulate since)."""
+        return {"pos1": self._s1["pos"], "vel1": self._s1["vel"], "acc1": self._s1["acc"],
+                "pos2": self._s2["pos"], "vel2": self._s2["vel"], "acc2": self._s2["acc"],
+                "r1": self._r1acc, "r2": self._r2acc}
+
+    def render(self, goal=None, goal_op=None, player=1, sum_r1=0, sum_r2=0, tag_left=None,
+               tag_right=None, last_r1=0, last_r2=0):
+        """merging_env.py:241-342 (sum_r* / last_r* are accepted and unused, as there)."""
+        self.ui.render(self.render_view(), goal, goal_op, player, tag_left, tag_right)
+
+    def plot(self, player=1):
+        self.ui.plot(player)
+
+    def intro(self, player=1):
+        self.ui.intro(player)
+
+    def prepare(self, player=1):
+        self.ui.prepare(player)
+
+    def feedback(self, player=1):
+        self.ui.feedback(self._r1acc, self._r2acc, player)
+
+    def finish(self, sum_r1, sum_r2, player=1):
+        self.ui.finish(sum_r1, sum_r2, player)
 
     def close(self):
-        pass
+        pass  # the reference's close() is cv2.destroyAllWindows() (:398-399): no cv2 window here
 
 
 _ACTION_CODE = {0: 0, 1: 1, 2: 2, 3: 3, 4: 4}  # keys of action_dict (merging_env.py:101)

@@ -279,6 +279,24 @@ class MergeVecEnv:
     def winner(self):
         return (self.tf & self._nat.TF_WINNER_MASK) >> self._nat.TF_WINNER_SHIFT
 
+    def render_view(self, i: int, acc=(0.0, 0.0)):
+        """Env i's state as envs/ui.py draws it (`MergeUI(...).render(env.render_view(i))`):
+        positions, speeds and accumulated rewards of row i, read back from the device. The
+        last step's accelerations are not kept on the device; `acc` stands in for
+        state{1,2}['acc'], which only picks the cars' colour (merging_env.py:270-288). A row
+        that has not stepped since its reset has the reference's reset types (int 50, int 0)."""
+        i = int(i)
+        if not 0 <= i < self.num_envs:
+            raise IndexError(f"env {i} out of range [0, {self.num_envs})")
+        torch = self._torch
+        row = torch.stack([t[i] for t in (self.p1, self.v1, self.p2, self.v2, self.ret1, self.ret2)])
+        p1, v1, p2, v2, r1, r2 = (float(x) for x in row.cpu())
+        if int(self.tf[i].item()) & self._nat.TF_STEPS_MASK == 0 and (p1, p2, r1, r2) == (50.0, 50.0, 0.0, 0.0):
+            p1 = p2 = 50
+            r1 = r2 = 0
+        return {"pos1": p1, "vel1": v1, "acc1": float(acc[0]), "pos2": p2, "vel2": v2,
+                "acc2": float(acc[1]), "r1": r1, "r2": r2}
+
     def episode_statistics(self):
         """Completed-episode totals per env: returns sum [N,2] f64 and counts [N,4] i32
         (episodes, collisions, ego-first arrivals, steps)."""
