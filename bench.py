@@ -397,8 +397,9 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (deterministic reset, Philox4x32-10 uniform actions for both players)",
-            "config": {"workload": "config 3/4: 1,048,576 envs per MI355X, device-drawn random actions, "
-                                   "autoreset, episode statistics",
+            "config": {"workload": (("config 3/4: " if E == 1 << 20 else "")
+                                    + f"{E:,} envs per MI355X, device-drawn random actions, "
+                                    "autoreset, episode statistics"),
                        "envs_per_gpu": E, "global_envs": world * E,
                        "parallelism": f"dp{world} (env shards, no per-step collective)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
