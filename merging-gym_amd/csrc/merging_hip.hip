@@ -759,6 +759,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kQH1 = 224, kQH2 = 128, kQOut = 32;                 // padded 200, 100, out
+constexpr int kQH1Real = 200, kQH2Real = 100;                      // main.py:30-47 Net widths
 constexpr int kQS1 = 24, kQS2 = 232, kQS3 = 136;                   // row strides (bf16): every
 constexpr int kQOffW2 = kQH1 * kQS1 * 2;                           // ds_read_b128 lane group hits
 constexpr int kQOffW3 = kQOffW2 + kQH2 * kQS2 * 2;                 // 16 distinct 4-bank slots
@@ -1048,17 +1049,21 @@ __device__ __forceinline__ void qnet_forward_swp(const uint8_t* net, const float
     return *reinterpret_cast<const bf16x8*>(W2 + (32 * (j >> 1) + r) * kQS2 + 16 * (2 * mt + (j & 1)) + 8 * h);
   };
   // one hidden tile: its layer 2, with the next tile's layer 1 + ReLU folded in when `more`
-  // (a constant at both call sites: the last tile is peeled, so no branch per ReLU piece)
-  auto tile_step = [&](int mt, bool more) __attribute__((always_inline)) {
+  // (a constant at both call sites: the last tile is peeled, so no branch per ReLU piece).
+  // nk: 16-unit k-blocks of the tile that hold real units -- the last tile's second block
+  // (units 208-223) is all padding, zero weights times zero activations, so it is skipped.
+  auto tile_step = [&](int mt, bool more, int nk) __attribute__((always_inline)) {
     bf16x8 a2n = w2frag(mt, 0);
     if (more) layer1(mt + 1, c0, c1);
     uint32_t nx[16];  // next tile's packed ReLU pairs, built between this tile's MFMAs
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int m2 = j >> 1, sk = j & 1;
+      if (sk >= nk) continue;
       // one fragment ahead: the next load is in flight under this pair of MFMAs
       const bf16x8 a2 = a2n;
-      if (j + 1 < 8) a2n = w2frag(mt, j + 1);
+      const int jn = nk == 2 ? j + 1 : j + 2;
+      if (jn < 8) a2n = w2frag(mt, jn);
       __builtin_amdgcn_sched_barrier(0);
       acc2a[m2] = mfma32(a2, hb[sk], acc2a[m2]);
       acc2b[m2] = mfma32(a2, hb[2 + sk], acc2b[m2]);
@@ -1077,9 +1082,12 @@ __device__ __forceinline__ void qnet_forward_swp(const uint8_t* net, const float
         hb[f] = __builtin_bit_cast(bf16x8, u32x4{nx[4 * f], nx[4 * f + 1], nx[4 * f + 2], nx[4 * f + 3]});
     }
   };
+  constexpr int kLast = kQH1 / 32 - 1;
+  static_assert(16 * (2 * kLast + 1) >= kQH1Real && 32 * kLast < kQH1Real,
+                "only the last hidden tile's second k-block is padding");
 #pragma unroll 1
-  for (int mt = 0; mt < kQH1 / 32 - 1; ++mt) tile_step(mt, true);
-  tile_step(kQH1 / 32 - 1, false);
+  for (int mt = 0; mt < kLast; ++mt) tile_step(mt, true, 2);
+  tile_step(kLast, false, 1);
   f32x16 acc3_0 = bias_tile(B3, h), acc3_1 = bias_tile(B3 + zb, h);
 #pragma unroll
   for (int m2 = 0; m2 < kQH2 / 32; ++m2) {
@@ -1087,6 +1095,7 @@ __device__ __forceinline__ void qnet_forward_swp(const uint8_t* net, const float
     const bf16x8 hbb[2] = {relu_bf16(acc2b[m2], 0), relu_bf16(acc2b[m2], 1)};
 #pragma unroll
     for (int sk = 0; sk < 2; ++sk) {
+      if (16 * (2 * m2 + sk) >= kQH2Real) continue;  // units 112-127: padding only
       const bf16x8 a3 = *reinterpret_cast<const bf16x8*>(W3 + r * kQS3 + 16 * (2 * m2 + sk) + 8 * h);
       acc3_0 = mfma32(a3, ha[sk], acc3_0);
       acc3_1 = mfma32(a3, hbb[sk], acc3_1);
