@@ -139,7 +139,7 @@ def rollout_leg(env, args, world, dist, torch):
 
 
 QNET_USEFUL_FLOP = 2 * (10 * 200 + 200 * 100 + 100 * 5)      # one Net forward, main.py:30-47
-QNET_MFMA_FLOP = 142 * 32 * 32 * 16 * 2 // 64                 # padded 224/128/32 tiles, per env
+QNET_MFMA_FLOP = 132 * 32 * 32 * 16 * 2 // 64  # MFMAs issued per 64 envs (padded tiles, all-padding k-blocks skipped), per env
 MFMA_BF16_PEAK_TFLOPS = 2500.0                                 # MI355X dense bf16
 
 
