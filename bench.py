@@ -26,12 +26,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "merging-gym_amd"))
 
 # Algorithmic bytes per env-step of mg_step_random (DESIGN.md "Roofline"):
-#   read  p1 v1 p2 v2 ret1 ret2 (6 x f64) + tf (u32)                      = 52
-#   write the same state 52 + obs 10 x f32 40 + rew 2 x f32 8 + done 1 + coll 1
-#         + actions 2 x i8 2                                            = 104
+#   read  p1 v1 p2 v2 ret1 ret2 (6 x f64) + tf (u16)                      = 50
+#   write the same state 50 + obs 10 x f32 40 + rew 2 x f32 8 + done 1 + coll 1
+#         + actions 2 x i8 2                                            = 102
 # (final_obs / episode-statistics writes happen only for the ~0.5 % of envs that finish
 #  in a step and are not counted.)
-BYTES_PER_ENV_STEP = 156
+BYTES_PER_ENV_STEP = 152
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 KERNEL_NAME = "step_kernel<1, false>"
 
@@ -104,7 +104,7 @@ def load_pmc(envs: int):
 def rollout_leg(env, args, world, dist, torch):
     """The fused T-step kernel (mg_rollout_random): same per-step work and outputs, the env's
     state read and written once per launch. Algorithmic bytes per env-step:
-    52 (obs 40 + rew 8 + done 1 + coll 1 + actions 2) + 104 / T (state in and out)."""
+    52 (obs 40 + rew 8 + done 1 + coll 1 + actions 2) + 100 / T (state in and out)."""
     T, L, E = args.rollout_steps, args.rollout_launches, env.num_envs
     k = 10_000_000
     for _ in range(3):
@@ -129,7 +129,7 @@ def rollout_leg(env, args, world, dist, torch):
                      device="cpu" if args.dist_backend != "nccl" else env.device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    bytes_per_env_step = 52.0 + 104.0 / T
+    bytes_per_env_step = 52.0 + 100.0 / T
     achieved = bytes_per_env_step * E * T / (kernel_ms * 1e-3) / 1e9
     return {"kernel": "rollout_kernel", "steps_per_launch": T, "launches": L,
             "value": world * E * T * L / float(t[0]), "unit": "env-steps/s",

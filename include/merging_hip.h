@@ -49,16 +49,17 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 3
+#define MG_ABI_VERSION 4
 #define MG_OBS_DIM 10   /* merging_env.py:75 observation_shape = (10) */
 #define MG_NUM_ACTIONS 5 /* merging_env.py:101-102 action_dict / Discrete(5) */
 #define MG_ACTION_NONE (-1) /* action2=None: the constant-speed "L0" opponent, merging_env.py:152 */
 
-/* Bits of mg_state.tf (one uint32 per env). */
-#define MG_TF_STEPS_MASK 0x0000FFFFu /* steps since reset, saturating at 65535 */
-#define MG_TF_WINNER_SHIFT 16        /* 2 bits: 0 = None, 1 = ego, 2 = opponent (self.winner) */
-#define MG_TF_WINNER_MASK 0x00030000u
-#define MG_TF_DONE 0x00040000u       /* self.done */
+/* Bits of mg_state.tf (one uint16 per env). The step count only decides the timeout (done from
+ * step 2501, merging_env.py:141-143), so it saturates at 8191. */
+#define MG_TF_STEPS_MASK 0x1FFFu  /* steps since reset, saturating at 8191 */
+#define MG_TF_WINNER_SHIFT 13     /* 2 bits: 0 = None, 1 = ego, 2 = opponent (self.winner) */
+#define MG_TF_WINNER_MASK 0x6000u
+#define MG_TF_DONE 0x8000u        /* self.done */
 
 /* Flags argument of mg_step / mg_step_random. */
 #define MG_AUTORESET 0x1u /* gym.vector semantics: an env that is done after this step is reset
@@ -107,7 +108,7 @@ typedef struct mg_state {
   double* v2;   /* state2['vel'] */
   double* ret1; /* r1_accumulate */
   double* ret2; /* r2_accumulate */
-  uint32_t* tf; /* step count | winner | done, see MG_TF_* */
+  uint16_t* tf; /* step count | winner | done, see MG_TF_* */
 } mg_state;
 
 /* Packed fp64 record for the single-env (list API) path. */

@@ -66,6 +66,11 @@ namespace {
 // unpaired forward that fits
 #define MG_QNET_WS_ENV_WAVES 4
 #endif
+#ifndef MG_QNET_WS_ILP
+// specialised kernel: envs each env-wave lane steps per phase, in lockstep (independent fp64
+// chains interleaved in one instruction stream); the Q-net waves take ILP tiles per phase
+#define MG_QNET_WS_ILP 2
+#endif
 #ifndef MG_QNET_WS
 #define MG_QNET_WS 1  // Q-net rollout: specialised waves (4 Q-net + 4 env) instead of uniform ones
 #endif
@@ -161,20 +166,25 @@ __device__ __attribute__((noinline)) void sincos_cold(double t, double* s, doubl
 __device__ __forceinline__ void sincos_cold(double t, double* s, double* c) { sincos(t, s, c); }
 #endif
 
+// the polynomial branch (|t| < 1/16)
+__device__ __forceinline__ void sincos_poly(double t, double& s, double& c) {
+  const double t2 = t * t;
+  const double ps = fma(t2, fma(t2, fma(t2, 2.7557319223985893e-06, -1.9841269841269841e-04),
+                                8.3333333333333332e-03),
+                        -1.6666666666666666e-01);
+  s = fma(t * t2, ps, t);
+  const double pc =
+      fma(t2, fma(t2, fma(t2, fma(t2, -2.7557319223985888e-07, 2.4801587301587302e-05),
+                          -1.3888888888888889e-03),
+                  4.1666666666666664e-02),
+          -0.5);
+  c = fma(t2, pc, 1.0);
+}
+
 __device__ __forceinline__ void arc_sincos(double t, double& s, double& c) {
 #if MG_FAST_SINCOS
   if (fabs(t) < 0.0625) {
-    const double t2 = t * t;
-    const double ps = fma(t2, fma(t2, fma(t2, 2.7557319223985893e-06, -1.9841269841269841e-04),
-                                  8.3333333333333332e-03),
-                          -1.6666666666666666e-01);
-    s = fma(t * t2, ps, t);
-    const double pc =
-        fma(t2, fma(t2, fma(t2, fma(t2, -2.7557319223985888e-07, 2.4801587301587302e-05),
-                            -1.3888888888888889e-03),
-                    4.1666666666666664e-02),
-            -0.5);
-    c = fma(t2, pc, 1.0);
+    sincos_poly(t, s, c);
     return;
   }
   sincos_cold(t, &s, &c);
@@ -183,17 +193,45 @@ __device__ __forceinline__ void arc_sincos(double t, double& s, double& c) {
 #endif
 }
 
+// arc_sincos of M angles: when every one is in the polynomial's range (the usual case) the M
+// polynomials form one straight-line block the scheduler can interleave; otherwise each angle
+// takes arc_sincos's own branch. Same results as M arc_sincos calls.
+template <int M>
+__device__ __forceinline__ void arc_sincos_n(const double (&t)[M], double (&s)[M], double (&c)[M]) {
+#if MG_FAST_SINCOS
+  bool fast = true;
+#pragma unroll
+  for (int k = 0; k < M; ++k) fast = fast && fabs(t[k]) < 0.0625;
+  if (fast) {
+#pragma unroll
+    for (int k = 0; k < M; ++k) sincos_poly(t[k], s[k], c[k]);
+    return;
+  }
+#endif
+#pragma unroll
+  for (int k = 0; k < M; ++k) arc_sincos(t[k], s[k], c[k]);
+}
+
 // lon2coord (merging_env.py:48-58): position along the arc -> (x longitudinal, y lateral).
-// The ego rides the arc on +y, the opponent its mirror image on -y.
-__device__ __forceinline__ void lon2coord(const mg_params& P, double lon, bool ego, double& x,
-                                          double& y) {
-  const double angle = P.angle0 - div_const(lon, P.R, P.inv_R);
-  double s, c;
-  arc_sincos(angle, s, c);
+// The ego rides the arc on +y, the opponent its mirror image on -y. Split in three so the
+// lockstep step can batch the sin/cos of several cars.
+__device__ __forceinline__ double arc_angle(const mg_params& P, double lon) {
+  return P.angle0 - div_const(lon, P.R, P.inv_R);
+}
+
+__device__ __forceinline__ void arc_xy(const mg_params& P, double s, double c, bool ego, double& x,
+                                       double& y) {
   x = P.R * s;
   const double d = P.R - P.R * c;
   const double half_w = P.W * 0.5;  // W/2 = 150.0 exactly
   y = ego ? (half_w + d) : (half_w - d);
+}
+
+__device__ __forceinline__ void lon2coord(const mg_params& P, double lon, bool ego, double& x,
+                                          double& y) {
+  double s, c;
+  arc_sincos(arc_angle(P, lon), s, c);
+  arc_xy(P, s, c, ego, x, y);
 }
 
 // corners (merging_env.py:232-239) is called as corners(agent, y=x, x=y, 0) (:201-202), so
@@ -303,7 +341,7 @@ __device__ __forceinline__ void store_env(const mg_state& S, int64_t i, const En
   st_state(S.v2 + i, e.v2);
   st_state(S.ret1 + i, e.ret1);
   st_state(S.ret2 + i, e.ret2);
-  st_state(S.tf + i, pack_tf(e));
+  st_state(S.tf + i, static_cast<uint16_t>(pack_tf(e)));
 }
 
 // What one step returns besides the new state.
@@ -331,13 +369,35 @@ __device__ __forceinline__ void draw_actions(uint64_t gi, uint64_t step, uint64_
   a2 = opp_random ? action_from_u32(u.y) : MG_ACTION_NONE;
 }
 
-// MergeEnv.step (merging_env.py:138-195) for one env held in registers.
-__device__ __forceinline__ void env_step(const mg_params& P, Env& e, int a1, int a2, StepOut& r) {
-  // time_stamp += dT; done if time_stamp > 500 (:141-143). The fp64 clock first exceeds 500
-  // on step 2501; an integer count reproduces that exactly.
+// time_stamp += dT; done if time_stamp > 500 (:141-143). The fp64 clock first exceeds 500
+// on step 2501; an integer count reproduces that exactly.
+__device__ __forceinline__ void env_clock(const mg_params& P, Env& e) {
   e.steps = e.steps < MG_TF_STEPS_MASK ? e.steps + 1 : e.steps;
   if (static_cast<int32_t>(e.steps) >= P.timeout_steps) e.done = true;
+}
 
+// mpc_1d (helper.py:152-191): min u'(D'D + 0.01 I)u s.t. sum(dt u) = vt - v0 (the only row of
+// the constraint passed to solve_qp, :172-173, :182). D.1 = 0, so P.1 = 0.01 * 1 and the
+// minimiser is u = (vt - v0) / t * 1; action() = u[0].
+__device__ __forceinline__ double mpc_acc(const mg_params& P, int a, double v) {
+  return div_const(P.action_speed[a] - v, P.prediction_t, P.inv_prediction_t);
+}
+
+// v = max(0, v + acc*dT) (an int 0 when the max picks 0), p += v*dT  (:149-150, :153-154)
+__device__ __forceinline__ void move_car(const mg_params& P, double acc, double& p, double& v,
+                                         bool& v_int) {
+  const double nv = v + acc * P.dT;
+  v_int = !(nv > 0.0);
+  v = v_int ? 0.0 : nv;
+  p = p + v * P.dT;
+}
+
+__device__ __forceinline__ void score_step(const mg_params& P, Env& e, double x1, double y1,
+                                           double x2, double y2, StepOut& r, bool frozen = false);
+
+// MergeEnv.step (merging_env.py:138-195) for one env held in registers.
+__device__ __forceinline__ void env_step(const mg_params& P, Env& e, int a1, int a2, StepOut& r) {
+  env_clock(P, e);
   const bool bad1 = !valid_action(a1);
   const bool bad2 = !(a2 == MG_ACTION_NONE || valid_action(a2));
   r.bad = (bad1 ? 1 : 0) | (bad2 ? 2 : 0);
@@ -346,14 +406,8 @@ __device__ __forceinline__ void env_step(const mg_params& P, Env& e, int a1, int
   r.done = r.coll = r.r1_int = r.r2_int = false;
   r.r1 = r.r2 = 0.0;
   if (!bad1) {
-    // mpc_1d (helper.py:152-191): min u'(D'D + 0.01 I)u s.t. sum(dt u) = vt - v0 (the only
-    // row of the constraint passed to solve_qp, :172-173, :182). D.1 = 0, so P.1 = 0.01 * 1
-    // and the minimiser is u = (vt - v0) / t * 1; action() = u[0].
-    r.acc1 = div_const(P.action_speed[a1] - e.v1, P.prediction_t, P.inv_prediction_t);
-    const double nv = e.v1 + r.acc1 * P.dT;  // max(0, v + acc*dT)  :149
-    r.v1_int = !(nv > 0.0);
-    e.v1 = r.v1_int ? 0.0 : nv;
-    e.p1 = e.p1 + e.v1 * P.dT;  // :150
+    r.acc1 = mpc_acc(P, a1, e.v1);
+    move_car(P, r.acc1, e.p1, e.v1, r.v1_int);
   }
   if (r.bad) {  // the reference raises KeyError at action_dict[...] after advancing this far
 #pragma unroll
@@ -361,24 +415,80 @@ __device__ __forceinline__ void env_step(const mg_params& P, Env& e, int a1, int
     return;
   }
   // action2 None -> acc 0 (:152): the "L0" constant-speed opponent
-  if (a2 != MG_ACTION_NONE)
-    r.acc2 = div_const(P.action_speed[a2] - e.v2, P.prediction_t, P.inv_prediction_t);
-  const double nv2 = e.v2 + r.acc2 * P.dT;  // :153
-  r.v2_int = !(nv2 > 0.0);
-  e.v2 = r.v2_int ? 0.0 : nv2;
-  e.p2 = e.p2 + e.v2 * P.dT;  // :154
+  if (a2 != MG_ACTION_NONE) r.acc2 = mpc_acc(P, a2, e.v2);
+  move_car(P, r.acc2, e.p2, e.v2, r.v2_int);
 
   double x1, y1, x2, y2;
   lon2coord(P, e.p1, true, x1, y1);
   lon2coord(P, e.p2, false, x2, y2);
+  score_step(P, e, x1, y1, x2, y2, r);
+}
+
+// N envs stepped statement by statement, so their independent fp64 chains interleave in one
+// instruction stream. Identical results to N env_step calls, invalid actions included: those
+// are computed with a stand-in action and their effects dropped by selects (the ego keeps its
+// move unless action1 is bad; nothing after the moves happens, as in env_step's early return).
+template <int N>
+__device__ __forceinline__ void env_step_lockstep(const mg_params& P, Env (&e)[N], const int (&a1)[N],
+                                                  const int (&a2)[N], StepOut (&r)[N]) {
+  double ang[2 * N], sn[2 * N], cs[2 * N];
+  bool bad[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const bool bad1 = !valid_action(a1[j]);
+    const bool none2 = a2[j] == MG_ACTION_NONE;
+    const bool bad2 = !(none2 || valid_action(a2[j]));
+    bad[j] = bad1 || bad2;
+    r[j].bad = (bad1 ? 1 : 0) | (bad2 ? 2 : 0);
+    r[j].r1_int = r[j].r2_int = false;
+    env_clock(P, e[j]);
+    const double acc1 = mpc_acc(P, bad1 ? 0 : a1[j], e[j].v1);
+    r[j].acc1 = bad1 ? 0.0 : acc1;
+    double p = e[j].p1, v = e[j].v1;
+    bool vi;
+    move_car(P, r[j].acc1, p, v, vi);
+    e[j].p1 = bad1 ? e[j].p1 : p;
+    e[j].v1 = bad1 ? e[j].v1 : v;
+    r[j].v1_int = !bad1 && vi;
+    const double acc2 = mpc_acc(P, (none2 || bad2) ? 0 : a2[j], e[j].v2);
+    r[j].acc2 = (none2 || bad[j]) ? 0.0 : acc2;
+    p = e[j].p2;
+    v = e[j].v2;
+    move_car(P, r[j].acc2, p, v, vi);
+    e[j].p2 = bad[j] ? e[j].p2 : p;
+    e[j].v2 = bad[j] ? e[j].v2 : v;
+    r[j].v2_int = !bad[j] && vi;
+    ang[2 * j] = arc_angle(P, e[j].p1);
+    ang[2 * j + 1] = arc_angle(P, e[j].p2);
+  }
+  arc_sincos_n<2 * N>(ang, sn, cs);
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    double x1, y1, x2, y2;
+    arc_xy(P, sn[2 * j], cs[2 * j], true, x1, y1);
+    arc_xy(P, sn[2 * j + 1], cs[2 * j + 1], false, x2, y2);
+    score_step(P, e[j], x1, y1, x2, y2, r[j], bad[j]);
+  }
+}
+
+// The rest of a step once both cars have moved (merging_env.py:156-192): observation, rewards,
+// arrival / winner, collision, returns. r.r1_int / r.r2_int must be false on entry. frozen: an
+// invalid action -- the step stops before any of this (observation and rewards 0, no state
+// change), as env_step's early return.
+__device__ __forceinline__ void score_step(const mg_params& P, Env& e, double x1, double y1,
+                                           double x2, double y2, StepOut& r, bool frozen) {
   observe(P, e.p1, e.v1, e.p2, e.v2, x1, y1, x2, y2, r.o);
+  if (frozen) {
+#pragma unroll
+    for (int k = 0; k < kObs; ++k) r.o[k] = 0.0;
+  }
 
   // rewards (:158-159): -time_penalty - vel_penalty * |v - 20|
   double r1 = (0.0 - P.time_penalty) - P.vel_penalty * fabs(e.v1 - P.vel_ref);
   double r2 = (0.0 - P.time_penalty) - P.vel_penalty * fabs(e.v2 - P.vel_ref);
 
   // arrival / winner state machine (:163-181); ego strict '>', opponent '>='
-  if (e.p1 > P.end_point) {
+  if (!frozen && e.p1 > P.end_point) {
     if (e.winner == 0) {
       e.winner = 1;
       r1 += P.r_first;
@@ -390,7 +500,7 @@ __device__ __forceinline__ void env_step(const mg_params& P, Env& e, int a1, int
       e.done = true;
     }
   }
-  if (e.p2 >= P.end_point) {
+  if (!frozen && e.p2 >= P.end_point) {
     if (e.winner == 0) {
       e.winner = 2;
       r2 += P.r_first;
@@ -404,17 +514,19 @@ __device__ __forceinline__ void env_step(const mg_params& P, Env& e, int a1, int
   }
 
   // is_collided (:183-187, :198-206)
-  r.coll = boxes_intersect(vehicle_box(P, y1, x1), vehicle_box(P, y2, x2));
+  r.coll = !frozen && boxes_intersect(vehicle_box(P, y1, x1), vehicle_box(P, y2, x2));
   if (r.coll) {
     e.done = true;
     r1 += P.r_collision;
     r2 += P.r_collision;
   }
-  e.ret1 += r1;  // :191-192
-  e.ret2 += r2;
-  r.r1 = r1;
-  r.r2 = r2;
-  r.done = e.done;
+  if (!frozen) {
+    e.ret1 += r1;  // :191-192
+    e.ret2 += r2;
+  }
+  r.r1 = frozen ? 0.0 : r1;
+  r.r2 = frozen ? 0.0 : r2;
+  r.done = !frozen && e.done;
 }
 
 // Completed-episode statistics of one env held in registers for a multi-step launch: loaded
@@ -532,6 +644,8 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 // The same as store_obs_tile for one wave's 64 rows: the wave's tile slice holds the new
 // observations afterwards, and no other wave is waited for.
+__device__ __forceinline__ void wave_copy_rows(const float* wtile, float* dst, int nrows);
+
 __device__ __forceinline__ void wave_store_obs(float* wtile, const double (&o)[kObs], float* dst,
                                                int nrows) {
   const int lane = threadIdx.x & 63;
@@ -540,6 +654,31 @@ __device__ __forceinline__ void wave_store_obs(float* wtile, const double (&o)[k
   for (int k = 0; k < kObs / 2; ++k)
     t2[k] = make_float2(static_cast<float>(o[2 * k]), static_cast<float>(o[2 * k + 1]));
   wave_lds_sync();
+  wave_copy_rows(wtile, dst, nrows);
+  wave_lds_sync();
+}
+
+// wave_store_obs for N consecutive 64-row slices (slice j = r[j].o of every lane), written out
+// as one run of nrows <= 64 N rows.
+template <int N>
+__device__ __forceinline__ void wave_store_obs_n(float* wtile, const StepOut (&r)[N], float* dst,
+                                                 int nrows) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    float2* t2 = reinterpret_cast<float2*>(wtile + (64 * j + lane) * kObs);
+#pragma unroll
+    for (int k = 0; k < kObs / 2; ++k)
+      t2[k] = make_float2(static_cast<float>(r[j].o[2 * k]), static_cast<float>(r[j].o[2 * k + 1]));
+  }
+  wave_lds_sync();
+  wave_copy_rows(wtile, dst, nrows);
+  wave_lds_sync();
+}
+
+// A wave's nrows x 10 fp32 LDS slice to dst: 16-byte stores when dst allows, else 8-byte.
+__device__ __forceinline__ void wave_copy_rows(const float* wtile, float* dst, int nrows) {
+  const int lane = threadIdx.x & 63;
   if (dst != nullptr && nrows > 0) {
     const int nfl = nrows * kObs;
     if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
@@ -556,7 +695,6 @@ __device__ __forceinline__ void wave_store_obs(float* wtile, const double (&o)[k
       for (int j = lane; j < n2; j += 64) st_out(d2 + j, s2[j]);
     }
   }
-  wave_lds_sync();
 }
 
 // Step t's won bits of one wave (every lane calls it): word t * ceil(n/64) + wbase / 64.
@@ -603,8 +741,10 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const Launch L) {
     int a1, a2;
     if constexpr (ACT == kActPhilox) {
       draw_actions(static_cast<uint64_t>(L.env_offset + i), L.step_idx, L.seed, L.opp_random, a1, a2);
+#if !MG_ABL_NO_BYTES
       if (L.a1_out) st_out(L.a1_out + i, static_cast<int8_t>(a1));
       if (L.a2_out) st_out(L.a2_out + i, static_cast<int8_t>(a2));
+#endif
     } else {
       a1 = L.a1[i];
       a2 = L.a2 ? static_cast<int>(L.a2[i]) : MG_ACTION_NONE;
@@ -637,8 +777,12 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const Launch L) {
         st_out(reinterpret_cast<f32x2*>(L.O.rew) + i,
                f32x2{static_cast<float>(r.r1), static_cast<float>(r.r2)});
       }
+#if !MG_ABL_NO_BYTES
       if (L.O.done) st_out(L.O.done + i, static_cast<uint8_t>(r.done ? 1 : 0));
       if (L.O.coll) st_out(L.O.coll + i, static_cast<uint8_t>(r.coll ? 1 : 0));
+#else
+      if (a1 + a2 == 1234 && r.coll) L.O.done[0] = 1;
+#endif
       won = e.winner == 1;
       if ((L.flags & MG_AUTORESET) && r.done)
         finish_episode(P, e, r, L.St, L.O.final_obs ? L.O.final_obs + i * kObs : nullptr, i);
@@ -768,11 +912,11 @@ constexpr int kQOffB2 = kQOffB1 + kQH1 * 4;
 constexpr int kQOffB3 = kQOffB2 + kQH2 * 4;
 constexpr int kQNetBytes = kQOffB3 + kQOut * 4;                    // 80,384 B
 constexpr int kQBlock = MG_QNET_BLOCK;                             // waves sharing one LDS copy
-// specialised kernel: 4 Q-net waves + MG_QNET_WS_ENV_WAVES env waves; each env lane steps one
-// env per phase, so a group is 64 x env waves envs and a block holds two groups
+// specialised kernel: 4 Q-net waves + MG_QNET_WS_ENV_WAVES env waves; each env lane steps
+// MG_QNET_WS_ILP envs per phase, so a group is 64 x env waves x ILP envs and a block holds two
 constexpr int kQWsThreads = 64 * (4 + MG_QNET_WS_ENV_WAVES);
 constexpr int kQWsWavesPerSimd = (4 + MG_QNET_WS_ENV_WAVES) / 4;
-constexpr int kQWsEnvs = 2 * 64 * MG_QNET_WS_ENV_WAVES;
+constexpr int kQWsEnvs = 2 * 64 * MG_QNET_WS_ENV_WAVES * MG_QNET_WS_ILP;
 static_assert(kQOffW2 % 16 == 0 && kQOffW3 % 16 == 0 && kQOffB1 % 16 == 0 && kQOffB2 % 16 == 0 &&
                   kQOffB3 % 16 == 0 && kQNetBytes % 16 == 0,
               "packed Q-net sections must stay 16-byte aligned");
@@ -1201,6 +1345,49 @@ __device__ __forceinline__ void qnet_policy_step(const QRollout& R, Env& e, Step
     finish_episode(R.P, e, r, R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i);
 }
 
+// qnet_policy_step for the N envs i0 + 64 j of one env-wave lane, stepped in lockstep. Envs
+// past n (live[j] false) are stepped too but never stored. A greedy action outside 0..4 (a
+// net with out_dim > 5) gets env_step's KeyError semantics (env_step_lockstep).
+template <int OPP, int N>
+__device__ __forceinline__ void qnet_policy_step_n(const QRollout& R, Env (&e)[N], StepOut (&r)[N],
+                                                   int64_t i0, const bool (&live)[N], int t,
+                                                   const int (&greedy1)[N], const int (&greedy2)[N],
+                                                   bool (&won)[N]) {
+  const uint64_t step = R.first_step + t;
+  int a1[N], a2[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const uint64_t gi = static_cast<uint64_t>(R.env_offset + i0 + 64 * j);
+    const uint4 u = philox4x32_10(
+        make_uint4(static_cast<uint32_t>(gi), static_cast<uint32_t>(gi >> 32),
+                   static_cast<uint32_t>(step), static_cast<uint32_t>(step >> 32)),
+        static_cast<uint32_t>(R.seed), static_cast<uint32_t>(R.seed >> 32));
+    a1[j] = (static_cast<uint64_t>(u.x) < R.greedy_thr) ? greedy1[j] : action_from_u32(u.y);
+    a2[j] = MG_ACTION_NONE;
+    if constexpr (OPP == 1) a2[j] = action_from_u32(u.w);
+    if constexpr (OPP == 2)
+      a2[j] = (static_cast<uint64_t>(u.z) < R.opp_greedy_thr) ? greedy2[j] : action_from_u32(u.w);
+  }
+  env_step_lockstep<N>(R.P, e, a1, a2, r);
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    won[j] = false;
+    if (!live[j]) continue;
+    const int64_t i = i0 + 64 * j;
+    const int64_t row = static_cast<int64_t>(t) * R.n + i;
+    if (R.T.a1) st_out(R.T.a1 + row, static_cast<int8_t>(a1[j]));
+    if (R.T.a2) st_out(R.T.a2 + row, static_cast<int8_t>(a2[j]));
+    if (R.T.rew)
+      st_out(reinterpret_cast<f32x2*>(R.T.rew) + row,
+             f32x2{static_cast<float>(r[j].r1), static_cast<float>(r[j].r2)});
+    if (R.T.done) st_out(R.T.done + row, static_cast<uint8_t>(r[j].done ? 1 : 0));
+    if (R.T.coll) st_out(R.T.coll + row, static_cast<uint8_t>(r[j].coll ? 1 : 0));
+    won[j] = e[j].winner == 1;
+    if ((R.flags & MG_AUTORESET) && r[j].done)
+      finish_episode(R.P, e[j], r[j], R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i);
+  }
+}
+
 // Observation of env i (or zeros past n) into its fp32 tile row; returns live.
 __device__ __forceinline__ bool qnet_load_env(const QRollout& R, int64_t i, Env& e, float* row) {
   double o[kObs];
@@ -1211,7 +1398,13 @@ __device__ __forceinline__ bool qnet_load_env(const QRollout& R, int64_t i, Env&
     lon2coord(R.P, e.p1, true, x1, y1);
     lon2coord(R.P, e.p2, false, x2, y2);
     observe(R.P, e.p1, e.v1, e.p2, e.v2, x1, y1, x2, y2, o);
-  } else {
+  } else {  // a defined state for the lockstep step, which also steps envs past n (never stored)
+    e.p1 = e.p2 = R.P.start_point;
+    e.v1 = e.v2 = R.P.start_vel;
+    e.ret1 = e.ret2 = 0.0;
+    e.steps = 0;
+    e.winner = 0;
+    e.done = false;
 #pragma unroll
     for (int k = 0; k < kObs; ++k) o[k] = 0.0;
   }
@@ -1279,10 +1472,12 @@ __global__ __launch_bounds__(kQBlock, MG_QNET_WAVES_PER_EU) void qnet_rollout_ke
 // tile rows. Each env-wave lane holds the two envs (one per group) it steps.
 template <int OPP>
 __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws_kernel(const QRollout R) {
+  constexpr int kIlp = MG_QNET_WS_ILP;
   constexpr int kHalf = kQWsEnvs / 2;   // envs per group
   constexpr int kTiles = kHalf / 256;   // 64-env tiles each Q-net wave computes per phase
   constexpr int kEnvWaves = MG_QNET_WS_ENV_WAVES;
-  static_assert(kTiles >= 1 && kHalf == 64 * kEnvWaves, "group = 4 Q-net waves x kTiles x 64 envs");
+  static_assert(kTiles >= 1 && kHalf == 64 * kEnvWaves * kIlp && kHalf % 256 == 0,
+                "group = 4 Q-net waves x kTiles x 64 envs = env waves x ILP x 64 envs");
   __shared__ __attribute__((aligned(16))) uint8_t lds_net[kQNetBytes];
   __shared__ __attribute__((aligned(16))) float tile[kQWsEnvs * kObs];
   __shared__ uint8_t greedy[2][kQWsEnvs];
@@ -1304,6 +1499,10 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
 #pragma unroll 1
         for (int tt = 0; tt < kTiles; ++tt) {
           const int row0 = (p & 1) * kHalf + (4 * tt + wave) * 64;
+#if MG_ABL_WS_NOQ  // timing ablation only: the Q-net waves skip the forward
+          greedy[0][row0 + lane] = static_cast<uint8_t>(tile[(row0 + lane) * kObs] > 0.f ? 1 : 3);
+          continue;
+#endif
           float q[8];
           qnet_forward_ws(lds_net, tile, row0, false, q);
           greedy[0][row0 + lane] = static_cast<uint8_t>(argmax_first(q, R.out_dim));
@@ -1317,48 +1516,63 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
     }
     return;
   }
-  // env lane: env ew * 64 + lane of group 0 (e0) and of group 1 (e1)
-  const int local_a = ew * 64 + lane, local_b = kHalf + ew * 64 + lane;
-  Env e0, e1;
-  StepOut r;
-  bool won0 = false, won1 = false;
-  const bool live0 = qnet_load_env(R, base + local_a, e0, tile + local_a * kObs);
-  const bool live1 = qnet_load_env(R, base + local_b, e1, tile + local_b * kObs);
+  // env lane: envs lbase + 64 j + lane (j < kIlp) of group 0 (e0) and of group 1 (e1)
+  const int lbase = ew * 64 * kIlp;
+  Env e0[kIlp], e1[kIlp];
+  StepOut r[kIlp];
+  bool live0[kIlp], live1[kIlp];
 #pragma unroll
-  for (int k = 0; k < kObs; ++k) r.o[k] = 0.0;
+  for (int j = 0; j < kIlp; ++j) {
+    const int la = lbase + 64 * j + lane, lb = kHalf + la;
+    live0[j] = qnet_load_env(R, base + la, e0[j], tile + la * kObs);
+    live1[j] = qnet_load_env(R, base + lb, e1[j], tile + lb * kObs);
+#pragma unroll
+    for (int k = 0; k < kObs; ++k) r[j].o[k] = 0.0;
+  }
   __syncthreads();
   for (int p = 0; p < phases; ++p) {
     if (p > 0) {
       const int g = (p - 1) & 1, t = (p - 1) >> 1;
-      const int local0 = g * kHalf + ew * 64;
-      const int local = local0 + lane;
-      const int64_t i = base + local;
-      const int greedy1 = greedy[0][local];
-      const int greedy2 = OPP == 2 ? greedy[1][local] : 0;
-      bool won = false;
-#if MG_ABL_WS_NOENV  // timing ablation only: the env waves skip the step
-      if (greedy1 + greedy2 == 1000) R.T.done[0] = 0;
-#else
-      if (g == 0) {  // wave-uniform: the two envs stay in named registers
-        if (live0) qnet_policy_step<OPP>(R, e0, r, i, t, greedy1, greedy2, won0);
-        won = won0;
-      } else {
-        if (live1) qnet_policy_step<OPP>(R, e1, r, i, t, greedy1, greedy2, won1);
-        won = won1;
+      const int local0 = g * kHalf + lbase;
+      int greedy1[kIlp], greedy2[kIlp];
+#pragma unroll
+      for (int j = 0; j < kIlp; ++j) {
+        greedy1[j] = greedy[0][local0 + 64 * j + lane];
+        greedy2[j] = OPP == 2 ? greedy[1][local0 + 64 * j + lane] : 0;
       }
+      bool won[kIlp];
+#if MG_ABL_WS_NOENV  // timing ablation only: the env waves skip the step
+#pragma unroll
+      for (int j = 0; j < kIlp; ++j) won[j] = false;
+      if (greedy1[0] + greedy2[0] == 1000) R.T.done[0] = 0;
+#else
+      // wave-uniform branch: each group's envs stay in named registers
+      if (g == 0)
+        qnet_policy_step_n<OPP, kIlp>(R, e0, r, base + local0 + lane, live0, t, greedy1, greedy2, won);
+      else
+        qnet_policy_step_n<OPP, kIlp>(R, e1, r, base + local0 + lane, live1, t, greedy1, greedy2, won);
 #endif
       const int64_t wbase = base + local0;
+#pragma unroll
+      for (int j = 0; j < kIlp; ++j) {
+        const int64_t rem = R.n - (wbase + 64 * j);
+        store_won_mask(R.T.won_mask, won[j], t, R.n, wbase + 64 * j,
+                       rem <= 0 ? 0 : (rem < 64 ? static_cast<int>(rem) : 64));
+      }
       const int64_t wrem = R.n - wbase;
-      const int wrows = wrem <= 0 ? 0 : (wrem < 64 ? static_cast<int>(wrem) : 64);
-      store_won_mask(R.T.won_mask, won, t, R.n, wbase, wrows);
-      wave_store_obs(tile + local0 * kObs, r.o,
-                     R.T.obs ? R.T.obs + (static_cast<int64_t>(t) * R.n + wbase) * kObs : nullptr,
-                     wrows);
+      const int wrows = wrem <= 0 ? 0 : (wrem < 64 * kIlp ? static_cast<int>(wrem) : 64 * kIlp);
+      wave_store_obs_n<kIlp>(tile + local0 * kObs, r,
+                             R.T.obs ? R.T.obs + (static_cast<int64_t>(t) * R.n + wbase) * kObs : nullptr,
+                             wrows);
     }
     __syncthreads();
   }
-  if (live0) store_env(R.S, base + local_a, e0);
-  if (live1) store_env(R.S, base + local_b, e1);
+#pragma unroll
+  for (int j = 0; j < kIlp; ++j) {
+    const int la = lbase + 64 * j + lane;
+    if (live0[j]) store_env(R.S, base + la, e0[j]);
+    if (live1[j]) store_env(R.S, base + kHalf + la, e1[j]);
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void reset_kernel(const mg_params P, const mg_state S,

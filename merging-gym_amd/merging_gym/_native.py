@@ -15,17 +15,17 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libmerging_hip.so"
 LIB_PATH = os.environ.get("MERGING_HIP_LIB", os.path.join(_HERE, LIB_NAME))
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 OBS_DIM = 10
 NUM_ACTIONS = 5
 ACTION_NONE = -1
 ACTION_INVALID = 127  # host marker for a value the reference's action_dict would reject
 
-TF_STEPS_MASK = 0x0000FFFF
-TF_WINNER_SHIFT = 16
-TF_WINNER_MASK = 0x00030000
-TF_DONE = 0x00040000
+TF_STEPS_MASK = 0x1FFF  # mg_state.tf is one uint16 per env
+TF_WINNER_SHIFT = 13
+TF_WINNER_MASK = 0x6000
+TF_DONE = 0x8000
 
 AUTORESET = 0x1
 

@@ -134,7 +134,7 @@ class MergeEnv(_EnvBase):
         tf |= nat.TF_DONE if self._done else 0
         host = np.array([self._s1["pos"], self._s1["vel"], self._s2["pos"], self._s2["vel"],
                          self._r1acc, self._r2acc, 0.0], dtype=np.float64)
-        host[6:7].view(np.uint32)[0] = tf
+        host[6:7].view(np.uint16)[0] = tf
         self._dstate.copy_(self._torch.from_numpy(host))
         self._dirty = False
 
@@ -251,7 +251,7 @@ class MergeEnv(_EnvBase):
         # reference does before its KeyError; refresh the host mirror from the device
         self._err.zero_()
         st = self._dstate.cpu().numpy()
-        tf = int(st[6:7].view(np.uint32)[0])
+        tf = int(st[6:7].view(np.uint16)[0])
         self._done = bool(tf & self._nat.TF_DONE)
         self._steps = tf & self._nat.TF_STEPS_MASK
         self._s1 = dict(self._s1, pos=float(st[0]), vel=float(st[1]))

@@ -61,7 +61,7 @@ class MergeVecEnv:
         self.p1, self.v1 = torch.empty(n, **f64), torch.empty(n, **f64)
         self.p2, self.v2 = torch.empty(n, **f64), torch.empty(n, **f64)
         self.ret1, self.ret2 = torch.empty(n, **f64), torch.empty(n, **f64)
-        self.tf = torch.empty(n, dtype=torch.int32, device=dev)
+        self.tf = torch.empty(n, dtype=torch.int16, device=dev)  # uint16 bits, see MG_TF_*
         self.obs = torch.empty((n, _OBS_DIM), dtype=torch.float32, device=dev)
         self.rew = torch.empty((n, 2), dtype=torch.float32, device=dev)
         self.done = torch.zeros(n, dtype=torch.uint8, device=dev)

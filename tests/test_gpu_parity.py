@@ -166,9 +166,11 @@ def test_golden_one_step_rows(torch, golden):
     env.v2.copy_(torch.from_numpy(g["one_v"][:, 1]))
     env.ret1.copy_(torch.from_numpy(g["one_racc"][:, 0]))
     env.ret2.copy_(torch.from_numpy(g["one_racc"][:, 1]))
-    tf = (g["one_k"].astype(np.int64) & 0xFFFF) | (g["one_winner"].astype(np.int64) << 16) | (
-        g["one_done"].astype(np.int64) << 18)
-    env.tf.copy_(torch.from_numpy(tf.astype(np.int32)))
+    nat = env._nat
+    tf = (np.minimum(g["one_k"].astype(np.int64), nat.TF_STEPS_MASK)
+          | (g["one_winner"].astype(np.int64) << nat.TF_WINNER_SHIFT)
+          | (g["one_done"].astype(np.int64) * nat.TF_DONE))
+    env.tf.copy_(torch.from_numpy(tf.astype(np.uint16).view(np.int16)))
     obs, rew, done, info = env.step(torch.from_numpy(g["one_a1"]).to(dev), torch.from_numpy(g["one_a2"]).to(dev))
     coll = info["collision"].cpu().numpy()
     bad = coll != g["one_coll"]

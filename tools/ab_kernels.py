@@ -51,7 +51,7 @@ class Bed:
         self.lib, self.n, self.T = lib, n, T
         dev = "cuda"
         f = lambda: torch.empty(n, dtype=torch.float64, device=dev)  # noqa: E731
-        self.t = [f() for _ in range(6)] + [torch.empty(n, dtype=torch.int32, device=dev)]
+        self.t = [f() for _ in range(6)] + [torch.empty(n, dtype=torch.int16, device=dev)]
         self.obs = torch.empty((n, 10), device=dev)
         self.rew = torch.empty((n, 2), device=dev)
         self.done = torch.empty(n, dtype=torch.uint8, device=dev)
@@ -186,10 +186,10 @@ def main():
     for name, d in res.items():
         s, ro = d["step"], d["rollout"]
         out[name] = {"step_us_median": 1e3 * statistics.median(s), "step_us_min": 1e3 * min(s),
-                     "step_TBps": 156 * a.envs / (statistics.median(s) * 1e-3) / 1e12,
+                     "step_TBps": 152 * a.envs / (statistics.median(s) * 1e-3) / 1e12,
                      "rollout_us_per_step_median": 1e3 * statistics.median(ro),
                      "rollout_us_per_step_min": 1e3 * min(ro),
-                     "rollout_TBps": (52 + 104 / a.T) * a.envs / (statistics.median(ro) * 1e-3) / 1e12,
+                     "rollout_TBps": (52 + 100 / a.T) * a.envs / (statistics.median(ro) * 1e-3) / 1e12,
                      "step_wall_us_median": 1e3 * statistics.median(d["step_wall"]),
                      "rollout_wall_us_per_step_median": 1e3 * statistics.median(d["rollout_wall"])}
         print(f"{name:24s} step {out[name]['step_us_median']:7.2f} us (min {out[name]['step_us_min']:6.2f}, "

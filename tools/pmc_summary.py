@@ -5,7 +5,7 @@
 Dispatch order inside each env count is reset x reps, observe x reps, step x reps (tools/profile_pmc.py),
 so rows are grouped by kernel name and then split evenly over the env counts.
 Calibration (MI355X_MICROARCH.md "HBM": on gfx950 FETCH_SIZE under-reads wide streaming loads and
-other widths are uncalibrated): reset_kernel writes exactly 52 B/env, observe_kernel reads exactly
+other widths are uncalibrated): reset_kernel writes exactly 50 B/env, observe_kernel reads exactly
 32 B/env (obs written only); the step kernel's counters are divided by those ratios. Both
 counters see L2 -> fabric traffic, so Infinity Cache (MALL) hits are counted too.
 """
@@ -50,15 +50,15 @@ def main():
             per = len(v) // len(a.envs)
             chunk = v[i * per:(i + 1) * per]
             return 1024.0 * sum(chunk) / len(chunk)  # counters are in KiB
-        cal_w = mean(w, "reset") / (52.0 * n)
+        cal_w = mean(w, "reset") / (50.0 * n)
         cal_r = mean(f, "observe") / (32.0 * n)
         sf, sw = mean(f, "step"), mean(w, "step")
         res[n] = {"envs": n, "fetch_raw_bytes": sf, "write_raw_bytes": sw,
                   "read_calibration": cal_r, "write_calibration": cal_w,
                   "fetch_bytes": sf / cal_r, "write_bytes": sw / cal_w,
                   "hbm_bytes_per_launch": sf / cal_r + sw / cal_w,
-                  "algorithmic_bytes_per_launch": 156.0 * n,
-                  "ratio_to_algorithmic": (sf / cal_r + sw / cal_w) / (156.0 * n)}
+                  "algorithmic_bytes_per_launch": 152.0 * n,
+                  "ratio_to_algorithmic": (sf / cal_r + sw / cal_w) / (152.0 * n)}
     print(json.dumps(res, indent=1))
     if a.out:
         first = res[a.envs[0]]

@@ -1,6 +1,6 @@
 """Workload for rocprofv3 PMC passes (run under `rocprofv3 --pmc ... -- python tools/profile_pmc.py`).
 
-Per env count it launches, in order: `reps` x reset_kernel (writes 52 B/env: 6 f64 + 1 u32 --
+Per env count it launches, in order: `reps` x reset_kernel (writes 50 B/env: 6 f64 + 1 u16 --
 the write calibration), `reps` x observe_kernel (reads 32 B/env of f64 -- the read
 calibration), `reps` x step_kernel<philox> (the bench kernel). tools/pmc_summary.py turns the
 counter CSVs into per-launch bytes.
