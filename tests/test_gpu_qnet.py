@@ -139,6 +139,57 @@ def test_rollout_qnet_policy_and_transitions(torch, coracle, nets, opponent, n):
     assert env._step_idx == k0 + T
 
 
+@pytest.mark.parametrize("opponent", ["none", "self"])
+def test_rollout_qnet_invalid_greedy_actions(torch, coracle, nets, opponent):
+    """A net with 8 outputs (out_dim <= 8 is allowed) picks actions 5-7, which the reference's
+    action_dict rejects with a KeyError after the clock (and the ego, for a bad action2) has
+    advanced. The fused kernel steps such an env exactly that far and emits zeros (obs, rewards,
+    flags), like the oracle's error path; every transition is compared with the oracle stepping
+    the kernel's actions, invalid ones included."""
+    from merging_gym import MergeVecEnv
+    from merging_gym.policy import QNet
+
+    sd = dict(nets["l1"])
+    w3, b3 = sd["out.weight"], sd["out.bias"]
+    # output 5 = action 2's row with a slightly larger bias: it wins wherever action 2 would
+    # (most greedy choices of this checkpoint); outputs 6-7 never win
+    sd["out.weight"] = np.concatenate([w3, w3[[2, 0, 1]]])
+    sd["out.bias"] = np.concatenate([b3, [b3[2] + 0.01, b3[0] - 100.0, b3[1] - 100.0]]).astype(np.float32)
+    qnet = QNet.from_state_dict(sd, device="cuda:0")
+    assert qnet.out_dim == 8
+    n, T, seed, k0 = 1000, 16, 23, 300
+    env = MergeVecEnv(n, device="cuda:0")
+    for k in range(40):
+        env.step_random(seed + 1, step_idx=k)
+    envs = coracle.new_envs(n)
+    for name, src in (("pos1", env.p1), ("vel1", env.v1), ("pos2", env.p2), ("vel2", env.v2),
+                      ("r1_acc", env.ret1), ("r2_acc", env.ret2)):
+        envs[name] = src.cpu().numpy()
+    envs["steps"] = env.steps.cpu().numpy()
+    envs["winner"] = env.winner.cpu().numpy()
+    envs["time_stamp"] = np.cumsum(np.full(2700, 0.2))[np.maximum(envs["steps"] - 1, 0)] * (envs["steps"] > 0)
+    traj = env.rollout_qnet(T, qnet, seed, opponent=opponent, first_step=k0)
+    traj = {k: (v.cpu().numpy() if v is not None else None) for k, v in traj.items()}
+    assert (traj["a1"] >= 5).sum() > 100
+    if opponent == "self":
+        assert (traj["a2"] >= 5).sum() > 100
+    for t in range(T):
+        o_obs, o_rew, o_done, o_coll, _, o_fobs, err = coracle.step(
+            envs, traj["a1"][t], traj["a2"][t], autoreset=True, final_obs=True)
+        assert err != 0
+        np.testing.assert_array_equal(traj["done"][t], o_done.astype(bool), err_msg=str(t))
+        np.testing.assert_array_equal(traj["collision"][t], o_coll.astype(bool), err_msg=str(t))
+        np.testing.assert_allclose(traj["obs"][t], o_obs.astype(np.float32), **OBS_TOL)
+        np.testing.assert_allclose(traj["rew"][t], o_rew.astype(np.float32), **OBS_TOL)
+        d = o_done.astype(bool)
+        np.testing.assert_allclose(traj["final_observation"][t][d], o_fobs[d].astype(np.float32), **OBS_TOL)
+    for name, src in (("pos1", env.p1), ("vel1", env.v1), ("pos2", env.p2), ("vel2", env.v2),
+                      ("r1_acc", env.ret1), ("r2_acc", env.ret2)):
+        np.testing.assert_allclose(src.cpu().numpy(), envs[name], rtol=0, atol=1e-9, err_msg=name)
+    np.testing.assert_array_equal(env.steps.cpu().numpy(), np.minimum(envs["steps"], 0x1FFF))
+    np.testing.assert_array_equal(env.winner.cpu().numpy(), envs["winner"])
+
+
 def test_greedy_threshold_is_phi_of_episilo():
     from merging_gym.policy import greedy_threshold
 
