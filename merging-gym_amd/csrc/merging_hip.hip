@@ -725,7 +725,10 @@ struct Launch {
 
 // The step kernel. OUT64 = the single-env path (packed fp64 record, no LDS staging).
 template <int ACT, bool OUT64>
-__global__ __launch_bounds__(kBlock) void step_kernel(const Launch L) {
+#ifndef MG_STEP_WAVES_PER_EU
+#define MG_STEP_WAVES_PER_EU 1  // step kernel: minimum waves per SIMD the register budget must allow
+#endif
+__global__ __launch_bounds__(kBlock, MG_STEP_WAVES_PER_EU) void step_kernel(const Launch L) {
   __shared__ __attribute__((aligned(16))) float obs_tile[kBlock * kObs];
 
   const mg_params& P = L.P;
