@@ -52,10 +52,14 @@ def parse():
                     help="time every k-th launch with dispatch-recorded events (arming costs host time)")
     ap.add_argument("--rollout-steps", type=int, default=16,
                     help="T of the fused rollout leg (mg_rollout_random); 0 disables it")
-    ap.add_argument("--rollout-launches", type=int, default=60)
+    ap.add_argument("--rollout-launches", type=int, default=200,
+                    help="timed launches of the rollout leg (after --leg-warmup untimed ones)")
+    ap.add_argument("--leg-warmup", type=int, default=10,
+                    help="untimed launches before each rollout / Q-net leg: a compute-heavy kernel after the "
+                         "memory-bound step leg first runs through a clock transient (tools/rollout_sustain.py)")
     ap.add_argument("--replay-stores", type=int, default=20,
                     help="timed mg_replay_store calls of the replay-memory leg; 0 disables it")
-    ap.add_argument("--qnet-launches", type=int, default=20,
+    ap.add_argument("--qnet-launches", type=int, default=40,
                     help="launches of the config-5 leg (fused epsilon-greedy DQN rollout); 0 disables it")
     return ap.parse_args()
 
@@ -107,7 +111,7 @@ def rollout_leg(env, args, world, dist, torch):
     52 (obs 40 + rew 8 + done 1 + coll 1 + actions 2) + 100 / T (state in and out)."""
     T, L, E = args.rollout_steps, args.rollout_launches, env.num_envs
     k = 10_000_000
-    for _ in range(3):
+    for _ in range(max(1, args.leg_warmup)):
         env.rollout_random(T, args.seed, first_step=k, final_observation=False, won_mask=False)
         k += T
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -155,7 +159,7 @@ def qnet_leg(env, args, world, dist, torch, opponent):
                                 device=env.device)
     T, L, E = args.rollout_steps, args.qnet_launches, env.num_envs
     k = 20_000_000
-    for _ in range(2):
+    for _ in range(max(1, args.leg_warmup)):
         env.rollout_qnet(T, qnet, args.seed, opponent=opponent, first_step=k, final_observation=False,
                          won_mask=False)
         k += T
