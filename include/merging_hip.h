@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 4
+#define MG_ABI_VERSION 5
 #define MG_OBS_DIM 10   /* merging_env.py:75 observation_shape = (10) */
 #define MG_NUM_ACTIONS 5 /* merging_env.py:101-102 action_dict / Discrete(5) */
 #define MG_ACTION_NONE (-1) /* action2=None: the constant-speed "L0" opponent, merging_env.py:152 */
@@ -157,7 +157,11 @@ typedef struct mg_traj {
  * trajectory buffers of a rollout, or one step's outputs with T = 1). Transition (t, i) is
  *   s  = obs_first[i] (t = 0) or obs[t-1, i],   a = a1[t, i],   r = rew[t, i, 0] (the ego's),
  *   s' = final_obs[t, i] where done[t, i] (autoreset put the reset observation in obs), else obs[t, i]
- * -- exactly what the reference's loop hands store_transition (main.py:195-211). */
+ * -- exactly what the reference's loop hands store_transition (main.py:195-211).
+ * Goal-augmented rows (hdqn.py's lower-level memory, :158 np.zeros((MEMORY_CAPACITY,
+ * (NUM_STATES + 1) * 2 + 2)), :180-184, fed at :291-316 with goal_state = [goal] + state):
+ * with goal != NULL a row is 24 floats [goal, s(10), a, r, next_goal, s'(10)]; reward != NULL
+ * replaces rew[t, i, 0] (hdqn's intrinsic reward, :314). */
 typedef struct mg_transitions {
   const float* obs_first;   /* [n, 10] observation before step 0 */
   const float* obs;         /* [T, n, 10] */
@@ -166,6 +170,9 @@ typedef struct mg_transitions {
   const float* rew;         /* [T, n, 2] */
   const uint8_t* done;      /* [T, n] or NULL (never done) */
   const uint64_t* won_mask; /* [T, ceil(n/64)] or NULL (nobody has won) */
+  const float* goal;        /* [T, n] goal column of s, or NULL (22-float rows) */
+  const float* next_goal;   /* [T, n] goal column of s' (required with goal) */
+  const float* reward;      /* [T, n] r of the row, or NULL (r = rew[t, i, 0]) */
 } mg_transitions;
 
 /* Completed-episode statistics, updated only when an env finishes (MG_AUTORESET). */
@@ -242,8 +249,10 @@ int mg_rollout_qnet(const mg_params* params, const mg_state* state, const mg_tra
                     uint64_t opp_greedy_threshold, uint32_t flags, void* stream);
 
 /* ---- replay memory (scripts/main.py:91-92, :115-119, :130-135) --------------------------------
- * rows: [capacity, 22] fp32 device buffer, row = [s(10), a, r, s'(10)] like np.hstack((state,
- * [action, reward], next_state)); counter: one device uint64, the reference's memory_counter.
+ * rows: [capacity, row_floats] fp32 device buffer, row = [s(10), a, r, s'(10)] like
+ * np.hstack((state, [action, reward], next_state)) (row_floats 22), or the goal-augmented
+ * [goal, s(10), a, r, next_goal, s'(10)] of hdqn.py's lower memory (row_floats 24, tr->goal set);
+ * counter: one device uint64, the reference's memory_counter.
  * mg_replay_store appends the transitions of *tr in (t, i) order -- the order in which
  * stepping env 0..n-1 at each step and calling store_transition would append them -- at
  * slot (memory_counter + k) % capacity, skipping those whose won bit is set when
@@ -253,17 +262,17 @@ int mg_rollout_qnet(const mg_params* params, const mg_state* state, const mg_tra
  * buffer of at least mg_replay_scratch_bytes(n, num_steps) bytes, 8-byte aligned, any contents;
  * one scratch buffer per stream. Three launches, stream-ordered, no host synchronisation. */
 size_t mg_replay_scratch_bytes(int64_t n, int32_t num_steps);
-int mg_replay_store(float* rows, uint64_t* counter, int64_t capacity, const mg_transitions* tr,
-                    int64_t n, int32_t num_steps, int32_t skip_ego_won, void* scratch,
-                    size_t scratch_bytes, void* stream);
+int mg_replay_store(float* rows, uint64_t* counter, int64_t capacity, int32_t row_floats,
+                    const mg_transitions* tr, int64_t n, int32_t num_steps, int32_t skip_ego_won,
+                    void* scratch, size_t scratch_bytes, void* stream);
 
-/* out[batch, 22] = rows[idx[b]], idx[b] = floor(u0 * M / 2^32) with u = Philox4x32-10(key = seed,
+/* out[batch, row_floats] = rows[idx[b]], idx[b] = floor(u0 * M / 2^32) with u = Philox4x32-10(key = seed,
  * counter = (b, draw)) and M = capacity (np.random.choice(MEMORY_CAPACITY, BATCH_SIZE),
  * main.py:130 -- the reference learns only once the memory is full) or, when filled_only != 0,
  * M = min(*counter, capacity) (at least 1). idx_out[batch] (int64, may be NULL) gets the slots. */
-int mg_replay_sample(const float* rows, const uint64_t* counter, int64_t capacity, uint64_t seed,
-                     uint64_t draw, int32_t filled_only, float* out, int64_t* idx_out,
-                     int64_t batch, void* stream);
+int mg_replay_sample(const float* rows, const uint64_t* counter, int64_t capacity,
+                     int32_t row_floats, uint64_t seed, uint64_t draw, int32_t filled_only,
+                     float* out, int64_t* idx_out, int64_t batch, void* stream);
 
 /* Resets the envs whose mask byte is non-zero (mask == NULL: all n) and writes their reset
  * observation to out->obs / out->rec64 when given. Replaces MergeEnv.reset (merging_env.py:208-230). */

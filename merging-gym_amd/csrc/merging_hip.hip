@@ -1651,7 +1651,10 @@ __global__ __launch_bounds__(kBlock) void observe_kernel(const mg_params P, cons
 //                             observation kept in registers as the next transition's s; rows
 //                             gathered in LDS in ring order and written as contiguous 8-byte
 //                             stores (a row is 88 B: 16-byte alignment alternates).
-constexpr int kRow = 2 * kObs + 2;  // 22 floats: s(10), a, r, s'(10)
+// Rows are kRow floats [s(10), a, r, s'(10)], or kRowGoal [goal, s(10), a, r, next_goal, s'(10)]
+// for hdqn.py's lower-level memory (:158, :180-184; goal_state = [goal] + state at :291, :304).
+constexpr int kRow = 2 * kObs + 2;       // 22
+constexpr int kRowGoal = 2 * kObs + 4;   // 24
 constexpr int kRBlock = 256;        // envs per write block
 constexpr int kRGroup = 64;         // write blocks per scan wave
 
@@ -1784,9 +1787,13 @@ __device__ __forceinline__ void load_row10(const float* src, float (&v)[kObs]) {
   }
 }
 
+template <bool GOAL>
 __global__ __launch_bounds__(kRBlock) void replay_write_kernel(const ReplayIn R, const ReplayScratch S,
                                                                const uint64_t* counter, float* rows,
                                                                int64_t cap) {
+  constexpr int kRow = GOAL ? kRowGoal : 2 * kObs + 2;  // floats per row
+  constexpr int kS = GOAL ? 1 : 0;                      // column of s[0]
+  constexpr int kS2 = kS + kObs + 2 + kS;               // column of s'[0]
   __shared__ __attribute__((aligned(16))) float tile[kRBlock * kRow];
   __shared__ int wave_cnt[kRBlock / 64];
   const int64_t bx = blockIdx.x;
@@ -1830,11 +1837,15 @@ __global__ __launch_bounds__(kRBlock) void replay_write_kernel(const ReplayIn R,
           for (int k = 0; k < kObs; ++k) s2[k] = o[k];
 #pragma unroll
         for (int k = 0; k < kObs; ++k) {
-          d[k] = s[k];
-          d[kObs + 2 + k] = s2[k];
+          d[kS + k] = s[k];
+          d[kS2 + k] = s2[k];
         }
-        d[kObs] = static_cast<float>(R.X.a1[row]);
-        d[kObs + 1] = R.X.rew[2 * row];
+        d[kS + kObs] = static_cast<float>(R.X.a1[row]);
+        d[kS + kObs + 1] = R.X.reward ? R.X.reward[row] : R.X.rew[2 * row];
+        if constexpr (GOAL) {
+          d[0] = R.X.goal[row];
+          d[kS2 - 1] = R.X.next_goal[row];
+        }
       }
       __syncthreads();
       const int skip = base >= first ? 0 : static_cast<int>(min<uint64_t>(first - base, total));
@@ -1887,7 +1898,7 @@ __global__ __launch_bounds__(kRBlock) void replay_write_kernel(const ReplayIn R,
 
 __global__ __launch_bounds__(kBlock) void replay_sample_kernel(const float* rows,
                                                                const uint64_t* counter, int64_t cap,
-                                                               uint64_t seed, uint64_t draw,
+                                                               int row_floats, uint64_t seed, uint64_t draw,
                                                                int32_t filled_only, float* out,
                                                                int64_t* idx_out, int64_t batch) {
   const int64_t b = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
@@ -1904,10 +1915,9 @@ __global__ __launch_bounds__(kBlock) void replay_sample_kernel(const float* rows
       static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32));
   const uint64_t idx = (static_cast<uint64_t>(u.x) * m) >> 32;
   if (idx_out) idx_out[b] = static_cast<int64_t>(idx);
-  const f32x2* src = reinterpret_cast<const f32x2*>(rows + idx * kRow);
-  f32x2* dst = reinterpret_cast<f32x2*>(out + b * kRow);
-#pragma unroll
-  for (int k = 0; k < kRow / 2; ++k) dst[k] = src[k];
+  const f32x2* src = reinterpret_cast<const f32x2*>(rows + idx * row_floats);
+  f32x2* dst = reinterpret_cast<f32x2*>(out + b * row_floats);
+  for (int k = 0; k < row_floats / 2; ++k) dst[k] = src[k];
 }
 
 thread_local char g_err[512] = "";
@@ -2193,11 +2203,14 @@ size_t mg_replay_scratch_bytes(int64_t n, int32_t num_steps) {
   return static_cast<size_t>((8 + ng * 8 + nb * 4 + ng * 4 + 7) & ~int64_t{7});
 }
 
-int mg_replay_store(float* rows, uint64_t* counter, int64_t capacity, const mg_transitions* tr,
-                    int64_t n, int32_t num_steps, int32_t skip_ego_won, void* scratch,
-                    size_t scratch_bytes, void* stream) {
+int mg_replay_store(float* rows, uint64_t* counter, int64_t capacity, int32_t row_floats,
+                    const mg_transitions* tr, int64_t n, int32_t num_steps, int32_t skip_ego_won,
+                    void* scratch, size_t scratch_bytes, void* stream) {
   if (!rows || !counter || !tr) return fail(hipErrorInvalidValue, "%s", "mg_replay_store: NULL pointer");
   if (capacity < 1) return fail(hipErrorInvalidValue, "%s", "mg_replay_store: capacity < 1");
+  if (row_floats != (tr->goal ? kRowGoal : kRow) || (tr->goal != nullptr) != (tr->next_goal != nullptr))
+    return fail(hipErrorInvalidValue, "%s",
+                "mg_replay_store: row_floats must be 22, or 24 with both goal and next_goal set");
   if (n < 0 || num_steps < 0) return fail(hipErrorInvalidValue, "%s", "mg_replay_store: n < 0 or num_steps < 0");
   if (n == 0 || num_steps == 0) return 0;
   if (!tr->obs_first || !tr->obs || !tr->a1 || !tr->rew)
@@ -2206,6 +2219,9 @@ int mg_replay_store(float* rows, uint64_t* counter, int64_t capacity, const mg_t
        reinterpret_cast<uintptr_t>(tr->obs) | reinterpret_cast<uintptr_t>(tr->final_obs) |
        reinterpret_cast<uintptr_t>(tr->rew) | reinterpret_cast<uintptr_t>(scratch)) & 7)
     return fail(hipErrorInvalidValue, "%s", "mg_replay_store: float buffers and scratch must be 8-byte aligned");
+  if ((reinterpret_cast<uintptr_t>(tr->goal) | reinterpret_cast<uintptr_t>(tr->next_goal) |
+       reinterpret_cast<uintptr_t>(tr->reward)) & 3)
+    return fail(hipErrorInvalidValue, "%s", "mg_replay_store: goal, next_goal and reward must be 4-byte aligned");
   const int64_t nbx = (n + kRBlock - 1) / kRBlock;
   const int64_t nb = nbx * num_steps;
   if (nbx > 0x7fffffff || replay_groups(nb) > 0x7fffffff)
@@ -2227,14 +2243,20 @@ int mg_replay_store(float* rows, uint64_t* counter, int64_t capacity, const mg_t
   hipLaunchKernelGGL(replay_scan_kernel, dim3(static_cast<unsigned>(replay_groups(nb))), dim3(64), 0, st,
                      R, S);
   hipLaunchKernelGGL(replay_group_scan_kernel, dim3(1), dim3(64), 0, st, S, replay_groups(nb), counter);
-  hipLaunchKernelGGL(replay_write_kernel, dim3(static_cast<unsigned>(nbx), chunks), dim3(kRBlock), 0, st, R,
-                     S, counter, rows, capacity);
+  if (tr->goal)
+    hipLaunchKernelGGL(replay_write_kernel<true>, dim3(static_cast<unsigned>(nbx), chunks), dim3(kRBlock), 0,
+                       st, R, S, counter, rows, capacity);
+  else
+    hipLaunchKernelGGL(replay_write_kernel<false>, dim3(static_cast<unsigned>(nbx), chunks), dim3(kRBlock), 0,
+                       st, R, S, counter, rows, capacity);
   return finish_launch("mg_replay_store");
 }
 
-int mg_replay_sample(const float* rows, const uint64_t* counter, int64_t capacity, uint64_t seed,
-                     uint64_t draw, int32_t filled_only, float* out, int64_t* idx_out,
-                     int64_t batch, void* stream) {
+int mg_replay_sample(const float* rows, const uint64_t* counter, int64_t capacity,
+                     int32_t row_floats, uint64_t seed, uint64_t draw, int32_t filled_only,
+                     float* out, int64_t* idx_out, int64_t batch, void* stream) {
+  if (row_floats != kRow && row_floats != kRowGoal)
+    return fail(hipErrorInvalidValue, "%s", "mg_replay_sample: row_floats must be 22 or 24");
   if (!rows || !out || (filled_only && !counter))
     return fail(hipErrorInvalidValue, "%s", "mg_replay_sample: NULL pointer");
   if (capacity < 1 || capacity > (int64_t{1} << 32) || batch < 0)
@@ -2244,7 +2266,7 @@ int mg_replay_sample(const float* rows, const uint64_t* counter, int64_t capacit
   if (batch == 0) return 0;
   const unsigned blocks = static_cast<unsigned>((batch + kBlock - 1) / kBlock);
   hipLaunchKernelGGL(replay_sample_kernel, dim3(blocks), dim3(kBlock), 0,
-                     static_cast<hipStream_t>(stream), rows, counter, capacity, seed, draw,
+                     static_cast<hipStream_t>(stream), rows, counter, capacity, row_floats, seed, draw,
                      filled_only, out, idx_out, batch);
   return finish_launch("mg_replay_sample");
 }

@@ -4,7 +4,10 @@ Device twin of the reference's memory (scripts/main.py:91-92 `np.zeros((MEMORY_C
 NUM_STATES * 2 + 2))`, :115-119 store_transition, :129-135 the minibatch draw in learn(); the
 same structure in scripts/hdqn.py:157-158, :180-184, :194-199). Rows are
 [s(10), a, r, s'(10)] fp32 -- the reference keeps fp64 rows and reads them back through
-torch.FloatTensor, so the values learn() sees are the same.
+torch.FloatTensor, so the values learn() sees are the same. `ReplayRing(cap, goal=True)` holds
+hdqn.py's lower-level rows [goal, s(10), a, r, next_goal, s'(10)] (goal_state = [goal] + state,
+:291 and :304; intrinsic reward :314): store() then takes the per-transition goals and the
+reward column.
 
 Transitions go in straight from a MergeVecEnv's trajectory buffers (one batched store per
 rollout, three kernel launches from libmerging_hip.so) instead of one store_transition call
@@ -26,11 +29,12 @@ import ctypes
 from . import _native
 
 _OBS_DIM = 10
-ROW = 2 * _OBS_DIM + 2
+ROW = 2 * _OBS_DIM + 2        # main.py:91: NUM_STATES * 2 + 2
+ROW_GOAL = 2 * _OBS_DIM + 4   # hdqn.py:158: (NUM_STATES + 1) * 2 + 2
 
 
 class ReplayRing:
-    def __init__(self, capacity: int = 2000, device=None):
+    def __init__(self, capacity: int = 2000, device=None, goal: bool = False):
         import torch
 
         if not torch.cuda.is_available():
@@ -39,10 +43,13 @@ class ReplayRing:
             raise ValueError("capacity must be >= 1")
         self._torch = torch
         self.capacity = int(capacity)
+        self.goal = bool(goal)
+        self.row = ROW_GOAL if self.goal else ROW
+        self._s0 = 1 if self.goal else 0  # column of s[0]
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
-        self.memory = torch.zeros((self.capacity, ROW), dtype=torch.float32, device=self.device)
+        self.memory = torch.zeros((self.capacity, self.row), dtype=torch.float32, device=self.device)
         self._counter = torch.zeros(1, dtype=torch.int64, device=self.device)
         self._scratch = torch.empty(0, dtype=torch.int64, device=self.device)
         self._sample_bufs = {}
@@ -73,13 +80,20 @@ class ReplayRing:
         return int(self._counter.item())
 
     def store(self, obs_first, obs, a1, rew, done=None, final_obs=None, won_mask=None,
-              skip_ego_won: bool = True):
+              skip_ego_won: bool = True, goal=None, next_goal=None, reward=None):
         """Append T steps of N envs ([T, N, ...] tensors; obs_first [N, 10] = observation
         before step 0). skip_ego_won drops the transitions whose won bit is set (main.py:209;
-        hdqn.py:316 stores all: pass False). Stream-ordered; nothing is synchronised."""
+        hdqn.py:316 stores all: pass False). A goal ring needs goal / next_goal [T, N] (the goal
+        columns of s and s'); reward [T, N] replaces the ego's env reward rew[..., 0] as the r
+        column (hdqn.py:314's intrinsic reward). Stream-ordered; nothing is synchronised."""
         torch = self._torch
+        if self.goal != (goal is not None) or (goal is None) != (next_goal is None):
+            raise ValueError("a goal ring takes goal and next_goal; a plain ring takes neither")
         a1 = torch.as_tensor(a1, device=self.device)
         if a1.dim() == 1:  # one step
+            goal = None if goal is None else torch.as_tensor(goal, device=self.device)[None]
+            next_goal = None if next_goal is None else torch.as_tensor(next_goal, device=self.device)[None]
+            reward = None if reward is None else torch.as_tensor(reward, device=self.device)[None]
             a1 = a1[None]
             obs = torch.as_tensor(obs, device=self.device)[None]
             rew = torch.as_tensor(rew, device=self.device)[None]
@@ -95,6 +109,10 @@ class ReplayRing:
         rew = self._f32(rew, (T, n, 2))
         if final_obs is not None:
             final_obs = self._f32(final_obs, (T, n, _OBS_DIM))
+        if goal is not None:
+            goal, next_goal = self._f32(goal, (T, n)), self._f32(next_goal, (T, n))
+        if reward is not None:
+            reward = self._f32(reward, (T, n))
         if done is not None:
             done = torch.as_tensor(done, device=self.device)
             if done.dtype == torch.bool:
@@ -111,15 +129,17 @@ class ReplayRing:
                              "with won_mask=True / MergeVecEnv(won_mask=True), or pass skip_ego_won=False")
         ptr = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
         tr = _native.Transitions(ptr(obs_first), ptr(obs), ptr(final_obs), ptr(a1), ptr(rew),
-                                 ptr(done), ptr(won_mask) if skip_ego_won else None)
+                                 ptr(done), ptr(won_mask) if skip_ego_won else None, ptr(goal),
+                                 ptr(next_goal), ptr(reward))
         scratch = self._scratch_for(n, T)
         rc = _native.lib.mg_replay_store(
-            self.memory.data_ptr(), self._counter.data_ptr(), self.capacity, ctypes.byref(tr), n, T,
-            1 if skip_ego_won else 0, scratch.data_ptr(), scratch.numel() * 8, self._stream())
+            self.memory.data_ptr(), self._counter.data_ptr(), self.capacity, self.row, ctypes.byref(tr), n,
+            T, 1 if skip_ego_won else 0, scratch.data_ptr(), scratch.numel() * 8, self._stream())
         _native.check(rc, "mg_replay_store")
-        self._keepalive = (obs_first, obs, a1, rew, done, final_obs, won_mask)
+        self._keepalive = (obs_first, obs, a1, rew, done, final_obs, won_mask, goal, next_goal, reward)
 
-    def store_rollout(self, obs_first, traj, skip_ego_won: bool = True):
+    def store_rollout(self, obs_first, traj, skip_ego_won: bool = True, goal=None, next_goal=None,
+                      reward=None):
         """Append a MergeVecEnv rollout (the dict rollout_random / rollout_qnet return). With
         autoreset the obs row of a finished env is already the reset observation, so the
         terminal one must come from final_observation (roll out with final_observation=True)."""
@@ -127,11 +147,24 @@ class ReplayRing:
             raise ValueError("the rollout has no final_observation: episode ends would store the "
                              "reset observation as next_state; roll out with final_observation=True")
         self.store(obs_first, traj["obs"], traj["a1"], traj["rew"], traj["done"],
-                   traj["final_observation"], traj.get("won_mask"), skip_ego_won)
+                   traj["final_observation"], traj.get("won_mask"), skip_ego_won, goal, next_goal, reward)
 
     def store_transition(self, state, action, reward, next_state):
-        """The reference's single-transition call (main.py:115-119), through the same kernels."""
+        """The reference's single-transition call (main.py:115-119; hdqn.py:180-184 for a goal
+        ring, where state / next_state are the 11-value goal states [goal] + state), through the
+        same kernels."""
         torch = self._torch
+        if self.goal:
+            gs, gs2 = [float(x) for x in state], [float(x) for x in next_state]
+            s = torch.as_tensor([gs[1:]], dtype=torch.float32)
+            s2 = torch.as_tensor([[gs2[1:]]], dtype=torch.float32)
+            a = torch.as_tensor([[int(action)]], dtype=torch.int8)
+            r = torch.as_tensor([[[float(reward), 0.0]]], dtype=torch.float32)
+            g = torch.as_tensor([[gs[0]]], dtype=torch.float32)
+            g2 = torch.as_tensor([[gs2[0]]], dtype=torch.float32)
+            self.store(s.to(self.device), s2.to(self.device), a.to(self.device), r.to(self.device),
+                       skip_ego_won=False, goal=g.to(self.device), next_goal=g2.to(self.device))
+            return
         s = torch.as_tensor([list(map(float, state))], dtype=torch.float32)
         s2 = torch.as_tensor([[list(map(float, next_state))]], dtype=torch.float32)
         a = torch.as_tensor([[int(action)]], dtype=torch.int8)
@@ -142,19 +175,19 @@ class ReplayRing:
     # ------------------------------------------------------------------ sampling
     def sample_rows(self, batch_size: int = 128, seed: int = 0, draw: int = 0,
                     filled_only: bool = False, return_index: bool = False):
-        """[B, 22] rows at Philox-drawn slots: np.random.choice(MEMORY_CAPACITY, BATCH_SIZE)
+        """[B, 22] (goal ring: [B, 24]) rows at Philox-drawn slots: np.random.choice(MEMORY_CAPACITY, BATCH_SIZE)
         (main.py:130-131); filled_only draws from the stored rows only. The returned tensor is
         reused by the next call with the same batch size."""
         torch = self._torch
         B = int(batch_size)
         buf = self._sample_bufs.get(B)
         if buf is None:
-            buf = (torch.empty((B, ROW), dtype=torch.float32, device=self.device),
+            buf = (torch.empty((B, self.row), dtype=torch.float32, device=self.device),
                    torch.empty(B, dtype=torch.int64, device=self.device))
             self._sample_bufs[B] = buf
         rows, idx = buf
         rc = _native.lib.mg_replay_sample(
-            self.memory.data_ptr(), self._counter.data_ptr(), self.capacity, seed & 0xFFFFFFFFFFFFFFFF,
+            self.memory.data_ptr(), self._counter.data_ptr(), self.capacity, self.row, seed & 0xFFFFFFFFFFFFFFFF,
             draw & 0xFFFFFFFFFFFFFFFF, 1 if filled_only else 0, rows.data_ptr(), idx.data_ptr(), B,
             self._stream())
         _native.check(rc, "mg_replay_sample")
@@ -162,7 +195,8 @@ class ReplayRing:
 
     def sample(self, batch_size: int = 128, seed: int = 0, draw: int = 0, filled_only: bool = False):
         """(batch_state [B,10] f32, batch_action [B,1] int64, batch_reward [B,1] f32,
-        batch_next_state [B,10] f32) -- the slices of main.py:131-135."""
+        batch_next_state [B,10] f32) -- the slices of main.py:131-135; for a goal ring the
+        states are the 11-value goal states, as hdqn.py:196-199 slices them."""
         rows = self.sample_rows(batch_size, seed, draw, filled_only)
-        return (rows[:, :_OBS_DIM], rows[:, _OBS_DIM:_OBS_DIM + 1].to(self._torch.int64),
-                rows[:, _OBS_DIM + 1:_OBS_DIM + 2], rows[:, -_OBS_DIM:])
+        k = _OBS_DIM + self._s0  # state width
+        return (rows[:, :k], rows[:, k:k + 1].to(self._torch.int64), rows[:, k + 1:k + 2], rows[:, -k:])

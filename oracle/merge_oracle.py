@@ -360,14 +360,18 @@ def step_with_won(coracle, envs, a1, a2=None):
 
 
 def replay_store(memory, counter, obs_first, obs, a1, rew, done=None, final_obs=None, won=None,
-                 skip_ego_won=True):
+                 skip_ego_won=True, goal=None, next_goal=None, reward=None):
     """DQN.store_transition (scripts/main.py:115-119) applied to T steps of n envs in (t, i)
     order -- the order of stepping envs 0..n-1 each step and storing in turn -- with main.py:209's
     `if env.winner is not 1` filter. Row = np.hstack((s, [a, r], s')) with s the observation
     before the step, r the ego's reward, s' the terminal observation where done. Rows are
     float32 (the reference's float64 memory is read back through torch.FloatTensor, main.py:131-135).
     Vectorised; only the newest len(memory) transitions are written, as sequential stores leave
-    them. Returns the new memory_counter."""
+    them. Returns the new memory_counter.
+
+    goal / next_goal [T, n]: hdqn.py's lower-level rows (HDQN.store_transition :180-184 on
+    goal_state = [goal] + state, :291 and :304): [goal, s, a, r, next_goal, s'], 24 floats.
+    reward [T, n] replaces the ego's env reward as r (hdqn.py:314's intrinsic reward)."""
     a1 = np.asarray(a1)
     T, n = a1.shape
     cap = memory.shape[0]
@@ -380,8 +384,16 @@ def replay_store(memory, counter, obs_first, obs, a1, rew, done=None, final_obs=
     keep = np.ones((T, n), bool)
     if skip_ego_won and won is not None:
         keep = ~np.asarray(won, bool).reshape(T, n)
-    rows = np.concatenate([prev, a1[..., None].astype(np.float32),
-                           np.asarray(rew, np.float32).reshape(T, n, 2)[..., :1], nxt], axis=2)[keep]
+    r = (np.asarray(rew, np.float32).reshape(T, n, 2)[..., :1] if reward is None
+         else np.asarray(reward, np.float32).reshape(T, n, 1))
+    a = a1[..., None].astype(np.float32)
+    if goal is None:
+        cols = [prev, a, r, nxt]
+    else:  # hdqn.py:180-184 on goal_state = [goal] + state (:291, :304)
+        g = np.asarray(goal, np.float32).reshape(T, n, 1)
+        g2 = np.asarray(next_goal, np.float32).reshape(T, n, 1)
+        cols = [g, prev, a, r, g2, nxt]
+    rows = np.concatenate(cols, axis=2)[keep]
     k = len(rows)
     last = rows[max(0, k - cap):]
     slots = (counter + np.arange(max(0, k - cap), k)) % cap

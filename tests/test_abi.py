@@ -40,7 +40,7 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_native.State) == 7 * 8
     assert ctypes.sizeof(_native.Outputs) == 9 * 8
     assert ctypes.sizeof(_native.Traj) == 8 * 8
-    assert ctypes.sizeof(_native.Transitions) == 7 * 8
+    assert ctypes.sizeof(_native.Transitions) == 10 * 8
     assert ctypes.sizeof(_native.Stats) == 2 * 8
     assert _native.REC64_DTYPE.itemsize == 168
 
@@ -72,16 +72,24 @@ def test_argument_errors_without_gpu():
     assert rc != 0
     # replay: missing buffers, bad capacity and short scratch are refused before any launch
     tr = _native.Transitions()
-    rc = _native.lib.mg_replay_store(None, None, 16, ctypes.byref(tr), 4, 1, 0, None, 0, None)
+    rc = _native.lib.mg_replay_store(None, None, 16, 22, ctypes.byref(tr), 4, 1, 0, None, 0, None)
     assert rc != 0 and b"NULL" in _native.lib.mg_last_error()
     fake = ctypes.c_void_p(1 << 20)  # never dereferenced: validation fails first
-    rc = _native.lib.mg_replay_store(fake, fake, 0, ctypes.byref(tr), 4, 1, 0, None, 0, None)
+    rc = _native.lib.mg_replay_store(fake, fake, 0, 22, ctypes.byref(tr), 4, 1, 0, None, 0, None)
     assert rc != 0 and b"capacity" in _native.lib.mg_last_error()
     tr = _native.Transitions(fake, fake, None, fake, fake, None, None)
-    rc = _native.lib.mg_replay_store(fake, fake, 16, ctypes.byref(tr), 4, 1, 0, fake, 8, None)
+    rc = _native.lib.mg_replay_store(fake, fake, 16, 22, ctypes.byref(tr), 4, 1, 0, fake, 8, None)
     assert rc != 0 and b"scratch" in _native.lib.mg_last_error()
-    rc = _native.lib.mg_replay_sample(fake, fake, 0, 0, 0, 0, fake, None, 4, None)
+    rc = _native.lib.mg_replay_sample(fake, fake, 0, 22, 0, 0, 0, fake, None, 4, None)
     assert rc != 0 and b"capacity" in _native.lib.mg_last_error()
+    # row width must match the goal columns (hdqn.py:158's 24-float rows need goal + next_goal)
+    rc = _native.lib.mg_replay_store(fake, fake, 16, 24, ctypes.byref(tr), 4, 1, 0, fake, 1 << 20, None)
+    assert rc != 0 and b"row_floats" in _native.lib.mg_last_error()
+    trg = _native.Transitions(fake, fake, None, fake, fake, None, None, fake, None, None)
+    rc = _native.lib.mg_replay_store(fake, fake, 16, 24, ctypes.byref(trg), 4, 1, 0, fake, 1 << 20, None)
+    assert rc != 0 and b"row_floats" in _native.lib.mg_last_error()
+    rc = _native.lib.mg_replay_sample(fake, fake, 16, 23, 0, 0, 0, fake, None, 4, None)
+    assert rc != 0 and b"row_floats" in _native.lib.mg_last_error()
     # 65536 write blocks in 1024 scan groups: ticket (8) + bases u64 + offsets u32 + totals u32
     assert _native.lib.mg_replay_scratch_bytes(1 << 20, 16) == 8 + 1024 * 8 + 65536 * 4 + 1024 * 4
     assert _native.lib.mg_replay_scratch_bytes(0, 4) == 0
@@ -106,8 +114,8 @@ def test_empty_batches_are_no_ops_without_gpu():
     assert lib.mg_observe(P, ctypes.byref(st), out, 0, None) == 0
     assert lib.mg_qnet_forward(fake, fake, 0, fake, 0, None) == 0
     tr = _native.Transitions(fake, fake, None, fake, fake, None, None)
-    assert lib.mg_replay_store(fake, fake, 16, ctypes.byref(tr), 0, 4, 1, None, 0, None) == 0
-    assert lib.mg_replay_sample(fake, fake, 16, 0, 0, 0, fake, None, 0, None) == 0
+    assert lib.mg_replay_store(fake, fake, 16, 22, ctypes.byref(tr), 0, 4, 1, None, 0, None) == 0
+    assert lib.mg_replay_sample(fake, fake, 16, 22, 0, 0, 0, fake, None, 0, None) == 0
 
 
 def test_timeout_step_is_2501():

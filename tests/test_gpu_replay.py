@@ -164,6 +164,69 @@ def test_sample_rows_are_memory_at_oracle_slots(torch, coracle, filled_only):
     assert r.shape == (128, 1) and s2.shape == (128, 10)
 
 
+def test_goal_ring_reference_run(torch):
+    """hdqn.py's lower-level memory: the reference run's goals, intrinsic rewards and actions
+    (tests/golden/replay_golden.npz, HL0 / HRR) through MergeVecEnv(1) + a goal ring, one store
+    per step: the ring equals the reference's [2000, 24] memory and counter."""
+    from merging_gym import MergeVecEnv, ReplayRing
+
+    g = np.load(os.path.join(ROOT, "tests", "golden", "replay_golden.npz"))
+    for tag in ("HL0", "HRR"):
+        a1, a2 = g[f"{tag}_a1"], g[f"{tag}_a2"]
+        dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+        goal, goal2, r_int = dev(g[f"{tag}_goal"][:, None]), dev(g[f"{tag}_next_goal"][:, None]), \
+            dev(g[f"{tag}_intrinsic"][:, None])
+        env = MergeVecEnv(1, device="cuda:0")
+        ring = ReplayRing(int(g[f"{tag}_capacity"]), device="cuda:0", goal=True)
+        prev = env.reset().clone()
+        a1_d, a2_d = dev(a1.astype(np.int8)), dev(a2.astype(np.int8))
+        for k in range(len(a1)):
+            obs, rew, done, info = env.step(a1_d[k:k + 1], a2_d[k:k + 1])
+            ring.store(prev, obs, a1_d[k:k + 1], rew, done, info["final_observation"], skip_ego_won=False,
+                       goal=goal[k], next_goal=goal2[k], reward=r_int[k])
+            prev = obs.clone()
+        assert ring.memory_counter == int(g[f"{tag}_counter"])
+        np.testing.assert_allclose(ring.memory.cpu().numpy(), g[f"{tag}_memory"].astype(np.float32), **OBS_TOL)
+
+
+@pytest.mark.parametrize("cap", [7, 20_000])
+def test_goal_rows_match_oracle(torch, coracle, cap):
+    """Goal rows [goal, s, a, r, next_goal, s'] (24 floats, hdqn.py:158) with a reward column
+    override, over stores of several shapes: bit-exact with the oracle; sampled rows are the
+    memory at the oracle's slots and slice into hdqn.py:196-199's 11-value goal states."""
+    from merging_gym import ReplayRing
+
+    rng = np.random.default_rng(cap)
+    ring = ReplayRing(cap, device="cuda:0", goal=True)
+    mem = np.zeros((cap, 24), np.float32)
+    c = 0
+    dev = lambda a: torch.from_numpy(a).cuda()  # noqa: E731
+    for n, T in ((3000, 7), (5, 1), (257, 33)):
+        obs0 = rng.standard_normal((n, 10)).astype(np.float32)
+        obs = rng.standard_normal((T, n, 10)).astype(np.float32)
+        fobs = rng.standard_normal((T, n, 10)).astype(np.float32)
+        a1 = rng.integers(0, 5, (T, n)).astype(np.int8)
+        rew = rng.standard_normal((T, n, 2)).astype(np.float32)
+        done = (rng.random((T, n)) < 0.1).astype(np.uint8)
+        goal = rng.integers(0, 3, (T, n)).astype(np.float32)
+        goal2 = rng.integers(0, 3, (T, n)).astype(np.float32)
+        r_int = (rng.random((T, n)) < 0.3).astype(np.float32)
+        ring.store(dev(obs0), dev(obs), dev(a1), dev(rew), dev(done), dev(fobs), skip_ego_won=False,
+                   goal=dev(goal), next_goal=dev(goal2), reward=dev(r_int))
+        c = mo.replay_store(mem, c, obs0, obs, a1, rew, done, fobs, None, skip_ego_won=False, goal=goal,
+                            next_goal=goal2, reward=r_int)
+        assert ring.memory_counter == c, (n, T)
+        np.testing.assert_array_equal(ring.memory.cpu().numpy(), mem, err_msg=str((n, T)))
+    rows, idx = ring.sample_rows(512, seed=3, draw=5, return_index=True)
+    exp_idx = mo.replay_sample_index(coracle, cap, c, 3, 5, 512)
+    np.testing.assert_array_equal(idx.cpu().numpy(), exp_idx)
+    np.testing.assert_array_equal(rows.cpu().numpy(), mem[exp_idx])
+    s, a, r, s2 = ring.sample(128, seed=3, draw=6)
+    assert s.shape == (128, 11) and a.shape == (128, 1) and r.shape == (128, 1) and s2.shape == (128, 11)
+    with pytest.raises(ValueError):  # a goal ring needs the goal columns
+        ring.store(dev(obs0), dev(obs), dev(a1), dev(rew), skip_ego_won=False)
+
+
 def test_mixed_size_stores_share_scratch(torch):
     """Stores of different shapes through one ring (the scratch buffer is reused across
     sizes); random won words, including bits past n that must be ignored; random done rows

@@ -49,6 +49,24 @@ def test_oracle_store_reproduces_reference_memory(coracle, replay_golden, tag):
     np.testing.assert_array_equal(mem, ref)
 
 
+@pytest.mark.parametrize("tag", ["HL0", "HRR"])
+def test_oracle_goal_store_reproduces_hdqn_memory(coracle, replay_golden, tag):
+    """hdqn.py's lower-level memory (HDQN.store_transition :180-184 on goal states [goal] + state,
+    intrinsic reward :314, every transition stored :316): the reference's own run, recorded by
+    gen_replay.run_hdqn, equals the oracle's goal rows bit for bit (the reference's rows are
+    torch.FloatTensor values, i.e. fp32)."""
+    g = {k[len(tag) + 1:]: replay_golden[k] for k in replay_golden.files if k.startswith(tag + "_")}
+    cap = int(g["capacity"])
+    obs0, obs, fobs, rew, done, won = _oracle_episode_run(coracle, g["a1"], g["a2"])
+    np.testing.assert_array_equal(done[:, 0].astype(bool), g["done"])
+    mem = np.zeros((cap, 24), np.float32)
+    counter = mo.replay_store(mem, 0, obs0, obs, g["a1"][:, None], rew, done, fobs, won, skip_ego_won=False,
+                              goal=g["goal"][:, None], next_goal=g["next_goal"][:, None],
+                              reward=g["intrinsic"][:, None])
+    assert counter == int(g["counter"]) == len(g["a1"]) > cap  # every step stored, the ring wrapped
+    np.testing.assert_array_equal(mem, g["memory"].astype(np.float32))
+
+
 def _literal_loop(cap, obs0, obs, a1, rew, done, fobs, won, skip):
     """main.py:115-119 line by line, envs stepped in index order at each step."""
     memory = np.zeros((cap, 22), np.float64)

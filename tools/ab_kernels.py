@@ -246,7 +246,7 @@ def main_replay(a):
         lib = ctypes.CDLL(p)
         lib.mg_replay_scratch_bytes.argtypes = [ctypes.c_int64, ctypes.c_int32]
         lib.mg_replay_scratch_bytes.restype = ctypes.c_size_t
-        lib.mg_replay_store.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+        lib.mg_replay_store.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
                                         ctypes.POINTER(nat.Transitions), ctypes.c_int64, ctypes.c_int32,
                                         ctypes.c_int32, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
         nbytes = lib.mg_replay_scratch_bytes(a.envs, a.T)
@@ -256,7 +256,7 @@ def main_replay(a):
 
     def store(b):
         lib, ring, ctr, scr, nbytes = b
-        rc = lib.mg_replay_store(ring.data_ptr(), ctr.data_ptr(), cap, ctypes.byref(tr), a.envs, a.T, 1,
+        rc = lib.mg_replay_store(ring.data_ptr(), ctr.data_ptr(), cap, 22, ctypes.byref(tr), a.envs, a.T, 1,
                                  scr.data_ptr(), nbytes, torch.cuda.current_stream().cuda_stream)
         assert rc == 0
 
