@@ -229,10 +229,12 @@ int mg_qnet_pack(const float* fc1_w, const float* fc1_b, const float* fc2_w, con
                  const float* out_w, const float* out_b, int32_t in_dim, int32_t out_dim,
                  void* packed, void* stream);
 
-/* q[n,8] fp32 = Net(obs[n,10]) with bf16 operands and fp32 accumulation (rows >= out_dim are
- * padding). swap_halves != 0 feeds the opponent's view obs[5:] + obs[:5] (main.py:199). */
-int mg_qnet_forward(const void* packed, const float* obs, int32_t swap_halves, float* q, int64_t n,
-                    void* stream);
+/* q[n,8] fp32 = Net(x[n,in_dim]) with bf16 operands and fp32 accumulation (rows >= out_dim are
+ * padding; in_dim is the net's, 1..16: 10 for main.py's Net on observations, 11 for hdqn.py's
+ * lower-level Net on goal states [goal] + state, :145, :291). swap_halves != 0 (in_dim 10 only)
+ * feeds the opponent's view x[5:] + x[:5] (main.py:199). */
+int mg_qnet_forward(const void* packed, const float* x, int32_t in_dim, int32_t swap_halves, float* q,
+                    int64_t n, void* stream);
 
 /* num_steps steps in ONE launch with the epsilon-greedy Q-net policy computed on the device:
  * for each env and step, Philox4x32-10 (key = seed, counter = (env_offset + i, first_step + t))

@@ -975,6 +975,21 @@ __device__ __forceinline__ bf16x8 qnet_input(const float* row, bool swap, int h)
   return __builtin_bit_cast(bf16x8, w);
 }
 
+// Layer-1 B fragment from a 16-float row (in_dim <= 16, zero padded): features 8h .. 8h+7.
+// The standalone forward takes any input width this way, e.g. hdqn.py's goal states
+// [goal] + state (11 values, :291) for its lower-level Net(NUM_STATES + 1, NUM_ACTIONS) (:145).
+__device__ __forceinline__ bf16x8 qnet_input_wide(const float* row16, int h) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  const f32x4 lo = reinterpret_cast<const f32x4*>(row16 + 8 * h)[0];
+  const f32x4 hi = reinterpret_cast<const f32x4*>(row16 + 8 * h)[1];
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 w = {__builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{lo[0], lo[1]}, bf16x2)),
+                   __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{lo[2], lo[3]}, bf16x2)),
+                   __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{hi[0], hi[1]}, bf16x2)),
+                   __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{hi[2], hi[3]}, bf16x2))};
+  return __builtin_bit_cast(bf16x8, w);
+}
+
 __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
@@ -1052,6 +1067,8 @@ __device__ __forceinline__ void qnet_to_lds(const uint8_t* net, uint8_t* lds) {
 // Q-values of this lane's env (rows 0..7) from the block's f32 observation tile in LDS.
 // row0 = tile row of this wave's lane 0. swap = the opponent's view state[5:] + state[:5]
 // (scripts/main.py:199, human_player.py:40-41). Every lane of the wave must call it.
+// WIDE: tile rows are 16 floats (qnet_input_wide) instead of the 10-float observations.
+template <bool WIDE = false>
 __device__ __forceinline__ void qnet_forward(const uint8_t* net, const float* tile, int row0,
                                              bool swap, float (&q)[8]) {
   const __bf16* W1_ = reinterpret_cast<const __bf16*>(net);
@@ -1074,8 +1091,10 @@ __device__ __forceinline__ void qnet_forward(const uint8_t* net, const float* ti
     const float* B1 = B1_ + z;
     const float* B2 = B2_ + z;
     const float* B3 = B3_ + z;
-    const bf16x8 xb0 = qnet_input(tile + (row0 + r) * kObs, swap, h);
-    const bf16x8 xb1 = qnet_input(tile + (row0 + 32 + r) * kObs, swap, h);
+    const bf16x8 xb0 = WIDE ? qnet_input_wide(tile + (row0 + r) * 16, h)
+                            : qnet_input(tile + (row0 + r) * kObs, swap, h);
+    const bf16x8 xb1 = WIDE ? qnet_input_wide(tile + (row0 + 32 + r) * 16, h)
+                            : qnet_input(tile + (row0 + 32 + r) * kObs, swap, h);
     f32x16 acc2a[4], acc2b[4];
     // each accumulator loads its bias from LDS itself: sharing one load costs 16 v_mov per tile
     const int zb = opaque_zero();
@@ -1276,20 +1295,24 @@ __device__ __forceinline__ int argmax_first(const float (&q)[8], int out_dim) {
   return best;
 }
 
-// Standalone forward for tests / evaluation: q[i][0..7] for obs[i][0..9].
-__global__ __launch_bounds__(kBlock) void qnet_forward_kernel(const uint8_t* net, const float* obs,
-                                                              int swap, float* qout, int64_t n) {
+// Standalone forward for tests / evaluation: q[i][0..7] for x[i][0..in_dim-1], staged in LDS as
+// 16-float rows (swap, in_dim 10 only: the features in the order state[5:] + state[:5]).
+__global__ __launch_bounds__(kBlock) void qnet_forward_kernel(const uint8_t* net, const float* x,
+                                                              int in_dim, int swap, float* qout,
+                                                              int64_t n) {
   __shared__ __attribute__((aligned(16))) uint8_t lds_net[kQNetBytes];
-  __shared__ __attribute__((aligned(16))) float tile[kBlock * kObs];
+  __shared__ __attribute__((aligned(16))) float tile[kBlock * 16];
   const int64_t base = static_cast<int64_t>(blockIdx.x) * kBlock;
   qnet_to_lds(net, lds_net);
-  for (int j = threadIdx.x; j < kBlock * kObs; j += kBlock) {
-    const int64_t g = base * kObs + j;
-    tile[j] = g < n * kObs ? obs[g] : 0.f;
+  for (int j = threadIdx.x; j < kBlock * 16; j += kBlock) {
+    const int64_t i = base + (j >> 4);
+    const int k = j & 15;
+    const int src = swap ? (k + kObs / 2) % kObs : k;
+    tile[j] = (i < n && k < in_dim) ? x[i * in_dim + src] : 0.f;
   }
   __syncthreads();
   float q[8];
-  qnet_forward(lds_net, tile, (threadIdx.x >> 6) * 64, swap != 0, q);
+  qnet_forward<true>(lds_net, tile, (threadIdx.x >> 6) * 64, false, q);
   const int64_t i = base + threadIdx.x;
   if (i < n) {
 #pragma unroll
@@ -2118,16 +2141,18 @@ int mg_qnet_pack(const float* fc1_w, const float* fc1_b, const float* fc2_w, con
   return finish_launch("mg_qnet_pack");
 }
 
-int mg_qnet_forward(const void* packed, const float* obs, int32_t swap_halves, float* q, int64_t n,
-                    void* stream) {
-  if (!packed || !obs || !q) return fail(hipErrorInvalidValue, "%s", "mg_qnet_forward: NULL pointer");
+int mg_qnet_forward(const void* packed, const float* x, int32_t in_dim, int32_t swap_halves, float* q,
+                    int64_t n, void* stream) {
+  if (!packed || !x || !q) return fail(hipErrorInvalidValue, "%s", "mg_qnet_forward: NULL pointer");
   if (n < 0) return fail(hipErrorInvalidValue, "%s", "n < 0");
+  if (in_dim < 1 || in_dim > 16 || (swap_halves && in_dim != kObs))
+    return fail(hipErrorInvalidValue, "%s", "mg_qnet_forward: need 1 <= in_dim <= 16 (swap_halves: in_dim 10)");
   if (reinterpret_cast<uintptr_t>(packed) & 15)
     return fail(hipErrorInvalidValue, "%s", "packed net must be 16-byte aligned");
   if (n == 0) return 0;
   const unsigned blocks = static_cast<unsigned>((n + kBlock - 1) / kBlock);
   hipLaunchKernelGGL(qnet_forward_kernel, dim3(blocks), dim3(kBlock), 0,
-                     static_cast<hipStream_t>(stream), static_cast<const uint8_t*>(packed), obs,
+                     static_cast<hipStream_t>(stream), static_cast<const uint8_t*>(packed), x, in_dim,
                      swap_halves, q, n);
   return finish_launch("mg_qnet_forward");
 }

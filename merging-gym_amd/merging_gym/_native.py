@@ -101,7 +101,7 @@ def _load():
                                       _c.c_uint64, _c.c_uint64, _c.c_int32, _c.c_int32, _c.c_uint32, _P]
     lib.mg_qnet_packed_bytes.restype = _c.c_size_t
     lib.mg_qnet_pack.argtypes = [_P] * 6 + [_c.c_int32, _c.c_int32, _P, _P]
-    lib.mg_qnet_forward.argtypes = [_P, _P, _c.c_int32, _P, _c.c_int64, _P]
+    lib.mg_qnet_forward.argtypes = [_P, _P, _c.c_int32, _c.c_int32, _P, _c.c_int64, _P]
     lib.mg_rollout_qnet.argtypes = [PP, SP, _c.POINTER(Traj), STP, _c.c_int64, _c.c_int64, _c.c_uint64,
                                     _c.c_uint64, _c.c_int32, _P, _c.c_int32, _c.c_uint64, _c.c_int32,
                                     _c.c_uint64, _c.c_uint32, _P]

@@ -243,6 +243,8 @@ class MergeVecEnv:
         torch, nat = self._torch, self._nat
         T, n = int(num_steps), self.num_envs
         mode = {"none": 0, "uniform": 1, "self": 2}[opponent]
+        if qnet.in_dim != _OBS_DIM:
+            raise ValueError("the fused rollout feeds the 10-value observation: the net needs in_dim 10")
         k0 = self._step_idx if first_step is None else int(first_step)
         buf = self._traj(T, final_observation, won_mask)
         rc = nat.lib.mg_rollout_qnet(

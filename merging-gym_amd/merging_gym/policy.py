@@ -48,15 +48,20 @@ class QNet:
                    sd["out.bias"], device=device)
 
     def forward(self, obs, swap_halves: bool = False):
-        """Q-values [N, out_dim] of obs [N, 10] (device tensor), computed by mg_qnet_forward."""
+        """Q-values [N, out_dim] of inputs [N, in_dim] (device tensor), computed by
+        mg_qnet_forward: observations for main.py's Net (in_dim 10; swap_halves feeds the
+        opponent's view, main.py:199), goal states [goal] + state for hdqn.py's lower-level Net
+        (in_dim 11, :145, :291), or any other width up to 16 (e.g. Goal_DQN's meta-net, 10 -> 3)."""
         import torch
 
-        if self.in_dim != 10:
-            raise ValueError("the fused forward takes the 10-value observation (in_dim 10)")
         obs = obs.to(self.device, torch.float32).contiguous()
+        if obs.dim() != 2 or obs.shape[1] != self.in_dim:
+            raise ValueError(f"expected inputs [N, {self.in_dim}], got {tuple(obs.shape)}")
+        if swap_halves and self.in_dim != 10:
+            raise ValueError("swap_halves is the opponent's view of a 10-value observation")
         q = torch.empty((obs.shape[0], 8), dtype=torch.float32, device=self.device)
         stream = torch.cuda.current_stream(self.device).cuda_stream
-        self._nat.check(self._nat.lib.mg_qnet_forward(self.packed.data_ptr(), obs.data_ptr(),
+        self._nat.check(self._nat.lib.mg_qnet_forward(self.packed.data_ptr(), obs.data_ptr(), self.in_dim,
                                                       1 if swap_halves else 0, q.data_ptr(),
                                                       obs.shape[0], stream), "mg_qnet_forward")
         return q[:, : self.out_dim]

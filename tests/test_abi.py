@@ -112,7 +112,8 @@ def test_empty_batches_are_no_ops_without_gpu():
                                None) == 0
     assert lib.mg_reset(P, ctypes.byref(st), None, out, 0, None) == 0
     assert lib.mg_observe(P, ctypes.byref(st), out, 0, None) == 0
-    assert lib.mg_qnet_forward(fake, fake, 0, fake, 0, None) == 0
+    assert lib.mg_qnet_forward(fake, fake, 10, 0, fake, 0, None) == 0
+    assert lib.mg_qnet_forward(fake, fake, 11, 1, fake, 4, None) != 0  # swap needs in_dim 10
     tr = _native.Transitions(fake, fake, None, fake, fake, None, None)
     assert lib.mg_replay_store(fake, fake, 16, 22, ctypes.byref(tr), 0, 4, 1, None, 0, None) == 0
     assert lib.mg_replay_sample(fake, fake, 16, 22, 0, 0, 0, fake, None, 0, None) == 0

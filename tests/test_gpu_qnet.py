@@ -80,6 +80,36 @@ def test_qnet_forward_matches_bf16_reference(torch, coracle, nets, key, swap):
         assert agree >= 0.999, agree
 
 
+@pytest.mark.parametrize("in_dim,out_dim", [(11, 5), (10, 3)])
+def test_qnet_forward_hdqn_nets(torch, coracle, in_dim, out_dim):
+    """hdqn.py's two nets: the lower-level Net(NUM_STATES + 1, NUM_ACTIONS) on goal states
+    [goal] + state (:145, :291) and Goal_DQN's meta-net Net(NUM_STATES, NUM_GOALS) (:63), with
+    hdqn.py:41-47's initialisation (every weight U(0, 1); torch's default bias init). No h-DQN
+    checkpoint ships with the reference, so the weights are seeded draws."""
+    from merging_gym.policy import QNet
+
+    rng = np.random.default_rng(in_dim * 10 + out_dim)
+    dims = [(200, in_dim), (100, 200), (out_dim, 100)]
+    sd = {}
+    for name, (o, i) in zip(("fc1", "fc2", "out"), dims):
+        sd[f"{name}.weight"] = rng.uniform(0, 1, (o, i)).astype(np.float32)
+        sd[f"{name}.bias"] = rng.uniform(-i ** -0.5, i ** -0.5, o).astype(np.float32)
+    obs = _obs_samples(coracle, n=2048, steps=120)
+    x = obs if in_dim == 10 else np.concatenate(
+        [rng.integers(0, 3, (len(obs), 1)).astype(np.float32), obs], axis=1)  # [goal] + state
+    qnet = QNet.from_state_dict(sd, device="cuda:0")
+    q = qnet.forward(torch.from_numpy(x).cuda()).cpu().numpy()
+    assert q.shape == (len(x), out_dim)
+    q_bf = mo.qnet_reference(sd, x, bf16=True)
+    scale = np.maximum(1.0, np.abs(q_bf).max(axis=1, keepdims=True))
+    err = np.abs(q - q_bf) / scale
+    assert np.median(err) < 1e-5 and err.max() < 1e-2, (np.median(err), err.max())
+    tie = _near_tie(q_bf)
+    assert (q.argmax(1) == q_bf.argmax(1))[~tie].all()
+    with pytest.raises(ValueError):  # the input width is the net's
+        qnet.forward(torch.zeros((4, in_dim + 1), device="cuda:0"))
+
+
 @pytest.mark.parametrize("opponent,n", [("none", 4096), ("uniform", 4096), ("self", 4096),
                                         ("none", 1000), ("self", 577)])
 def test_rollout_qnet_policy_and_transitions(torch, coracle, nets, opponent, n):
