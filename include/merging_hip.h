@@ -151,6 +151,9 @@ typedef struct mg_traj {
   int8_t* a2;       /* [T, n] (-1 = None) */
   float* final_obs; /* [T, n, 10] written only at rows whose env finished at that step */
   uint64_t* won_mask; /* [T, ceil(n/64)] as mg_outputs.won_mask, one bitmask per step */
+  uint8_t* flags;   /* [T, n, 4] = (a1, a2, done, coll) interleaved, 4-byte aligned, or NULL. When
+                       set, the four byte arrays above are ignored and each env-step's four bytes
+                       leave as one 32-bit store (separate byte arrays cost the rollout ~5 %) */
 } mg_traj;
 
 /* A batch of transitions for the replay memory, T steps of n envs in [T, n, ...] layout (the
@@ -166,13 +169,15 @@ typedef struct mg_transitions {
   const float* obs_first;   /* [n, 10] observation before step 0 */
   const float* obs;         /* [T, n, 10] */
   const float* final_obs;   /* [T, n, 10] or NULL (then s' = obs even where done) */
-  const int8_t* a1;         /* [T, n] */
+  const int8_t* a1;         /* [T, n] (or NULL with flags) */
   const float* rew;         /* [T, n, 2] */
-  const uint8_t* done;      /* [T, n] or NULL (never done) */
+  const uint8_t* done;      /* [T, n] or NULL (never done; ignored with flags) */
   const uint64_t* won_mask; /* [T, ceil(n/64)] or NULL (nobody has won) */
   const float* goal;        /* [T, n] goal column of s, or NULL (22-float rows) */
   const float* next_goal;   /* [T, n] goal column of s' (required with goal) */
   const float* reward;      /* [T, n] r of the row, or NULL (r = rew[t, i, 0]) */
+  const uint8_t* flags;     /* [T, n, 4] interleaved (a1, a2, done, coll) of mg_traj.flags, or NULL:
+                               then a1 = flags[4 row], done = flags[4 row + 2] */
 } mg_transitions;
 
 /* Completed-episode statistics, updated only when an env finishes (MG_AUTORESET). */

@@ -809,6 +809,22 @@ __global__ __launch_bounds__(kBlock, MG_STEP_WAVES_PER_EU) void step_kernel(cons
   }
 }
 
+// One env-step's four byte outputs of a trajectory (a1, a2, done, collision): a single 32-bit
+// store into the interleaved [T, n, 4] buffer when the caller gave one, else four byte stores.
+__device__ __forceinline__ void store_step_bytes(const mg_traj& T, int64_t row, int a1, int a2, bool done,
+                                                 bool coll) {
+  if (T.flags) {
+    st_out(reinterpret_cast<uint32_t*>(T.flags) + row,
+           static_cast<uint32_t>(a1 & 0xff) | (static_cast<uint32_t>(a2 & 0xff) << 8) |
+               (done ? 0x10000u : 0u) | (coll ? 0x1000000u : 0u));
+    return;
+  }
+  if (T.a1) st_out(T.a1 + row, static_cast<int8_t>(a1));
+  if (T.a2) st_out(T.a2 + row, static_cast<int8_t>(a2));
+  if (T.done) st_out(T.done + row, static_cast<uint8_t>(done ? 1 : 0));
+  if (T.coll) st_out(T.coll + row, static_cast<uint8_t>(coll ? 1 : 0));
+}
+
 struct Rollout {
   mg_params P;
   mg_state S;
@@ -853,18 +869,13 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(const Rollout R) {
       draw_actions(static_cast<uint64_t>(R.env_offset + i), R.first_step + t, R.seed, R.opp_random,
                    a1, a2, /*opaque_key=*/true);
       env_step(P, e, a1, a2, r);  // Philox actions are always valid
-#if !MG_ABL_NO_BYTES
-      if (R.T.a1) st_out(R.T.a1 + row, static_cast<int8_t>(a1));
-      if (R.T.a2) st_out(R.T.a2 + row, static_cast<int8_t>(a2));
-#endif
       if (R.T.rew)
         st_out(reinterpret_cast<f32x2*>(R.T.rew) + row,
                f32x2{static_cast<float>(r.r1), static_cast<float>(r.r2)});
 #if !MG_ABL_NO_BYTES
-      if (R.T.done) st_out(R.T.done + row, static_cast<uint8_t>(r.done ? 1 : 0));
-      if (R.T.coll) st_out(R.T.coll + row, static_cast<uint8_t>(r.coll ? 1 : 0));
-#else
-      if (a1 + a2 == 1234 && r.coll) R.T.done[0] = 1;
+      store_step_bytes(R.T, row, a1, a2, r.done, r.coll);
+#else  // timing ablation only: no byte outputs
+      if (a1 + a2 == 1234 && r.coll) R.T.rew[0] = 1.f;
 #endif
       won = e.winner == 1;
       if (autoreset && r.done)
@@ -1365,12 +1376,9 @@ __device__ __forceinline__ void qnet_policy_step(const QRollout& R, Env& e, Step
   if constexpr (OPP == 2)
     a2 = (static_cast<uint64_t>(u.z) < R.opp_greedy_thr) ? greedy2 : action_from_u32(u.w);
   env_step(R.P, e, a1, a2, r);
-  if (R.T.a1) st_out(R.T.a1 + row, static_cast<int8_t>(a1));
-  if (R.T.a2) st_out(R.T.a2 + row, static_cast<int8_t>(a2));
   if (R.T.rew)
     st_out(reinterpret_cast<f32x2*>(R.T.rew) + row, f32x2{static_cast<float>(r.r1), static_cast<float>(r.r2)});
-  if (R.T.done) st_out(R.T.done + row, static_cast<uint8_t>(r.done ? 1 : 0));
-  if (R.T.coll) st_out(R.T.coll + row, static_cast<uint8_t>(r.coll ? 1 : 0));
+  store_step_bytes(R.T, row, a1, a2, r.done, r.coll);
   won = e.winner == 1;
   if ((R.flags & MG_AUTORESET) && r.done)
     finish_episode(R.P, e, r, R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i);
@@ -1406,13 +1414,10 @@ __device__ __forceinline__ void qnet_policy_step_n(const QRollout& R, Env (&e)[N
     if (!live[j]) continue;
     const int64_t i = i0 + 64 * j;
     const int64_t row = static_cast<int64_t>(t) * R.n + i;
-    if (R.T.a1) st_out(R.T.a1 + row, static_cast<int8_t>(a1[j]));
-    if (R.T.a2) st_out(R.T.a2 + row, static_cast<int8_t>(a2[j]));
     if (R.T.rew)
       st_out(reinterpret_cast<f32x2*>(R.T.rew) + row,
              f32x2{static_cast<float>(r[j].r1), static_cast<float>(r[j].r2)});
-    if (R.T.done) st_out(R.T.done + row, static_cast<uint8_t>(r[j].done ? 1 : 0));
-    if (R.T.coll) st_out(R.T.coll + row, static_cast<uint8_t>(r[j].coll ? 1 : 0));
+    store_step_bytes(R.T, row, a1[j], a2[j], r[j].done, r[j].coll);
     won[j] = e[j].winner == 1;
     if ((R.flags & MG_AUTORESET) && r[j].done)
       finish_episode(R.P, e[j], r[j], R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i);
@@ -1851,7 +1856,7 @@ __global__ __launch_bounds__(kRBlock) void replay_write_kernel(const ReplayIn R,
       const uint64_t base = S.group_base[b / kRGroup] + S.local[b];
       if (keep) {
         float* d = tile + rank * kRow;
-        const bool done = R.X.done != nullptr && R.X.done[row] != 0;
+        const bool done = R.X.flags ? R.X.flags[4 * row + 2] != 0 : (R.X.done != nullptr && R.X.done[row] != 0);
         float s2[kObs];
         if (done && R.X.final_obs)
           load_row10(R.X.final_obs + row * kObs, s2);
@@ -1863,7 +1868,7 @@ __global__ __launch_bounds__(kRBlock) void replay_write_kernel(const ReplayIn R,
           d[kS + k] = s[k];
           d[kS2 + k] = s2[k];
         }
-        d[kS + kObs] = static_cast<float>(R.X.a1[row]);
+        d[kS + kObs] = static_cast<float>(R.X.flags ? static_cast<int8_t>(R.X.flags[4 * row]) : R.X.a1[row]);
         d[kS + kObs + 1] = R.X.reward ? R.X.reward[row] : R.X.rew[2 * row];
         if constexpr (GOAL) {
           d[0] = R.X.goal[row];
@@ -2105,8 +2110,9 @@ int mg_rollout_random(const mg_params* params, const mg_state* state, const mg_t
   if (num_steps < 0) return fail(hipErrorInvalidValue, "%s", "num_steps < 0");
   if ((traj->obs && (reinterpret_cast<uintptr_t>(traj->obs) & 15)) ||
       (traj->final_obs && (reinterpret_cast<uintptr_t>(traj->final_obs) & 7)) ||
-      (traj->rew && (reinterpret_cast<uintptr_t>(traj->rew) & 7)))
-    return fail(hipErrorInvalidValue, "%s", "traj.obs must be 16-byte, rew/final_obs 8-byte aligned");
+      (traj->rew && (reinterpret_cast<uintptr_t>(traj->rew) & 7)) ||
+      (reinterpret_cast<uintptr_t>(traj->flags) & 3))
+    return fail(hipErrorInvalidValue, "%s", "traj.obs must be 16-byte, rew/final_obs 8-byte, flags 4-byte aligned");
   if (n == 0 || num_steps == 0) return 0;
   Rollout R{};
   R.P = *params;
@@ -2173,8 +2179,9 @@ int mg_rollout_qnet(const mg_params* params, const mg_state* state, const mg_tra
     return fail(hipErrorInvalidValue, "%s", "opponent_mode must be 0 (None), 1 (uniform) or 2 (same net)");
   if ((traj->obs && (reinterpret_cast<uintptr_t>(traj->obs) & 15)) ||
       (traj->final_obs && (reinterpret_cast<uintptr_t>(traj->final_obs) & 7)) ||
-      (traj->rew && (reinterpret_cast<uintptr_t>(traj->rew) & 7)))
-    return fail(hipErrorInvalidValue, "%s", "traj.obs must be 16-byte, rew/final_obs 8-byte aligned");
+      (traj->rew && (reinterpret_cast<uintptr_t>(traj->rew) & 7)) ||
+      (reinterpret_cast<uintptr_t>(traj->flags) & 3))
+    return fail(hipErrorInvalidValue, "%s", "traj.obs must be 16-byte, rew/final_obs 8-byte, flags 4-byte aligned");
   if (n == 0 || num_steps == 0) return 0;
   QRollout R{};
   R.P = *params;
@@ -2238,8 +2245,8 @@ int mg_replay_store(float* rows, uint64_t* counter, int64_t capacity, int32_t ro
                 "mg_replay_store: row_floats must be 22, or 24 with both goal and next_goal set");
   if (n < 0 || num_steps < 0) return fail(hipErrorInvalidValue, "%s", "mg_replay_store: n < 0 or num_steps < 0");
   if (n == 0 || num_steps == 0) return 0;
-  if (!tr->obs_first || !tr->obs || !tr->a1 || !tr->rew)
-    return fail(hipErrorInvalidValue, "%s", "mg_replay_store: obs_first, obs, a1 and rew are required");
+  if (!tr->obs_first || !tr->obs || !(tr->a1 || tr->flags) || !tr->rew)
+    return fail(hipErrorInvalidValue, "%s", "mg_replay_store: obs_first, obs, a1 (or flags) and rew are required");
   if ((reinterpret_cast<uintptr_t>(rows) | reinterpret_cast<uintptr_t>(tr->obs_first) |
        reinterpret_cast<uintptr_t>(tr->obs) | reinterpret_cast<uintptr_t>(tr->final_obs) |
        reinterpret_cast<uintptr_t>(tr->rew) | reinterpret_cast<uintptr_t>(scratch)) & 7)

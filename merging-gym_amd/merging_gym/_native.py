@@ -54,12 +54,12 @@ class Outputs(_c.Structure):
 
 
 class Traj(_c.Structure):
-    _fields_ = [(n, _P) for n in ("obs", "rew", "done", "coll", "a1", "a2", "final_obs", "won_mask")]
+    _fields_ = [(n, _P) for n in ("obs", "rew", "done", "coll", "a1", "a2", "final_obs", "won_mask", "flags")]
 
 
 class Transitions(_c.Structure):
     _fields_ = [(n, _P) for n in ("obs_first", "obs", "final_obs", "a1", "rew", "done", "won_mask", "goal",
-                                  "next_goal", "reward")]
+                                  "next_goal", "reward", "flags")]
 
 
 class Stats(_c.Structure):

@@ -189,8 +189,9 @@ class MergeVecEnv:
         obs, rew, done (bool), collision (bool), a1, a2, final_observation (rows where done)
         and won_mask ([T, ceil(N/64)] int64, bit i of step t = env i's winner == 1 after that
         step -- ReplayRing.store_rollout's filter; None with won_mask=False, which saves a
-        ballot and a store per wave-step). The buffers are reused by the next rollout with the
-        same T and output choices."""
+        ballot and a store per wave-step). a1, a2, done and collision are strided views of one
+        [T, N, 4] uint8 buffer, returned as "flags" (one 32-bit store per env-step in the
+        kernel). The buffers are reused by the next rollout with the same T and output choices."""
         nat = self._nat
         T, n = int(num_steps), self.num_envs
         k0 = self._step_idx if first_step is None else int(first_step)
@@ -210,24 +211,24 @@ class MergeVecEnv:
         if (buf is None or buf["T"] != T or (buf["final_observation"] is None) == final_observation
                 or (buf["won_mask"] is None) == won_mask):
             dev = self.device
+            # a1, a2, done, collision interleaved per env-step (mg_traj.flags): one 32-bit store
+            # per env-step instead of four byte stores; the four outputs are strided views
+            flags = torch.empty((T, n, 4), dtype=torch.uint8, device=dev)
             buf = {"T": T,
                    "obs": torch.empty((T, n, _OBS_DIM), dtype=torch.float32, device=dev),
                    "rew": torch.empty((T, n, 2), dtype=torch.float32, device=dev),
-                   "done": torch.empty((T, n), dtype=torch.uint8, device=dev),
-                   "collision": torch.empty((T, n), dtype=torch.uint8, device=dev),
-                   "a1": torch.empty((T, n), dtype=torch.int8, device=dev),
-                   "a2": torch.empty((T, n), dtype=torch.int8, device=dev),
+                   "flags": flags,
                    "final_observation": (torch.full((T, n, _OBS_DIM), float("nan"), dtype=torch.float32,
                                                     device=dev) if final_observation else None),
                    "won_mask": (torch.zeros((T, (n + 63) // 64), dtype=torch.int64, device=dev)
                                 if won_mask else None)}
             ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
-            buf["_traj"] = nat.Traj(*(ptr(buf[k]) for k in ("obs", "rew", "done", "collision", "a1", "a2",
-                                                             "final_observation", "won_mask")))
-            buf["_result"] = {"obs": buf["obs"], "rew": buf["rew"], "done": buf["done"].view(torch.bool),
-                              "collision": buf["collision"].view(torch.bool), "a1": buf["a1"],
-                              "a2": buf["a2"], "final_observation": buf["final_observation"],
-                              "won_mask": buf["won_mask"]}
+            buf["_traj"] = nat.Traj(ptr(buf["obs"]), ptr(buf["rew"]), None, None, None, None,
+                                    ptr(buf["final_observation"]), ptr(buf["won_mask"]), ptr(flags))
+            buf["_result"] = {"obs": buf["obs"], "rew": buf["rew"], "done": flags[..., 2].view(torch.bool),
+                              "collision": flags[..., 3].view(torch.bool), "a1": flags[..., 0].view(torch.int8),
+                              "a2": flags[..., 1].view(torch.int8), "final_observation": buf["final_observation"],
+                              "won_mask": buf["won_mask"], "flags": flags}
             self._traj_bufs = buf
         return buf
 

@@ -80,12 +80,14 @@ class ReplayRing:
         return int(self._counter.item())
 
     def store(self, obs_first, obs, a1, rew, done=None, final_obs=None, won_mask=None,
-              skip_ego_won: bool = True, goal=None, next_goal=None, reward=None):
+              skip_ego_won: bool = True, goal=None, next_goal=None, reward=None, flags=None):
         """Append T steps of N envs ([T, N, ...] tensors; obs_first [N, 10] = observation
         before step 0). skip_ego_won drops the transitions whose won bit is set (main.py:209;
         hdqn.py:316 stores all: pass False). A goal ring needs goal / next_goal [T, N] (the goal
         columns of s and s'); reward [T, N] replaces the ego's env reward rew[..., 0] as the r
-        column (hdqn.py:314's intrinsic reward). Stream-ordered; nothing is synchronised."""
+        column (hdqn.py:314's intrinsic reward). flags: a rollout's interleaved [T, N, 4] buffer
+        (a1, a2, done, collision), read in place of a1 / done. Stream-ordered; nothing is
+        synchronised."""
         torch = self._torch
         if self.goal != (goal is not None) or (goal is None) != (next_goal is None):
             raise ValueError("a goal ring takes goal and next_goal; a plain ring takes neither")
@@ -100,10 +102,17 @@ class ReplayRing:
             done = None if done is None else torch.as_tensor(done, device=self.device)[None]
             final_obs = None if final_obs is None else torch.as_tensor(final_obs, device=self.device)[None]
             won_mask = None if won_mask is None else torch.as_tensor(won_mask, device=self.device)[None]
+            flags = None if flags is None else torch.as_tensor(flags, device=self.device)[None]
         T, n = a1.shape
-        if a1.dtype != torch.int8:
+        if flags is not None:
+            flags = torch.as_tensor(flags, device=self.device)
+            if flags.dtype != torch.uint8 or tuple(flags.shape) != (T, n, 4) or not flags.is_contiguous():
+                raise ValueError(f"flags must be a contiguous [{T}, {n}, 4] uint8 tensor")
+            a1, done = None, None  # read from flags
+        elif a1.dtype != torch.int8:
             a1 = a1.to(torch.int8)
-        a1 = a1.contiguous()
+        if a1 is not None:
+            a1 = a1.contiguous()
         obs_first = self._f32(obs_first, (n, _OBS_DIM))
         obs = self._f32(obs, (T, n, _OBS_DIM))
         rew = self._f32(rew, (T, n, 2))
@@ -130,13 +139,13 @@ class ReplayRing:
         ptr = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
         tr = _native.Transitions(ptr(obs_first), ptr(obs), ptr(final_obs), ptr(a1), ptr(rew),
                                  ptr(done), ptr(won_mask) if skip_ego_won else None, ptr(goal),
-                                 ptr(next_goal), ptr(reward))
+                                 ptr(next_goal), ptr(reward), ptr(flags))
         scratch = self._scratch_for(n, T)
         rc = _native.lib.mg_replay_store(
             self.memory.data_ptr(), self._counter.data_ptr(), self.capacity, self.row, ctypes.byref(tr), n,
             T, 1 if skip_ego_won else 0, scratch.data_ptr(), scratch.numel() * 8, self._stream())
         _native.check(rc, "mg_replay_store")
-        self._keepalive = (obs_first, obs, a1, rew, done, final_obs, won_mask, goal, next_goal, reward)
+        self._keepalive = (obs_first, obs, a1, rew, done, final_obs, won_mask, goal, next_goal, reward, flags)
 
     def store_rollout(self, obs_first, traj, skip_ego_won: bool = True, goal=None, next_goal=None,
                       reward=None):
@@ -147,7 +156,8 @@ class ReplayRing:
             raise ValueError("the rollout has no final_observation: episode ends would store the "
                              "reset observation as next_state; roll out with final_observation=True")
         self.store(obs_first, traj["obs"], traj["a1"], traj["rew"], traj["done"],
-                   traj["final_observation"], traj.get("won_mask"), skip_ego_won, goal, next_goal, reward)
+                   traj["final_observation"], traj.get("won_mask"), skip_ego_won, goal, next_goal, reward,
+                   traj.get("flags"))
 
     def store_transition(self, state, action, reward, next_state):
         """The reference's single-transition call (main.py:115-119; hdqn.py:180-184 for a goal

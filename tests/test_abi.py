@@ -39,8 +39,8 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_native.Params) == 20 * 8 + 16 + 16
     assert ctypes.sizeof(_native.State) == 7 * 8
     assert ctypes.sizeof(_native.Outputs) == 9 * 8
-    assert ctypes.sizeof(_native.Traj) == 8 * 8
-    assert ctypes.sizeof(_native.Transitions) == 10 * 8
+    assert ctypes.sizeof(_native.Traj) == 9 * 8
+    assert ctypes.sizeof(_native.Transitions) == 11 * 8
     assert ctypes.sizeof(_native.Stats) == 2 * 8
     assert _native.REC64_DTYPE.itemsize == 168
 

@@ -77,6 +77,10 @@ class Bed:
         won = self.twon.data_ptr() if os.environ.get("MG_AB_WON") == "1" else None
         self.traj = nat.Traj(self.tobs.data_ptr(), self.trew.data_ptr(), self.tdone.data_ptr(),
                              self.tcoll.data_ptr(), self.ta[0].data_ptr(), self.ta[1].data_ptr(), None, won)
+        if os.environ.get("MG_AB_FLAGS") == "1":  # interleaved (a1, a2, done, coll) per env-step
+            self.tflags = torch.empty((T, n, 4), dtype=torch.uint8, device=dev)
+            self.traj = nat.Traj(self.tobs.data_ptr(), self.trew.data_ptr(), None, None, None, None, None, won,
+                                 self.tflags.data_ptr())
         self.k = 0
         assert lib.mg_reset(ctypes.byref(self.params), ctypes.byref(self.state), None, None, n, None) == 0
 
@@ -238,8 +242,8 @@ def main_replay(a):
     obs0 = env.observe().clone()
     traj = env.rollout_random(a.T, 5, first_step=230)
     ptr = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
-    tr = nat.Transitions(ptr(obs0), ptr(traj["obs"]), ptr(traj["final_observation"]), ptr(traj["a1"]),
-                         ptr(traj["rew"]), ptr(traj["done"].view(torch.uint8)), ptr(traj["won_mask"]))
+    tr = nat.Transitions(ptr(obs0), ptr(traj["obs"]), ptr(traj["final_observation"]), None,
+                         ptr(traj["rew"]), None, ptr(traj["won_mask"]), None, None, None, ptr(traj["flags"]))
     cap = 1 << 24
     beds = {}
     for p in a.libs:
