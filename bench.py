@@ -203,10 +203,11 @@ def qnet_leg(env, args, world, dist, torch, opponent):
 
 
 def replay_algorithmic_bytes(n, T, kept, done_rows):
-    """Bytes mg_replay_store must move at minimum: every obs row once (40) + done (1) + won bits
-    (read by both kernels, 2 x 1/8); per stored transition a (1) + r (4) + the 88-byte row written;
-    the terminal observation of done rows (40); obs_first once per env (40)."""
-    return n * T * (40 + 1 + 0.25) + kept * (1 + 4 + 88) + done_rows * 40 + n * 40
+    """Bytes mg_replay_store must move at minimum: every obs row once (40) + the trajectory's
+    interleaved (a1, a2, done, collision) word (4: a and done are read from it) + won bits (read by
+    both kernels, 2 x 1/8); per stored transition r (4) + the 88-byte row written; the terminal
+    observation of done rows (40); obs_first once per env (40)."""
+    return n * T * (40 + 4 + 0.25) + kept * (4 + 88) + done_rows * 40 + n * 40
 
 
 def replay_leg(env, args, torch):
