@@ -11,6 +11,29 @@ from __future__ import annotations
 import math
 
 EPISILO = 0.7  # main.py:16, hdqn.py:20 -- greedy when np.random.randn() <= EPISILO
+NUM_GOALS = 3  # hdqn.py:31
+
+
+def goal_status(states):
+    """hdqn.py:223-237: the sub-goal an observation is in -- 0 if dx1 < -0.5 v2, 1 if dx1 < 0.5 v2,
+    else 2 (dx1 = obs[0], v2 = obs[9]). One observation (10 values) gives an int, as the reference;
+    a [N, 10] tensor gives int64 [N] on its device (the comparisons are exact in fp32: -0.5 v2 is a
+    power-of-two scaling, so only the observation's own rounding to fp32 can differ)."""
+    try:
+        import torch
+
+        if isinstance(states, torch.Tensor) and states.dim() == 2:
+            dx1, v2 = states[:, 0], states[:, 9]
+            one, two = torch.ones_like(dx1, dtype=torch.int64), torch.full_like(dx1, 2, dtype=torch.int64)
+            return torch.where(dx1 < -0.5 * v2, torch.zeros_like(one), torch.where(dx1 < 0.5 * v2, one, two))
+    except ImportError:  # pragma: no cover - torch is part of the image
+        pass
+    dx1, v2 = states[0], states[9]
+    if dx1 < -0.5 * v2:
+        return 0
+    elif dx1 < 0.5 * v2:
+        return 1
+    return 2
 
 
 def greedy_threshold(episilo: float = EPISILO) -> int:

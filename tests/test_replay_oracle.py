@@ -111,3 +111,21 @@ def test_sample_index_range_and_uniformity(coracle):
     assert small.max() < 37
     empty = mo.replay_sample_index(coracle, 2000, 0, seed=3, draw=11, batch=64, filled_only=True)
     assert (empty == 0).all()
+
+
+@pytest.mark.parametrize("tag", ["HL0", "HRR"])
+def test_goal_status_matches_reference_intrinsic_rewards(coracle, replay_golden, tag):
+    """policy.goal_status (hdqn.py:223-237) on the oracle's observations reproduces every intrinsic
+    reward of the reference run (1.0 iff next_goal == goal_status(state), hdqn.py:314), scalar and
+    batched."""
+    import torch
+
+    from merging_gym.policy import goal_status
+
+    g = {k[len(tag) + 1:]: replay_golden[k] for k in replay_golden.files if k.startswith(tag + "_")}
+    obs0, obs, *_ = _oracle_episode_run(coracle, g["a1"], g["a2"])
+    prev = np.concatenate([obs0[None], obs[:-1]], axis=0)[:, 0]  # the state before each step
+    batch = goal_status(torch.from_numpy(prev)).numpy()
+    scalar = np.array([goal_status([float(x) for x in row]) for row in prev])
+    np.testing.assert_array_equal(batch, scalar)
+    np.testing.assert_array_equal((g["next_goal"] == batch).astype(np.float32), g["intrinsic"])
