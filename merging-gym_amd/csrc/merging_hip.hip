@@ -108,8 +108,12 @@ __device__ __forceinline__ void st_sc1(T* p, T v) {
     uint32_t w;
     __builtin_memcpy(&w, &v, 4);
     __hip_atomic_store(reinterpret_cast<uint32_t*>(p), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else if constexpr (sizeof(T) == 2) {
+    uint16_t w;
+    __builtin_memcpy(&w, &v, 2);
+    __hip_atomic_store(reinterpret_cast<uint16_t*>(p), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {
-    static_assert(sizeof(T) == 1, "st_sc1: 1, 4, 8 or 16 bytes");
+    static_assert(sizeof(T) == 1, "st_sc1: 1, 2, 4, 8 or 16 bytes");
     uint8_t w;
     __builtin_memcpy(&w, &v, 1);
     __hip_atomic_store(reinterpret_cast<uint8_t*>(p), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -131,6 +135,8 @@ template <class T>
 __device__ __forceinline__ void st_state(T* p, T v) {
 #if MG_SC1_STATE
   st_sc1(p, v);
+#elif MG_NT_STATE  // A/B knob: non-temporal state stores too
+  __builtin_nontemporal_store(v, p);
 #else
   *p = v;
 #endif
@@ -260,23 +266,26 @@ __device__ __forceinline__ bool boxes_intersect(const Box& a, const Box& b) {
   return a.l <= b.r && b.l <= a.r && a.t <= b.b && b.t <= a.b;
 }
 
-// observe (merging_env.py:118-132)
+// observe (merging_env.py:118-132): computed in fp64, stored as OT (fp64 for the single-env
+// record; fp32 -- the one rounding every fp32 output gets -- for the batched kernels)
+template <class OT>
 __device__ __forceinline__ void observe(const mg_params& P, double p1, double v1, double p2,
                                         double v2, double x1, double y1, double x2, double y2,
-                                        double (&o)[kObs]) {
-  o[0] = x2 - x1;
-  o[1] = y2 - y1;
-  o[2] = v2 - v1;
-  o[3] = P.end_point - p1;
-  o[4] = v1;
-  o[5] = x1 - x2;
-  o[6] = y1 - y2;
-  o[7] = v1 - v2;
-  o[8] = P.end_point - p2;
-  o[9] = v2;
+                                        OT (&o)[kObs]) {
+  o[0] = static_cast<OT>(x2 - x1);
+  o[1] = static_cast<OT>(y2 - y1);
+  o[2] = static_cast<OT>(v2 - v1);
+  o[3] = static_cast<OT>(P.end_point - p1);
+  o[4] = static_cast<OT>(v1);
+  o[5] = static_cast<OT>(x1 - x2);
+  o[6] = static_cast<OT>(y1 - y2);
+  o[7] = static_cast<OT>(v1 - v2);
+  o[8] = static_cast<OT>(P.end_point - p2);
+  o[9] = static_cast<OT>(v2);
 }
 
-__device__ __forceinline__ void reset_obs(const mg_params& P, double (&o)[kObs]) {
+template <class OT>
+__device__ __forceinline__ void reset_obs(const mg_params& P, OT (&o)[kObs]) {
   double x1, y1, x2, y2;
   lon2coord(P, P.start_point, true, x1, y1);
   lon2coord(P, P.start_point, false, x2, y2);
@@ -345,8 +354,20 @@ __device__ __forceinline__ void store_env(const mg_state& S, int64_t i, const En
 }
 
 // What one step returns besides the new state.
+// The observation a step hands back, held as fp32: every batched output is fp32, and fp32
+// here frees 10 VGPRs (66 -> fewer in the one-step kernel). The single-env record, which returns
+// the reference's fp64 floats, recomputes its observation in fp64 from the state.
+#ifndef MG_OBS_F32
+#define MG_OBS_F32 1
+#endif
+#if MG_OBS_F32
+typedef float obs_t;
+#else
+typedef double obs_t;
+#endif
+
 struct StepOut {
-  double o[kObs];  // observation (the reset observation once autoreset has fired)
+  obs_t o[kObs];  // observation (the reset observation once autoreset has fired)
   double r1, r2, acc1, acc2;
   bool done, coll, r1_int, r2_int, v1_int, v2_int;
   int bad;  // 1: action1 invalid, 2: action2 invalid (the reference's KeyError)
@@ -603,7 +624,7 @@ __device__ __forceinline__ void finish_episode(const mg_params& P, Env& e, StepO
 // Write a block's [rows,10] fp32 observation tile through LDS as contiguous 16-byte stores
 // (a wave's 64 rows of 40 B become 160 dwordx4 lanes instead of 640 scattered dwords).
 // Every thread of the block must call it (two barriers).
-__device__ __forceinline__ void store_obs_tile_n(float* tile, const double (&o)[kObs], float* dst,
+__device__ __forceinline__ void store_obs_tile_n(float* tile, const obs_t (&o)[kObs], float* dst,
                                                  int nrows, int block) {
   const int tid = threadIdx.x;
   float2* t2 = reinterpret_cast<float2*>(tile + tid * kObs);
@@ -629,7 +650,7 @@ __device__ __forceinline__ void store_obs_tile_n(float* tile, const double (&o)[
   __syncthreads();
 }
 
-__device__ __forceinline__ void store_obs_tile(float* tile, const double (&o)[kObs], float* dst,
+__device__ __forceinline__ void store_obs_tile(float* tile, const obs_t (&o)[kObs], float* dst,
                                                int nrows) {
   store_obs_tile_n(tile, o, dst, nrows, kBlock);
 }
@@ -646,7 +667,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 // observations afterwards, and no other wave is waited for.
 __device__ __forceinline__ void wave_copy_rows(const float* wtile, float* dst, int nrows);
 
-__device__ __forceinline__ void wave_store_obs(float* wtile, const double (&o)[kObs], float* dst,
+__device__ __forceinline__ void wave_store_obs(float* wtile, const obs_t (&o)[kObs], float* dst,
                                                int nrows) {
   const int lane = threadIdx.x & 63;
   float2* t2 = reinterpret_cast<float2*>(wtile + lane * kObs);
@@ -706,6 +727,18 @@ __device__ __forceinline__ void store_won_mask(uint64_t* mask, bool won, int t, 
     st_out(mask + static_cast<int64_t>(t) * ((n + 63) >> 6) + (wbase >> 6), m);
 }
 
+// The env index through an empty asm: the state stores recompute their addresses from it
+// instead of keeping the load addresses (two VGPRs per array) live across the step.
+#ifndef MG_STEP_OPAQUE_INDEX
+#define MG_STEP_OPAQUE_INDEX 1
+#endif
+__device__ __forceinline__ int64_t opaque_index(int64_t i) {
+#if MG_STEP_OPAQUE_INDEX
+  asm volatile("" : "+v"(i));
+#endif
+  return i;
+}
+
 struct Launch {
   mg_params P;
   mg_state S;
@@ -762,6 +795,16 @@ __global__ __launch_bounds__(kBlock, MG_STEP_WAVES_PER_EU) void step_kernel(cons
         mg_rec64* rec = L.O.rec64 + i;
 #pragma unroll
         for (int k = 0; k < kObs; ++k) rec->obs[k] = r.o[k];
+#if MG_OBS_F32
+        {  // the fp64 observation of the state after the step (score_step's values, recomputed)
+          double x1, y1, x2, y2, od[kObs];
+          lon2coord(P, e.p1, true, x1, y1);
+          lon2coord(P, e.p2, false, x2, y2);
+          observe(P, e.p1, e.v1, e.p2, e.v2, x1, y1, x2, y2, od);
+#pragma unroll
+          for (int k = 0; k < kObs; ++k) rec->obs[k] = od[k];
+        }
+#endif
         rec->rew[0] = r.r1;
         rec->rew[1] = r.r2;
         rec->acc[0] = r.acc1;
@@ -789,7 +832,7 @@ __global__ __launch_bounds__(kBlock, MG_STEP_WAVES_PER_EU) void step_kernel(cons
       won = e.winner == 1;
       if ((L.flags & MG_AUTORESET) && r.done)
         finish_episode(P, e, r, L.St, L.O.final_obs ? L.O.final_obs + i * kObs : nullptr, i);
-      store_env(L.S, i, e);
+      store_env(L.S, opaque_index(i), e);
     }
   }
 
