@@ -310,5 +310,34 @@ class MergeVecEnv:
             self.ret_sum.zero_()
             self.counts.zero_()
 
+    # ------------------------------------------------------------------ checkpoint / resume
+    _STATE_KEYS = ("p1", "v1", "p2", "v2", "ret1", "ret2", "tf")
+
+    def state_dict(self):
+        """The batch's full state as tensors (copies, on this device) plus the step index that
+        keys the Philox actions: `torch.save(env.state_dict(), path)` checkpoints a run, and
+        `load_state_dict` resumes it bit for bit (the reference keeps no env checkpoint; its
+        scripts save only the agents, main.py:244-245, hdqn.py:362-366)."""
+        sd = {k: getattr(self, k).clone() for k in self._STATE_KEYS}
+        sd["step_idx"] = self._step_idx
+        sd["env_offset"] = self.env_offset
+        if self.ret_sum is not None:
+            sd["ret_sum"], sd["counts"] = self.ret_sum.clone(), self.counts.clone()
+        return sd
+
+    def load_state_dict(self, sd):
+        for k in self._STATE_KEYS:
+            src = self._torch.as_tensor(sd[k])
+            dst = getattr(self, k)
+            if tuple(src.shape) != tuple(dst.shape) or src.dtype != dst.dtype:
+                raise ValueError(f"{k}: expected {tuple(dst.shape)} {dst.dtype}, got {tuple(src.shape)} {src.dtype}")
+            dst.copy_(src)  # in place: the kernels hold these buffers' addresses
+        if int(sd.get("env_offset", self.env_offset)) != self.env_offset:
+            raise ValueError("the checkpoint is of another env shard (env_offset differs)")
+        self._step_idx = int(sd["step_idx"])
+        if self.ret_sum is not None and "ret_sum" in sd:
+            self.ret_sum.copy_(self._torch.as_tensor(sd["ret_sum"]))
+            self.counts.copy_(self._torch.as_tensor(sd["counts"]))
+
     def close(self):
         pass

@@ -182,6 +182,18 @@ class ReplayRing:
         self.store(s.to(self.device), s2.to(self.device), a.to(self.device), r.to(self.device),
                    skip_ego_won=False)
 
+    # ------------------------------------------------------------------ checkpoint / resume
+    def state_dict(self):
+        """memory (copy) and memory_counter -- what DQN's memory and counter hold."""
+        return {"memory": self.memory.clone(), "counter": self._counter.clone(), "goal": self.goal}
+
+    def load_state_dict(self, sd):
+        mem = self._torch.as_tensor(sd["memory"])
+        if tuple(mem.shape) != tuple(self.memory.shape) or bool(sd.get("goal", False)) != self.goal:
+            raise ValueError(f"expected a {tuple(self.memory.shape)} ring (goal={self.goal})")
+        self.memory.copy_(mem)
+        self._counter.copy_(self._torch.as_tensor(sd["counter"]))
+
     # ------------------------------------------------------------------ sampling
     def sample_rows(self, batch_size: int = 128, seed: int = 0, draw: int = 0,
                     filled_only: bool = False, return_index: bool = False):
