@@ -332,6 +332,7 @@ def main():
     for k in range(args.steps):
         step(args.warmup + k)
     ev1.record()
+    host_ms = (time.perf_counter() - t0) * 1e3 / args.steps  # host enqueue time per launch
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -413,7 +414,7 @@ def main():
                          "bytes_per_env_step": BYTES_PER_ENV_STEP,
                          "kernel_ms_mean": kernel_ms, "kernel_ms_mean_max_rank": kernel_ms_max,
                          "timing": "HIP events recorded on the launch stream around the K timed launches, / K",
-                         "kernel_ms_dispatch_sample": dispatch_ms},
+                         "kernel_ms_dispatch_sample": dispatch_ms, "host_enqueue_ms_per_launch": host_ms},
             "episodes": episodes,
         }
         if rollout is not None:
