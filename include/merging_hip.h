@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 5
+#define MG_ABI_VERSION 6
 #define MG_OBS_DIM 10   /* merging_env.py:75 observation_shape = (10) */
 #define MG_NUM_ACTIONS 5 /* merging_env.py:101-102 action_dict / Discrete(5) */
 #define MG_ACTION_NONE (-1) /* action2=None: the constant-speed "L0" opponent, merging_env.py:152 */
@@ -138,6 +138,10 @@ typedef struct mg_outputs {
                            always, the ego too when only a2 is invalid; nothing else is written. */
   uint64_t* won_mask;   /* [ceil(n/64)] bit = env.winner == 1 after this step (read before any
                            autoreset): main.py:209 stores a transition only when it is 0 */
+  uint8_t* flags;       /* [n,4] interleaved a1, a2 (int8), done, collision (0/1), 4-byte aligned:
+                           one 32-bit store per env instead of four byte stores. When set, done
+                           and coll must be NULL, and so must mg_step_random's a1_out / a2_out
+                           (the actions land here); mg_observe writes byte 3. Not with rec64. */
 } mg_outputs;
 
 /* Trajectory buffers of mg_rollout_random: the outputs of step t for env i sit at row

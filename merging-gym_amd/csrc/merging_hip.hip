@@ -739,6 +739,13 @@ __device__ __forceinline__ int64_t opaque_index(int64_t i) {
   return i;
 }
 
+// One env-step's four byte outputs (a1, a2, done, collision) as the little-endian u32 of an
+// interleaved [.., 4] uint8 buffer (mg_outputs.flags, mg_traj.flags).
+__device__ __forceinline__ uint32_t pack_step_bytes(int a1, int a2, bool done, bool coll) {
+  return static_cast<uint32_t>(a1 & 0xff) | (static_cast<uint32_t>(a2 & 0xff) << 8) |
+         (done ? 0x10000u : 0u) | (coll ? 0x1000000u : 0u);
+}
+
 struct Launch {
   mg_params P;
   mg_state S;
@@ -778,8 +785,10 @@ __global__ __launch_bounds__(kBlock, MG_STEP_WAVES_PER_EU) void step_kernel(cons
     if constexpr (ACT == kActPhilox) {
       draw_actions(static_cast<uint64_t>(L.env_offset + i), L.step_idx, L.seed, L.opp_random, a1, a2);
 #if !MG_ABL_NO_BYTES
-      if (L.a1_out) st_out(L.a1_out + i, static_cast<int8_t>(a1));
-      if (L.a2_out) st_out(L.a2_out + i, static_cast<int8_t>(a2));
+      if (!L.O.flags) {  // with O.flags the actions go out with done / collision below
+        if (L.a1_out) st_out(L.a1_out + i, static_cast<int8_t>(a1));
+        if (L.a2_out) st_out(L.a2_out + i, static_cast<int8_t>(a2));
+      }
 #endif
     } else {
       a1 = L.a1[i];
@@ -824,8 +833,12 @@ __global__ __launch_bounds__(kBlock, MG_STEP_WAVES_PER_EU) void step_kernel(cons
                f32x2{static_cast<float>(r.r1), static_cast<float>(r.r2)});
       }
 #if !MG_ABL_NO_BYTES
-      if (L.O.done) st_out(L.O.done + i, static_cast<uint8_t>(r.done ? 1 : 0));
-      if (L.O.coll) st_out(L.O.coll + i, static_cast<uint8_t>(r.coll ? 1 : 0));
+      if (L.O.flags) {
+        st_out(reinterpret_cast<uint32_t*>(L.O.flags) + i, pack_step_bytes(a1, a2, r.done, r.coll));
+      } else {
+        if (L.O.done) st_out(L.O.done + i, static_cast<uint8_t>(r.done ? 1 : 0));
+        if (L.O.coll) st_out(L.O.coll + i, static_cast<uint8_t>(r.coll ? 1 : 0));
+      }
 #else
       if (a1 + a2 == 1234 && r.coll) L.O.done[0] = 1;
 #endif
@@ -857,9 +870,7 @@ __global__ __launch_bounds__(kBlock, MG_STEP_WAVES_PER_EU) void step_kernel(cons
 __device__ __forceinline__ void store_step_bytes(const mg_traj& T, int64_t row, int a1, int a2, bool done,
                                                  bool coll) {
   if (T.flags) {
-    st_out(reinterpret_cast<uint32_t*>(T.flags) + row,
-           static_cast<uint32_t>(a1 & 0xff) | (static_cast<uint32_t>(a2 & 0xff) << 8) |
-               (done ? 0x10000u : 0u) | (coll ? 0x1000000u : 0u));
+    st_out(reinterpret_cast<uint32_t*>(T.flags) + row, pack_step_bytes(a1, a2, done, coll));
     return;
   }
   if (T.a1) st_out(T.a1 + row, static_cast<int8_t>(a1));
@@ -1706,7 +1717,8 @@ __global__ __launch_bounds__(kBlock) void observe_kernel(const mg_params P, cons
 #pragma unroll
     for (int k = 0; k < kObs; ++k) O.rec64[i].obs[k] = o[k];
   }
-  if (O.coll) O.coll[i] = boxes_intersect(vehicle_box(P, y1, x1), vehicle_box(P, y2, x2)) ? 1 : 0;
+  uint8_t* coll = O.flags ? O.flags + 4 * i + 3 : (O.coll ? O.coll + i : nullptr);
+  if (coll) *coll = boxes_intersect(vehicle_box(P, y1, x1), vehicle_box(P, y2, x2)) ? 1 : 0;
 }
 
 // ============================================================================ replay memory
@@ -2018,6 +2030,12 @@ int check_common(const mg_params* p, const mg_state* s, const mg_outputs* o, int
     return fail(hipErrorInvalidValue, "%s", "obs must be 16-byte aligned");
   if (o->rew && (reinterpret_cast<uintptr_t>(o->rew) & 7))
     return fail(hipErrorInvalidValue, "%s", "rew must be 8-byte aligned");
+  if (o->flags) {
+    if (reinterpret_cast<uintptr_t>(o->flags) & 3)
+      return fail(hipErrorInvalidValue, "%s", "flags must be 4-byte aligned");
+    if (o->done || o->coll || o->rec64)
+      return fail(hipErrorInvalidValue, "%s", "flags replaces done / coll (and rec64 has its own status): pass NULL");
+  }
   return 0;
 }
 
@@ -2132,6 +2150,8 @@ int mg_step_random(const mg_params* params, const mg_state* state, int8_t* a1_ou
   L.S = *state;
   L.O = *out;
   if (stats) L.St = *stats;
+  if (out->flags && (a1_out || a2_out))
+    return fail(hipErrorInvalidValue, "%s", "flags records the actions: pass NULL a1_out / a2_out");
   L.a1_out = a1_out;
   L.a2_out = a2_out;
   L.seed = seed;

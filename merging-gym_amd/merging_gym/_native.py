@@ -15,7 +15,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libmerging_hip.so"
 LIB_PATH = os.environ.get("MERGING_HIP_LIB", os.path.join(_HERE, LIB_NAME))
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 OBS_DIM = 10
 NUM_ACTIONS = 5
@@ -50,7 +50,7 @@ class State(_c.Structure):
 
 class Outputs(_c.Structure):
     _fields_ = [(n, _P) for n in ("obs", "rew", "done", "coll", "done_mask", "final_obs",
-                                  "rec64", "error", "won_mask")]
+                                  "rec64", "error", "won_mask", "flags")]
 
 
 class Traj(_c.Structure):

@@ -35,6 +35,9 @@ _OBS_DIM = 10
 # low address bits; staggered, the step measured 2-3 % faster at 2^20 and 2^23 envs
 # (tools/stagger_probe.py). MG_ARENA_STAGGER=-1 restores separate allocations (A/B).
 _ARENA_STAGGER = int(os.environ.get("MG_ARENA_STAGGER", "4160"))
+# One interleaved [N, 4] uint8 record (a1, a2, done, collision) per step instead of four byte
+# arrays (mg_outputs.flags). MG_STEP_FLAGS=0 restores the four arrays (A/B, and the tests run both).
+_STEP_FLAGS = os.environ.get("MG_STEP_FLAGS", "1") != "0"
 
 
 class MergeVecEnv:
@@ -68,11 +71,25 @@ class MergeVecEnv:
         specs = [("p1", (n,), f64), ("v1", (n,), f64), ("p2", (n,), f64), ("v2", (n,), f64),
                  ("ret1", (n,), f64), ("ret2", (n,), f64),
                  ("tf", (n,), torch.int16),  # uint16 bits, see MG_TF_*
-                 ("obs", (n, _OBS_DIM), f32), ("rew", (n, 2), f32), ("done", (n,), torch.uint8),
-                 ("coll", (n,), torch.uint8), ("a1_buf", (n,), torch.int8), ("a2_buf", (n,), torch.int8)]
+                 ("obs", (n, _OBS_DIM), f32), ("rew", (n, 2), f32)]
+        if _STEP_FLAGS:
+            # a1, a2, done, collision interleaved per env (mg_outputs.flags): one 32-bit store per
+            # env-step instead of four byte streams; the four are strided views of self.flags.
+            # step()'s host actions are staged in separate contiguous buffers.
+            specs += [("flags", (n, 4), torch.uint8), ("_a1_in", (n,), torch.int8), ("_a2_in", (n,), torch.int8)]
+        else:
+            specs += [("done", (n,), torch.uint8), ("coll", (n,), torch.uint8), ("a1_buf", (n,), torch.int8),
+                      ("a2_buf", (n,), torch.int8)]
         if final_observation:
             specs.append(("final_obs", (n, _OBS_DIM), f32))
         self._arena = self._carve(specs, dev)
+        if _STEP_FLAGS:
+            self.a1_buf, self.a2_buf = self.flags[:, 0].view(torch.int8), self.flags[:, 1].view(torch.int8)
+            self.done, self.coll = self.flags[:, 2], self.flags[:, 3]
+            self.flags.zero_()
+        else:
+            self.flags = None
+            self._a1_in, self._a2_in = self.a1_buf, self.a2_buf
         self.done.zero_()
         self.coll.zero_()
         if final_observation:
@@ -91,16 +108,19 @@ class MergeVecEnv:
         ptr = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
         self._state = _native.State(*(ptr(t) for t in (self.p1, self.v1, self.p2, self.v2,
                                                         self.ret1, self.ret2, self.tf)))
-        self._out = _native.Outputs(ptr(self.obs), ptr(self.rew), ptr(self.done), ptr(self.coll),
-                                    ptr(self.done_mask), ptr(self.final_obs), None, ptr(self.error),
-                                    ptr(self.won_mask))
+        packed = self.flags is not None
+        self._out = _native.Outputs(ptr(self.obs), ptr(self.rew), None if packed else ptr(self.done),
+                                    None if packed else ptr(self.coll), ptr(self.done_mask),
+                                    ptr(self.final_obs), None, ptr(self.error), ptr(self.won_mask),
+                                    ptr(self.flags))
         self._stats = _native.Stats(ptr(self.ret_sum), ptr(self.counts))
         self._flags = _native.AUTORESET if self.autoreset else 0
         self._step_idx = 0
         # pre-bound call arguments: a step costs one ctypes call and no allocations
         self._p_ref, self._s_ref = ctypes.byref(self.params), ctypes.byref(self._state)
         self._o_ref, self._st_ref = ctypes.byref(self._out), ctypes.byref(self._stats)
-        self._a1_ptr, self._a2_ptr = self.a1_buf.data_ptr(), self.a2_buf.data_ptr()
+        # mg_step_random's a1_out / a2_out: NULL when the actions land in self.flags
+        self._a1_ptr, self._a2_ptr = (None, None) if packed else (self.a1_buf.data_ptr(), self.a2_buf.data_ptr())
         self._raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
         info = {"collision": self.coll.view(torch.bool)}
         if self.final_obs is not None and self.autoreset:
@@ -186,8 +206,8 @@ class MergeVecEnv:
     def step(self, actions1, actions2=None):
         """One step of every env: merging_env.py:138-195 batched. actions2=None is the
         reference's L0 opponent (constant speed); per-env -1 also means None."""
-        a1 = self._actions(actions1, self.a1_buf, allow_none=False)
-        a2 = self._actions(actions2, self.a2_buf, allow_none=True)
+        a1 = self._actions(actions1, self._a1_in, allow_none=False)
+        a2 = self._actions(actions2, self._a2_in, allow_none=True)
         rc = self._nat.lib.mg_step(
             self._p_ref, self._s_ref, a1.data_ptr(), None if a2 is None else a2.data_ptr(),
             self._o_ref, self._st_ref, self.num_envs, self._flags, self._stream())
@@ -197,7 +217,8 @@ class MergeVecEnv:
     def step_random(self, seed: int, opponent_random: bool = True, step_idx=None,
                     record_actions: bool = True):
         """One step with actions drawn on the GPU (Philox4x32-10 keyed by seed, counter =
-        (global env index, step index)). The actions used land in self.a1_buf / a2_buf."""
+        (global env index, step index)). The actions used land in self.a1_buf / a2_buf (always,
+        when they are views of self.flags)."""
         k = self._step_idx if step_idx is None else int(step_idx)
         rc = self._nat.lib.mg_step_random(
             self._p_ref, self._s_ref, self._a1_ptr if record_actions else None,
@@ -286,6 +307,7 @@ class MergeVecEnv:
     def observe(self):
         """Observation of the current state without stepping (merging_env.py:118-132)."""
         out = self._nat.Outputs(self._out.obs, None, None, self._out.coll)
+        out.flags = self._out.flags  # collision byte 3 of the interleaved record
         self._nat.check(self._nat.lib.mg_observe(ctypes.byref(self.params), ctypes.byref(self._state),
                                                  ctypes.byref(out), self.num_envs,
                                                  ctypes.c_void_p(self._stream())),

@@ -38,7 +38,7 @@ def test_struct_layouts_match_header():
     # mg_params: 15 doubles + 5 doubles + 4 int32 + 2 doubles; mg_rec64: 20 doubles + 2 uint32
     assert ctypes.sizeof(_native.Params) == 20 * 8 + 16 + 16
     assert ctypes.sizeof(_native.State) == 7 * 8
-    assert ctypes.sizeof(_native.Outputs) == 9 * 8
+    assert ctypes.sizeof(_native.Outputs) == 10 * 8
     assert ctypes.sizeof(_native.Traj) == 9 * 8
     assert ctypes.sizeof(_native.Transitions) == 11 * 8
     assert ctypes.sizeof(_native.Stats) == 2 * 8
@@ -90,6 +90,17 @@ def test_argument_errors_without_gpu():
     assert rc != 0 and b"row_floats" in _native.lib.mg_last_error()
     rc = _native.lib.mg_replay_sample(fake, fake, 16, 23, 0, 0, 0, fake, None, 4, None)
     assert rc != 0 and b"row_floats" in _native.lib.mg_last_error()
+    # the interleaved step record: 4-byte aligned, and it replaces done / coll / a1_out / a2_out
+    P, st = ctypes.byref(_native.default_params()), ctypes.byref(_native.State(*([fake] * 7)))
+    bad = _native.Outputs(flags=ctypes.c_void_p((1 << 20) + 2))
+    rc = _native.lib.mg_step_random(P, st, None, None, ctypes.byref(bad), None, 16, 0, 1, 0, 1, 0, None)
+    assert rc != 0 and b"4-byte" in _native.lib.mg_last_error()
+    both = _native.Outputs(done=fake, flags=fake)
+    rc = _native.lib.mg_step(P, st, fake, None, ctypes.byref(both), None, 16, 0, None)
+    assert rc != 0 and b"flags replaces" in _native.lib.mg_last_error()
+    rc = _native.lib.mg_step_random(P, st, fake, None, ctypes.byref(_native.Outputs(flags=fake)), None, 16, 0, 1,
+                                    0, 1, 0, None)
+    assert rc != 0 and b"a1_out" in _native.lib.mg_last_error()
     # 65536 write blocks in 1024 scan groups: ticket (8) + bases u64 + offsets u32 + totals u32
     assert _native.lib.mg_replay_scratch_bytes(1 << 20, 16) == 8 + 1024 * 8 + 65536 * 4 + 1024 * 4
     assert _native.lib.mg_replay_scratch_bytes(0, 4) == 0

@@ -152,6 +152,52 @@ def test_device_random_actions_match_philox(torch, coracle):
     _check_state(env, envs)
 
 
+def test_interleaved_step_record_equals_byte_arrays(torch, monkeypatch):
+    """mg_outputs.flags (a1, a2, done, collision as one u32 per env, MergeVecEnv's default) gives
+    the same outputs and state as the four byte arrays, for device and host actions (None
+    opponent included), autoreset, and observe()."""
+    from merging_gym import MergeVecEnv
+    from merging_gym.envs import vector_env
+
+    n, seed = 3001, 17
+    monkeypatch.setattr(vector_env, "_STEP_FLAGS", False)
+    plain = MergeVecEnv(n, device="cuda:0", final_observation=True, won_mask=True)
+    monkeypatch.setattr(vector_env, "_STEP_FLAGS", True)
+    packed = MergeVecEnv(n, device="cuda:0", final_observation=True, won_mask=True)
+    assert plain.flags is None and packed.flags is not None and packed.done.stride() == (4,)
+    rng = np.random.default_rng(5)
+    ndone = 0
+
+    def same(a, b, k):
+        for x, y in zip(a[:3], b[:3]):
+            assert torch.equal(x.nan_to_num(7.0) if x.is_floating_point() else x,
+                               y.nan_to_num(7.0) if y.is_floating_point() else y), k
+        assert torch.equal(a[3]["collision"], b[3]["collision"]), k
+        assert torch.equal(a[3]["final_observation"].nan_to_num(7.0), b[3]["final_observation"].nan_to_num(7.0)), k
+        for name in ("p1", "v1", "p2", "v2", "ret1", "ret2", "tf", "won_mask"):
+            assert torch.equal(getattr(plain, name), getattr(packed, name)), (name, k)
+
+    for k in range(260):
+        if k % 4 == 3:  # host actions; the L0 opponent (None) on odd rounds
+            a1 = torch.from_numpy(rng.integers(0, 5, n).astype(np.int8)).cuda()
+            a2 = None if k % 8 == 3 else torch.from_numpy(rng.integers(0, 5, n).astype(np.int8)).cuda()
+            outs = plain.step(a1, a2), packed.step(a1, a2)
+            assert torch.equal(packed.a1_buf, a1)
+            assert torch.equal(packed.a2_buf, a2 if a2 is not None else torch.full_like(a1, -1))
+        else:
+            outs = (plain.step_random(seed, opponent_random=k % 2 == 0, step_idx=k),
+                    packed.step_random(seed, opponent_random=k % 2 == 0, step_idx=k))
+            assert torch.equal(plain.a1_buf, packed.a1_buf) and torch.equal(plain.a2_buf, packed.a2_buf), k
+        same(*outs, k)
+        ndone += int(packed.done.sum())
+    assert ndone > 0
+    plain.coll.fill_(9)
+    packed.coll.fill_(9)
+    assert torch.equal(plain.observe(), packed.observe())
+    assert torch.equal(plain.coll, packed.coll) and int(packed.coll.max()) <= 1
+    assert torch.equal(plain.done, packed.done)
+
+
 def test_golden_one_step_rows(torch, golden):
     """The reference's own one-step outputs from 8,000 states near the boundaries."""
     from merging_gym import MergeVecEnv
