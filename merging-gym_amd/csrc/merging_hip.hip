@@ -895,9 +895,25 @@ struct Rollout {
 
 // num_steps consecutive mg_step_random steps with the env kept in registers: the state is
 // read once and written once per launch; step t's outputs go to slice t of the trajectory.
-__global__ __launch_bounds__(kBlock) void rollout_kernel(const Rollout R) {
+#ifndef MG_ROLLOUT_WAVES_PER_EU
+#define MG_ROLLOUT_WAVES_PER_EU 1  // rollout kernel: minimum waves per SIMD the register budget must allow
+#endif
+// FULL: the outputs every MergeVecEnv rollout passes are present (obs, rew, the interleaved step
+// record, statistics, autoreset; final observations and the won mask stay optional). The
+// instance assumes so, which drops null tests the compiler otherwise keeps live across the loop
+// as 64-bit lane masks (SGPR pairs, spilled into VGPR lanes: a v_readlane per use).
+template <bool FULL>
+__global__ __launch_bounds__(kBlock, MG_ROLLOUT_WAVES_PER_EU) void rollout_kernel(const Rollout R) {
   __shared__ __attribute__((aligned(16))) float obs_tile[kBlock * kObs];
 
+  if constexpr (FULL) {
+    __builtin_assume(R.T.obs != nullptr);
+    __builtin_assume(R.T.rew != nullptr);
+    __builtin_assume(R.T.flags != nullptr);
+    __builtin_assume(R.St.ret_sum != nullptr);
+    __builtin_assume(R.St.counts != nullptr);
+    __builtin_assume((R.flags & MG_AUTORESET) != 0);
+  }
   const mg_params& P = R.P;
   const int tid = threadIdx.x;
   const int64_t base = static_cast<int64_t>(blockIdx.x) * kBlock;
@@ -2073,10 +2089,21 @@ int launch_rollout(const Rollout& R, hipStream_t stream) {
   const unsigned blocks = static_cast<unsigned>((R.n + kBlock - 1) / kBlock);
   hipEvent_t start = g_ev_start, stop = g_ev_stop;
   g_ev_start = g_ev_stop = nullptr;
-  if (start || stop)
-    hipExtLaunchKernelGGL(rollout_kernel, dim3(blocks), dim3(kBlock), 0, stream, start, stop, 0, R);
-  else
-    hipLaunchKernelGGL(rollout_kernel, dim3(blocks), dim3(kBlock), 0, stream, R);
+#ifndef MG_ROLLOUT_FULL
+#define MG_ROLLOUT_FULL 1  // A/B knob: 0 always launches the generic instance
+#endif
+  const bool full = MG_ROLLOUT_FULL && R.T.obs && R.T.rew && R.T.flags && R.St.ret_sum && R.St.counts &&
+                    (R.flags & MG_AUTORESET);
+  if (start || stop) {
+    if (full)
+      hipExtLaunchKernelGGL(rollout_kernel<true>, dim3(blocks), dim3(kBlock), 0, stream, start, stop, 0, R);
+    else
+      hipExtLaunchKernelGGL(rollout_kernel<false>, dim3(blocks), dim3(kBlock), 0, stream, start, stop, 0, R);
+  } else if (full) {
+    hipLaunchKernelGGL(rollout_kernel<true>, dim3(blocks), dim3(kBlock), 0, stream, R);
+  } else {
+    hipLaunchKernelGGL(rollout_kernel<false>, dim3(blocks), dim3(kBlock), 0, stream, R);
+  }
   return finish_launch("mg_rollout_random");
 }
 
