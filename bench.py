@@ -202,12 +202,16 @@ def qnet_leg(env, args, world, dist, torch, opponent):
             "agreement_sample": int(x.shape[0])}
 
 
-def replay_algorithmic_bytes(n, T, kept, done_rows):
+def replay_algorithmic_bytes(n, T, kept, done_rows, capacity):
     """Bytes mg_replay_store must move at minimum: every obs row once (40) + the trajectory's
     interleaved (a1, a2, done, collision) word (4: a and done are read from it) + won bits (read by
     both kernels, 2 x 1/8); per stored transition r (4) + the 88-byte row written; the terminal
-    observation of done rows (40); obs_first once per env (40)."""
-    return n * T * (40 + 4 + 0.25) + kept * (4 + 88) + done_rows * 40 + n * 40
+    observation of done rows (40); obs_first once per env (40). When one store appends more than
+    the ring holds, only the newest `capacity` rows are written (the rest would be overwritten
+    within the same store), so only those count."""
+    written = min(kept, capacity)
+    frac = written / kept if kept else 0.0
+    return n * T * (40 + 4 + 0.25) + written * (4 + 88) + done_rows * frac * 40 + n * 40
 
 
 def replay_leg(env, args, torch):
@@ -239,7 +243,7 @@ def replay_leg(env, args, torch):
     torch.cuda.synchronize()
     kept = (ring.memory_counter - c0) / L
     ms = sum(ev[2 * j].elapsed_time(ev[2 * j + 1]) for j in range(L)) / L
-    nbytes = replay_algorithmic_bytes(E, T, kept, int(traj["done"].sum().item()))
+    nbytes = replay_algorithmic_bytes(E, T, kept, int(traj["done"].sum().item()), ring.capacity)
     achieved = nbytes / (ms * 1e-3) / 1e9
     s = torch.cuda.Event(enable_timing=True)
     e = torch.cuda.Event(enable_timing=True)
