@@ -7,11 +7,17 @@ A step = one launch of mg_step_random over this rank's 2^20 envs: Philox actions
 players drawn on the device, the full reference step (merging_env.py:138-195), autoreset,
 episode statistics. Envs are sharded across ranks (rank r owns global envs [r E, (r+1) E),
 Philox keyed by the global index), with no collective inside the timed loop; after it, one
-RCCL all-gather collects the per-env episode statistics (timed separately).
+RCCL all-gather of each rank's 48-byte statistics totals (timed separately).
+
+Before the W warm-up steps the batch is burned in (--burn-in steps, untimed, fused rollout
+launches) so the timed window sees the steady state: envs finishing every step, autoreset,
+final observations and statistics writes. The K timed launches are replayed from a HIP graph
+captured beforehand (--graph 1), so the window holds the kernels back to back.
 
 Rank 0 prints ONE JSON line: value = env-steps/s over all ranks (max-over-ranks time),
 roofline = algorithmic bytes per launch / mean kernel time (HIP events on the launch stream)
-against the 8 TB/s HBM3E peak, cpu_baseline = the C oracle on the host cores (N = 1 only).
+against the 8 TB/s HBM3E peak, size_2p22 = the same kernel at 2^22 envs (past the 256 MiB
+Infinity Cache, N = 1 only), cpu_baseline = the CPU restatements on the host cores (N = 1 only).
 """
 
 from __future__ import annotations
@@ -45,7 +51,16 @@ def parse():
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, one GPU per rank) or gloo (multi-rank rehearsal, ranks may share a GPU)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--burn-in", type=int, default=320,
+                    help="untimed steps (16-step fused rollouts) before the warm-up: steady state")
+    ap.add_argument("--graph", type=int, default=1,
+                    help="1: replay the K timed launches from a HIP graph captured before the window")
+    ap.add_argument("--size2-envs", type=int, default=1 << 22,
+                    help="envs of the post-Infinity-Cache leg (N = 1 only); 0 disables it")
+    ap.add_argument("--size2-steps", type=int, default=100)
+    ap.add_argument("--gather", choices=("summary", "per-env"), default="summary",
+                    help="statistics collective: 48-byte totals per rank, or every env's row")
+    ap.add_argument("--cpu-seconds", type=float, default=6.0, help="per CPU-baseline leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="skip per-launch HIP events")
     ap.add_argument("--event-every", type=int, default=8,
@@ -64,32 +79,34 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(seconds: float):
-    """C oracle (oracle/merge_oracle.c) on the host cores: same workload, bounded sample."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import numpy as np
+def cpu_baseline(seconds: float, envs: int):
+    """The CPU restatements on the host cores (oracle/cpu_baselines.py, run as a child process
+    that never touches the GPU): the C oracle on every core of the affinity mask, the NumPy
+    restatement at the GPU batch size on one core and one process per core, the scalar list-API
+    env one process per core. `value` is the fastest all-core figure; all are reported."""
+    import subprocess
 
-    import merge_oracle
-
-    co = merge_oracle.COracle(merge_oracle.build_c_oracle())
-    cores = len(os.sched_getaffinity(0))
-    threads = max(1, min(cores, 16))
-    co.set_threads(threads)
-    n = 16384
-    envs = co.new_envs(n)
-    co.reset(envs)
-    ret_sum = np.zeros((n, 2))
-    counts = np.zeros((n, 4), np.uint32)
-    done_steps, chunk, k = 0, 25, 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        done_steps += co.rollout_random(envs, chunk, 1234, k, True, stats=(ret_sum, counts))
-        k += chunk
-    dt = time.perf_counter() - t0
-    return {"value": done_steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{n} envs x {k} autoreset steps with Philox actions (same workload as the "
-                      f"GPU line), {dt:.1f} s on {threads} of {cores} host threads, "
-                      "oracle/merge_oracle.c (OpenMP, reference QP solved per car-step)"}
+    cmd = [sys.executable, os.path.join(ROOT, "oracle", "cpu_baselines.py"), "--seconds", str(seconds),
+           "--envs", str(envs)]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    if out.returncode != 0:
+        return {"error": out.stderr[-500:]}
+    d = json.loads(out.stdout.strip().splitlines()[-1])
+    legs = {"c_oracle": d["c_oracle"], "numpy_all_cores": d["numpy"].get("all_cores", d["numpy"]["one_core"]),
+            "scalar_per_core": d["scalar"]}
+    best = max(legs, key=lambda k: legs[k]["value"])
+    c = d["cores"]
+    cores = legs[best].get("threads", legs[best].get("procs"))
+    return {"value": legs[best]["value"], "unit": "env-steps/s", "cores": cores, "kind": "port",
+            "sample": f"{best}: {legs[best]['sample']}; host affinity {c['affinity']} cores, cgroup CPU quota "
+                      f"{c['cgroup_quota']}",
+            "host_cores": c,
+            "legs": {"c_oracle_all_affinity_threads": d["c_oracle"],
+                     "numpy_2p20_one_core": d["numpy"]["one_core"],
+                     "numpy_2p20_all_cores": d["numpy"].get("all_cores"),
+                     "scalar_list_api_per_core": d["scalar"]},
+            "workload": "Philox actions for both players, autoreset (scalar: host random actions, reset "
+                        "on done); oracle/merge_oracle.c, oracle/merge_numpy.py, oracle/merge_oracle.py"}
 
 
 def load_pmc(envs: int):
@@ -98,11 +115,65 @@ def load_pmc(envs: int):
     try:
         with open(path) as f:
             d = json.load(f)
-        if int(d.get("envs", -1)) == envs:
-            return d.get("hbm_bytes_per_launch")
+        row = d.get("by_envs", {}).get(str(envs))
+        if row is None and int(d.get("envs", -1)) == envs:
+            row = d
+        return None if row is None else row.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
-        pass
-    return None
+        return None
+
+
+def burn_in(env, steps: int, seed: int, first_step: int) -> int:
+    """Untimed fused rollouts until `steps` env-steps have passed; returns the next step index."""
+    k = first_step
+    while k - first_step < steps:
+        T = min(16, steps - (k - first_step))
+        env.rollout_random(T, seed, first_step=k, final_observation=False, won_mask=False)
+        k += T
+    return k
+
+
+def capture_steps(step, first: int, count: int, torch):
+    """The `count` launches step(first), ..., step(first + count - 1) captured into one HIP graph
+    (torch.cuda.CUDAGraph over torch's capture stream, which MergeVecEnv launches on); replaying
+    it runs exactly those launches. Capture executes nothing."""
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for k in range(first, first + count):
+            step(k)
+    return g
+
+
+def size2_leg(args, torch):
+    """The step kernel past the Infinity Cache: --size2-envs envs (638 MB of state and outputs per
+    step at 2^22 > 256 MiB), burned in to the steady state, --size2-steps launches timed with HIP
+    events on the launch stream."""
+    from merging_gym import MergeVecEnv
+
+    E = args.size2_envs
+    env = MergeVecEnv(E, device=torch.device("cuda", torch.cuda.current_device()), autoreset=True,
+                      final_observation=True, episode_stats=True)
+    k = burn_in(env, args.burn_in, args.seed, 0)
+    for _ in range(5):
+        env.step_random(args.seed, step_idx=k)
+        k += 1
+    env.clear_statistics()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    ev0.record()
+    for j in range(args.size2_steps):
+        env.step_random(args.seed, step_idx=k + j)
+    ev1.record()
+    torch.cuda.synchronize()
+    kernel_ms = ev0.elapsed_time(ev1) / args.size2_steps
+    achieved = BYTES_PER_ENV_STEP * E / (kernel_ms * 1e-3) / 1e9
+    completed = int(env.counts[:, 0].sum())
+    del env
+    torch.cuda.empty_cache()
+    return {"envs": E, "steps": args.size2_steps, "burn_in_steps": args.burn_in, "kernel_ms": kernel_ms,
+            "value": E / (kernel_ms * 1e-3), "unit": "env-steps/s", "achieved": achieved, "peak": HBM_PEAK_GBPS,
+            "unit_bw": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": load_pmc(E),
+            "episodes_completed": completed}
 
 
 def rollout_leg(env, args, world, dist, torch):
@@ -319,22 +390,29 @@ def main():
                       final_observation=True, episode_stats=True)
     step = lambda k: env.step_random(args.seed, opponent_random=True, step_idx=k)  # noqa: E731
 
-    for k in range(args.warmup):
+    # steady state first: every env past its first episodes, some finishing at every step
+    k0 = burn_in(env, args.burn_in, args.seed, 0)
+    for k in range(k0, k0 + args.warmup):
         step(k)
+    k0 += args.warmup
+    graph = capture_steps(step, k0, args.steps, torch) if args.graph else None
     env.clear_statistics()
     torch.cuda.synchronize()
 
-    # Timed region: K launches back to back, bracketed by a barrier + synchronize, with one HIP
-    # event pair recorded on the stream the kernels run on (torch's current stream, which
-    # MergeVecEnv launches on). Average launch duration = region / K (launch gaps included).
+    # Timed region: K launches back to back (one graph replay, or K host launches), bracketed by
+    # a barrier + synchronize, with one HIP event pair recorded on the stream the kernels run on
+    # (torch's current stream). Average launch duration = region / K (launch gaps included).
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     ev0.record()
-    for k in range(args.steps):
-        step(args.warmup + k)
+    if graph is not None:
+        graph.replay()
+    else:
+        for k in range(k0, k0 + args.steps):
+            step(k)
     ev1.record()
     host_ms = (time.perf_counter() - t0) * 1e3 / args.steps  # host enqueue time per launch
     torch.cuda.synchronize()
@@ -342,6 +420,9 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps
+    k0 += args.steps
+    completed_in_window = int(env.counts[:, 0].sum())
+    del graph
 
     # untimed: per-dispatch durations (events written by the dispatch packets themselves,
     # hipExtLaunchKernel via mg_time_next_launch) for a sample of launches, for reference
@@ -353,30 +434,39 @@ def main():
         timer = KernelTimer(nsamp)
         for j in range(nsamp):
             timer.arm(j)
-            step(args.warmup + args.steps + j)
+            step(k0 + j)
         torch.cuda.synchronize()
         durs = timer.durations_ms()
         dispatch_ms = sum(durs) / len(durs)
         timer.close()
+        k0 += nsamp
 
     t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cpu" if host_coll else device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kernel_ms_max = float(t[0]), float(t[1])
 
-    # episode statistics: one all-gather over RCCL (xGMI), outside the timed loop
-    from merging_gym.distributed import gather_episode_stats, summarize
+    # episode statistics (every episode completed since the window opened): each rank's 48-byte
+    # totals all-gathered over RCCL (xGMI) and reduced on every rank, outside the timed loop
+    from merging_gym.distributed import (PARTIAL_BYTES, gather_episode_stats, gather_episode_summary,
+                                         summarize)
 
     torch.cuda.synchronize()
     g0 = time.perf_counter()
-    if world > 1:
-        ret_sum, counts = gather_episode_stats(env.ret_sum, env.counts)
+    if world > 1 and args.gather == "per-env":
+        episodes = summarize(*gather_episode_stats(env.ret_sum, env.counts))
+        payload = E * 32
+    elif world > 1:
+        episodes = gather_episode_summary(env.ret_sum, env.counts)
+        payload = PARTIAL_BYTES
     else:
-        ret_sum, counts = env.ret_sum, env.counts
+        episodes = summarize(env.ret_sum, env.counts)
+        payload = 0
     torch.cuda.synchronize()
     gather_ms = (time.perf_counter() - g0) * 1e3
-    episodes = summarize(ret_sum, counts)
-    episodes["allgather_ms"] = gather_ms
+    episodes.update(allgather_ms=gather_ms, allgather_bytes_per_rank=payload,
+                    completed_in_timed_window_rank0=completed_in_window,
+                    counted_since="start of the timed window (statistics cleared after the warm-up)")
 
     rollout = None
     if args.rollout_steps > 0:
@@ -388,6 +478,10 @@ def main():
     qnet = None
     if args.qnet_launches > 0 and args.rollout_steps > 0:
         qnet = [qnet_leg(env, args, world, dist, torch, opp) for opp in ("none", "self")]
+
+    size2 = None
+    if world == 1 and args.size2_envs > 0 and args.size2_envs != E:
+        size2 = size2_leg(args, torch)
 
     total_env_steps = world * E * args.steps
     value = total_env_steps / elapsed
@@ -412,13 +506,17 @@ def main():
                                     "autoreset, episode statistics"),
                        "envs_per_gpu": E, "global_envs": world * E,
                        "parallelism": f"dp{world} (env shards, no per-step collective)"},
+            "burn_in_steps": args.burn_in,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBPS) if achieved else None,
                          "traffic": pmc, "kernel": KERNEL_NAME,
                          "bytes_per_env_step": BYTES_PER_ENV_STEP,
                          "kernel_ms_mean": kernel_ms, "kernel_ms_mean_max_rank": kernel_ms_max,
-                         "timing": "HIP events recorded on the launch stream around the K timed launches, / K",
-                         "kernel_ms_dispatch_sample": dispatch_ms, "host_enqueue_ms_per_launch": host_ms},
+                         "timing": ("HIP events recorded on the launch stream around the K timed launches "
+                                    f"({'one HIP-graph replay' if args.graph else 'K host launches'}), / K"),
+                         "kernel_ms_dispatch_sample": dispatch_ms, "host_enqueue_ms_per_launch": host_ms,
+                         "wall_over_kernel": (elapsed / args.steps * 1e3) / kernel_ms if kernel_ms else None,
+                         "traffic_rule": "2 x FETCH_SIZE + WRITE_SIZE per launch, profiles/pmc_traffic.json"},
             "episodes": episodes,
         }
         if rollout is not None:
@@ -427,9 +525,11 @@ def main():
             line["replay"] = replay
         if qnet is not None:
             line["qnet_policy"] = qnet
+        if size2 is not None:
+            line["size_2p22"] = size2
         if world == 1 and not args.no_cpu_baseline:
             line["dropin_single_env"] = dropin_leg(args.seed)
-            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, E)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

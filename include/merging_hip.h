@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 6
+#define MG_ABI_VERSION 7
 #define MG_OBS_DIM 10   /* merging_env.py:75 observation_shape = (10) */
 #define MG_NUM_ACTIONS 5 /* merging_env.py:101-102 action_dict / Discrete(5) */
 #define MG_ACTION_NONE (-1) /* action2=None: the constant-speed "L0" opponent, merging_env.py:152 */
@@ -96,8 +96,16 @@ typedef struct mg_params {
   int32_t veh_h;       /* 8  longitudinal box size                    merging_env.py:40,97 */
   int32_t timeout_steps; /* 2501: first step with time_stamp > 500    merging_env.py:141-143 */
   int32_t _pad;
-  double inv_R;            /* 1 / R, rounded: the kernel divides by R and prediction_t with */
-  double inv_prediction_t; /* an FMA-corrected reciprocal multiply (still correctly rounded) */
+  double inv_R;        /* 1 / R, rounded: the kernel divides by R (and by qp_nz) with an
+                          FMA-corrected reciprocal multiply (still correctly rounded) */
+  /* mpc_1d's QP (scripts/helper.py:152-191) as the Goldfarb-Idnani solver quadprog runs it
+   * (helper.py:182): with P = D'D + 0.01 I factored by Cholesky and n = A[1] the equality's
+   * normal, z = P^-1 n and the first control is u0 = (b / n'z) * z0, b = vt - v0. The two
+   * constants depend only on prediction_t; mg_params_default computes them the solver's way,
+   * so the kernel's u0 carries the solver's rounding, not that of the closed form (vt-v0)/t. */
+  double qp_nz;        /* n'P^-1 n = 90.00000000000153 (t = 3) */
+  double qp_z0;        /* (P^-1 n)[0] = 30.000000000000544 */
+  double qp_inv_nz;    /* 1 / qp_nz, rounded */
 } mg_params;
 
 /* Per-env state, struct of arrays, n entries each (device pointers). */

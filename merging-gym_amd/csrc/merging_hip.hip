@@ -14,8 +14,11 @@
 //
 // Numerics: fp64 throughout, IEEE add/mul/div without contraction (the file is compiled
 // with -ffp-contract=off and the pragma below), so positions, speeds, arrival tests and
-// rewards are the same doubles the reference's Python floats hold. sin/cos come from the
-// device math library (<= 1 ulp); every other operation is correctly rounded.
+// rewards are the same doubles the reference's Python floats hold (mpc_1d's first control
+// carries the QP solver's own rounding, see mpc_acc). sin/cos: for |theta| < 1/16 (every
+// live-episode state) a degree-9/10 Taylor polynomial in fma form, identical to glibc's
+// sin/cos in 99.98 % of 2e7 samples and otherwise 1 ulp off; larger angles use the device
+// math library (<= 1 ulp). Every other operation is correctly rounded.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
@@ -35,12 +38,6 @@ namespace {
 #endif
 #ifndef MG_NT_STORES
 #define MG_NT_STORES 1    // non-temporal stores for the per-step outputs
-#endif
-#ifndef MG_SC1_OUT
-#define MG_SC1_OUT 0      // write-through (sc1) stores for the per-step outputs (overrides NT)
-#endif
-#ifndef MG_SC1_STATE
-#define MG_SC1_STATE 0    // write-through (sc1) stores for the env state
 #endif
 #ifndef MG_BLOCK
 #define MG_BLOCK 256
@@ -89,42 +86,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // Store of a per-step output (observation, reward, flags, actions): written once, never
 // re-read by the step, so optionally non-temporal. The env state is stored normally: the
-// next step reads it back.
-// Write-through store: leaves no dirty line in the XCD's L2 for the kernel-boundary release
-// to write back (MI355X_MICROARCH.md: sc1 stores drop the line; relaxed agent-scope atomic
-// stores lower to `global_store_* sc1`).
-template <class T>
-__device__ __forceinline__ void st_sc1(T* p, T v) {
-  if constexpr (sizeof(T) == 16) {
-    uint64_t w[2];
-    __builtin_memcpy(w, &v, 16);
-    __hip_atomic_store(reinterpret_cast<uint64_t*>(p), w[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(reinterpret_cast<uint64_t*>(p) + 1, w[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else if constexpr (sizeof(T) == 8) {
-    uint64_t w;
-    __builtin_memcpy(&w, &v, 8);
-    __hip_atomic_store(reinterpret_cast<uint64_t*>(p), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else if constexpr (sizeof(T) == 4) {
-    uint32_t w;
-    __builtin_memcpy(&w, &v, 4);
-    __hip_atomic_store(reinterpret_cast<uint32_t*>(p), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else if constexpr (sizeof(T) == 2) {
-    uint16_t w;
-    __builtin_memcpy(&w, &v, 2);
-    __hip_atomic_store(reinterpret_cast<uint16_t*>(p), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    static_assert(sizeof(T) == 1, "st_sc1: 1, 2, 4, 8 or 16 bytes");
-    uint8_t w;
-    __builtin_memcpy(&w, &v, 1);
-    __hip_atomic_store(reinterpret_cast<uint8_t*>(p), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
+// next step reads it back (write-through or non-temporal state stores measured 0 to +4 %).
 template <class T>
 __device__ __forceinline__ void st_out(T* p, T v) {
-#if MG_SC1_OUT
-  st_sc1(p, v);
-#elif MG_NT_STORES
+#if MG_NT_STORES
   __builtin_nontemporal_store(v, p);
 #else
   *p = v;
@@ -133,13 +98,7 @@ __device__ __forceinline__ void st_out(T* p, T v) {
 
 template <class T>
 __device__ __forceinline__ void st_state(T* p, T v) {
-#if MG_SC1_STATE
-  st_sc1(p, v);
-#elif MG_NT_STATE  // A/B knob: non-temporal state stores too
-  __builtin_nontemporal_store(v, p);
-#else
   *p = v;
-#endif
 }
 
 // Action codes after host/device decoding: 0..4 valid, -1 None (opponent only), anything
@@ -156,7 +115,7 @@ __device__ __forceinline__ double div_const(double x, double d, double inv) {
   return fma(r, inv, q);
 }
 
-// sin and cos of the double theta. For |theta| < 1/16 -- pos in [-842, 2875], which covers
+// sin and cos of the double theta. For |theta| < 1/16 -- pos in [-875, 2875], which covers
 // every state of a live episode (pos 50..~1000) -- a degree-9 / degree-10 Taylor polynomial
 // in fma form: the correction terms are < 7e-4 of the result, so the one rounding of the
 // final fma dominates and the result agrees with libm's sin/cos to <= 1 ulp (identical in
@@ -293,12 +252,9 @@ __device__ __forceinline__ void reset_obs(const mg_params& P, OT (&o)[kObs]) {
 }
 
 // Philox4x32-10 (Salmon et al., SC'11 "Parallel random numbers: as easy as 1, 2, 3").
-#ifndef MG_ABL_PHILOX_ROUNDS
-#define MG_ABL_PHILOX_ROUNDS 10  // timing ablations only: any other value breaks parity
-#endif
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
-  for (int r = 0; r < MG_ABL_PHILOX_ROUNDS; ++r) {
+  for (int r = 0; r < 10; ++r) {
     if (r) {
       k0 += 0x9E3779B9u;
       k1 += 0xBB67AE85u;
@@ -397,11 +353,15 @@ __device__ __forceinline__ void env_clock(const mg_params& P, Env& e) {
   if (static_cast<int32_t>(e.steps) >= P.timeout_steps) e.done = true;
 }
 
-// mpc_1d (helper.py:152-191): min u'(D'D + 0.01 I)u s.t. sum(dt u) = vt - v0 (the only row of
-// the constraint passed to solve_qp, :172-173, :182). D.1 = 0, so P.1 = 0.01 * 1 and the
-// minimiser is u = (vt - v0) / t * 1; action() = u[0].
+// mpc_1d (helper.py:152-191): min u'(D'D + 0.01 I)u s.t. A[1] u = b, b = vt - v0 (only the
+// velocity row of the constraint reaches solve_qp, :172-173, :182). The dual active-set solver
+// starts at the unconstrained minimiser u = 0 and adds the one equality in a single step,
+// u = (b / n'z) z with z = P^-1 n; action() = u[0]. n'z and z[0] are per-launch constants
+// (mg_params.qp_nz / qp_z0, computed by mg_params_default the solver's way), so this is two
+// correctly rounded operations with the solver's own rounding. (Mathematically u0 = b / t,
+// since D.1 = 0; evaluating that closed form instead moves u0 by an ulp in ~97 % of steps.)
 __device__ __forceinline__ double mpc_acc(const mg_params& P, int a, double v) {
-  return div_const(P.action_speed[a] - v, P.prediction_t, P.inv_prediction_t);
+  return div_const(P.action_speed[a] - v, P.qp_nz, P.qp_inv_nz) * P.qp_z0;
 }
 
 // v = max(0, v + acc*dT) (an int 0 when the max picks 0), p += v*dT  (:149-150, :153-154)
@@ -784,12 +744,10 @@ __global__ __launch_bounds__(kBlock, MG_STEP_WAVES_PER_EU) void step_kernel(cons
     int a1, a2;
     if constexpr (ACT == kActPhilox) {
       draw_actions(static_cast<uint64_t>(L.env_offset + i), L.step_idx, L.seed, L.opp_random, a1, a2);
-#if !MG_ABL_NO_BYTES
       if (!L.O.flags) {  // with O.flags the actions go out with done / collision below
         if (L.a1_out) st_out(L.a1_out + i, static_cast<int8_t>(a1));
         if (L.a2_out) st_out(L.a2_out + i, static_cast<int8_t>(a2));
       }
-#endif
     } else {
       a1 = L.a1[i];
       a2 = L.a2 ? static_cast<int>(L.a2[i]) : MG_ACTION_NONE;
@@ -832,16 +790,12 @@ __global__ __launch_bounds__(kBlock, MG_STEP_WAVES_PER_EU) void step_kernel(cons
         st_out(reinterpret_cast<f32x2*>(L.O.rew) + i,
                f32x2{static_cast<float>(r.r1), static_cast<float>(r.r2)});
       }
-#if !MG_ABL_NO_BYTES
       if (L.O.flags) {
         st_out(reinterpret_cast<uint32_t*>(L.O.flags) + i, pack_step_bytes(a1, a2, r.done, r.coll));
       } else {
         if (L.O.done) st_out(L.O.done + i, static_cast<uint8_t>(r.done ? 1 : 0));
         if (L.O.coll) st_out(L.O.coll + i, static_cast<uint8_t>(r.coll ? 1 : 0));
       }
-#else
-      if (a1 + a2 == 1234 && r.coll) L.O.done[0] = 1;
-#endif
       won = e.winner == 1;
       if ((L.flags & MG_AUTORESET) && r.done)
         finish_episode(P, e, r, L.St, L.O.final_obs ? L.O.final_obs + i * kObs : nullptr, i);
@@ -942,27 +896,13 @@ __global__ __launch_bounds__(kBlock, MG_ROLLOUT_WAVES_PER_EU) void rollout_kerne
       if (R.T.rew)
         st_out(reinterpret_cast<f32x2*>(R.T.rew) + row,
                f32x2{static_cast<float>(r.r1), static_cast<float>(r.r2)});
-#if !MG_ABL_NO_BYTES
       store_step_bytes(R.T, row, a1, a2, r.done, r.coll);
-#else  // timing ablation only: no byte outputs
-      if (a1 + a2 == 1234 && r.coll) R.T.rew[0] = 1.f;
-#endif
       won = e.winner == 1;
       if (autoreset && r.done)
         finish_episode(P, e, r, R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i, &sreg);
     }
     store_won_mask(R.T.won_mask, won, t, R.n, wbase, wrows);
-#if MG_ABL_NO_OBS
-    {  // keep the observation computed, never stored
-      double acc = 0.0;
-#pragma unroll
-      for (int k = 0; k < kObs; ++k) acc += r.o[k];
-      if (acc == -1.2345e300) R.T.obs[0] = 0.f;
-    }
-    if (false)
-#else
     if (R.T.obs)  // staged per wave: waves never wait for each other
-#endif
       wave_store_obs(obs_tile + (tid & ~63) * kObs, r.o,
                      R.T.obs + (static_cast<int64_t>(t) * R.n + wbase) * kObs, wrows);
   }
@@ -1312,13 +1252,8 @@ __device__ __forceinline__ void qnet_forward_swp(const uint8_t* net, const float
       const int jn = nk == 2 ? j + 1 : j + 2;
       if (jn < 8) a2n = w2frag(mt, jn);
       __builtin_amdgcn_sched_barrier(0);
-#ifdef MG_ABL_SKIP_M3  // timing ablation only: the last layer-2 row tile's MFMAs skipped (-20 %)
-      if (m2 != 3)
-#endif
-      {
-        acc2a[m2] = mfma32(a2, hb[sk], acc2a[m2]);
-        acc2b[m2] = mfma32(a2, hb[2 + sk], acc2b[m2]);
-      }
+      acc2a[m2] = mfma32(a2, hb[sk], acc2a[m2]);
+      acc2b[m2] = mfma32(a2, hb[2 + sk], acc2b[m2]);
       if (more) {
 #pragma unroll
         for (int pp = 2 * j; pp < 2 * j + 2; ++pp) {
@@ -1605,10 +1540,6 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
 #pragma unroll 1
         for (int tt = 0; tt < kTiles; ++tt) {
           const int row0 = (p & 1) * kHalf + (4 * tt + wave) * 64;
-#if MG_ABL_WS_NOQ  // timing ablation only: the Q-net waves skip the forward
-          greedy[0][row0 + lane] = static_cast<uint8_t>(tile[(row0 + lane) * kObs] > 0.f ? 1 : 3);
-          continue;
-#endif
           float q[8];
           qnet_forward_ws(lds_net, tile, row0, false, q);
           greedy[0][row0 + lane] = static_cast<uint8_t>(argmax_first(q, R.out_dim));
@@ -1647,17 +1578,11 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
         greedy2[j] = OPP == 2 ? greedy[1][local0 + 64 * j + lane] : 0;
       }
       bool won[kIlp];
-#if MG_ABL_WS_NOENV  // timing ablation only: the env waves skip the step
-#pragma unroll
-      for (int j = 0; j < kIlp; ++j) won[j] = false;
-      if (greedy1[0] + greedy2[0] == 1000) R.T.done[0] = 0;
-#else
       // wave-uniform branch: each group's envs stay in named registers
       if (g == 0)
         qnet_policy_step_n<OPP, kIlp>(R, e0, r, base + local0 + lane, live0, t, greedy1, greedy2, won);
       else
         qnet_policy_step_n<OPP, kIlp>(R, e1, r, base + local0 + lane, live1, t, greedy1, greedy2, won);
-#endif
       const int64_t wbase = base + local0;
 #pragma unroll
       for (int j = 0; j < kIlp; ++j) {
@@ -2107,6 +2032,50 @@ int launch_rollout(const Rollout& R, hipStream_t stream) {
   return finish_launch("mg_rollout_random");
 }
 
+// The constants of mpc_1d's equality step (helper.py:152-191), computed in the order the
+// solver computes them (file compiled without contraction): the horizon's 10 controls of
+// dt = t / 10; the constraint normal n = A[1] = (dt, ..., dt) (the velocity row of
+// [a^9 b, ..., a b, b], a = [[1, dt], [0, 1]], b = [0, dt]); P = D'D + 0.01 I with D the
+// 9 x 10 first-difference operator, factored P = L L' column by column; z = L'^-1 L^-1 n by
+// forward then back substitution; nz = sum_i n_i z_i in index order.
+void mpc_qp_constants(double t, double* nz_out, double* z0_out) {
+  constexpr int kT = 10;
+  const double dt = t / kT;
+  double n[kT], P[kT][kT] = {}, L[kT][kT] = {}, y[kT], z[kT];
+  for (int i = 0; i < kT; ++i) n[i] = 0.0 * 0.0 + 1.0 * dt;  // row [0 1] of a^k times b
+  for (int i = 0; i + 1 < kT; ++i) {
+    P[i][i] += 1.0;
+    P[i + 1][i + 1] += 1.0;
+    P[i][i + 1] -= 1.0;
+    P[i + 1][i] -= 1.0;
+  }
+  for (int i = 0; i < kT; ++i) P[i][i] += 0.01;
+  for (int j = 0; j < kT; ++j) {
+    double d = P[j][j];
+    for (int k = 0; k < j; ++k) d -= L[j][k] * L[j][k];
+    L[j][j] = std::sqrt(d);
+    for (int i = j + 1; i < kT; ++i) {
+      double v = P[i][j];
+      for (int k = 0; k < j; ++k) v -= L[i][k] * L[j][k];
+      L[i][j] = v / L[j][j];
+    }
+  }
+  for (int i = 0; i < kT; ++i) {
+    double v = n[i];
+    for (int k = 0; k < i; ++k) v -= L[i][k] * y[k];
+    y[i] = v / L[i][i];
+  }
+  for (int i = kT - 1; i >= 0; --i) {
+    double v = y[i];
+    for (int k = i + 1; k < kT; ++k) v -= L[k][i] * z[k];
+    z[i] = v / L[i][i];
+  }
+  double nz = 0.0;
+  for (int i = 0; i < kT; ++i) nz += n[i] * z[i];
+  *nz_out = nz;
+  *z0_out = z[0];
+}
+
 }  // namespace
 
 extern "C" {
@@ -2145,7 +2114,8 @@ void mg_params_default(mg_params* p) {
   p->veh_h = 8;
   p->timeout_steps = 2501;
   p->inv_R = 1.0 / p->R;
-  p->inv_prediction_t = 1.0 / p->prediction_t;
+  mpc_qp_constants(p->prediction_t, &p->qp_nz, &p->qp_z0);
+  p->qp_inv_nz = 1.0 / p->qp_nz;
 }
 
 int mg_step(const mg_params* params, const mg_state* state, const int8_t* a1, const int8_t* a2,

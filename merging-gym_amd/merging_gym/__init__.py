@@ -23,16 +23,29 @@ ENV_IDS = {
     "merging_env_extend-v0": "merging_gym.envs:MergeEnvExtend",
 }
 
-try:  # pragma: no cover - gym is not installed in this image
-    from gym.envs.registration import register as _register
 
-    for _id, _entry in ENV_IDS.items():
-        try:
-            _register(id=_id, entry_point=_entry)
-        except Exception:  # noqa: BLE001 - already registered
-            pass
-except Exception:  # noqa: BLE001
-    pass
+def register_with_gym(registration=None):
+    """Register ENV_IDS with gym (merging_gym/__init__.py:3-11 in the reference). Runs at import
+    when gym is importable; an id gym already holds (a re-import) is skipped, and any other
+    failure propagates. Returns the ids registered by this call."""
+    if registration is None:
+        from gym.envs import registration
+    known = getattr(registration.registry, "env_specs", registration.registry)  # gym 0.20 / >= 0.26
+    added = []
+    for env_id, entry in ENV_IDS.items():
+        if env_id in known:
+            continue
+        registration.register(id=env_id, entry_point=entry)
+        added.append(env_id)
+    return added
+
+
+try:
+    import gym as _gym  # noqa: F401
+except ImportError:  # this image has no gym: merging_gym.make() builds the same envs
+    _gym = None
+if _gym is not None:
+    register_with_gym()
 
 
 def make(env_id: str, **kwargs):

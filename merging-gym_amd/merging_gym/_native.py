@@ -15,7 +15,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libmerging_hip.so"
 LIB_PATH = os.environ.get("MERGING_HIP_LIB", os.path.join(_HERE, LIB_NAME))
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 OBS_DIM = 10
 NUM_ACTIONS = 5
@@ -41,7 +41,8 @@ class Params(_c.Structure):
         "time_penalty", "start_point", "end_point", "start_vel", "vel_ref", "prediction_t",
         "angle0")] + [("action_speed", _c.c_double * NUM_ACTIONS), ("veh_w", _c.c_int32),
                       ("veh_h", _c.c_int32), ("timeout_steps", _c.c_int32), ("_pad", _c.c_int32),
-                      ("inv_R", _c.c_double), ("inv_prediction_t", _c.c_double)]
+                      ("inv_R", _c.c_double), ("qp_nz", _c.c_double), ("qp_z0", _c.c_double),
+                      ("qp_inv_nz", _c.c_double)]
 
 
 class State(_c.Structure):

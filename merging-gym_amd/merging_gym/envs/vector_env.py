@@ -130,7 +130,7 @@ class MergeVecEnv:
         self.single_observation_space = spaces.observation_space()
         self.single_action_space = spaces.action_space()
         self.observation_space = spaces.batched_observation_space(n)
-        self.action_space = self.single_action_space
+        self.action_space = spaces.batched_action_space(n)
         self.reset()
 
     # ------------------------------------------------------------------ helpers

@@ -81,6 +81,39 @@ def action_space(n=5):
     return Discrete(n)
 
 
+class MultiDiscrete:
+    """gym.spaces.MultiDiscrete stand-in: one Discrete(n) per entry of nvec."""
+
+    def __init__(self, nvec):
+        self.nvec = np.asarray(nvec, dtype=np.int64)
+        self.shape = self.nvec.shape
+        self.dtype = np.dtype(np.int64)
+        self._rng = np.random.default_rng()
+
+    def sample(self):
+        return self._rng.integers(0, self.nvec).astype(self.dtype)
+
+    def contains(self, x):
+        x = np.asarray(x)
+        return x.shape == self.shape and np.issubdtype(x.dtype, np.integer) and bool(
+            np.all((x >= 0) & (x < self.nvec)))
+
+    def seed(self, seed=None):
+        self._rng = np.random.default_rng(seed)
+        return [seed]
+
+    def __repr__(self):
+        return f"MultiDiscrete({self.nvec.tolist() if self.nvec.size <= 8 else self.shape})"
+
+
+def batched_action_space(num_envs, n=5):
+    """gym 0.20's batch_space(Discrete(n), num_envs): MultiDiscrete([n] * num_envs), one ego
+    action per env (the opponent's actions are step()'s second argument)."""
+    if _gym_spaces is not None:  # pragma: no cover
+        return _gym_spaces.MultiDiscrete(np.full(num_envs, n))
+    return MultiDiscrete(np.full(num_envs, n))
+
+
 def batched_observation_space(num_envs):
     low = np.tile(OBS_LOW, (num_envs, 1))
     high = np.tile(OBS_HIGH, (num_envs, 1))

@@ -238,6 +238,11 @@ static void finish_episode(oracle_env* e, int coll, double* o, double* fobs, dou
 }
 
 /* ------------------------------------------------------------------ Philox4x32-10 */
+/* mpc_1d(x0, v0, xt, vt, t).action() for tests: the QP solved from scratch (helper.py:152-191) */
+double oracle_mpc_first_accel(double x0, double v0, double xt, double vt, double t) {
+  return mpc_first_accel(x0, v0, xt, vt, t);
+}
+
 void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
   uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3], k0 = key[0], k1 = key[1];
   for (int r = 0; r < 10; ++r) {

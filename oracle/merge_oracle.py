@@ -243,6 +243,8 @@ class COracle:
         lib.oracle_rollout_random.restype = ctypes.c_int64
         lib.oracle_philox_batch.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint64,
                                             P(ctypes.c_uint32)]
+        lib.oracle_mpc_first_accel.argtypes = [ctypes.c_double] * 5
+        lib.oracle_mpc_first_accel.restype = ctypes.c_double
         lib.oracle_set_threads.argtypes = [ctypes.c_int32]
         lib.oracle_max_threads.restype = ctypes.c_int32
         self.lib = lib
@@ -282,6 +284,10 @@ class COracle:
             _ptr(ret_sum, ctypes.c_double), _ptr(counts, ctypes.c_uint32),
             _ptr(status, ctypes.c_uint32), 0)
         return obs, rew, done, coll, status, fobs, err
+
+    def mpc_first_accel(self, x0, v0, xt, vt, t=3.0):
+        """mpc_1d(x0, v0, xt, vt, t).action() with the QP solved in C (helper.py:152-191)."""
+        return float(self.lib.oracle_mpc_first_accel(x0, v0, xt, vt, t))
 
     def philox(self, ctr, key):
         c = np.ascontiguousarray(ctr, np.uint32)

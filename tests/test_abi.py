@@ -35,8 +35,8 @@ def test_library_exports_every_declared_symbol():
 def test_struct_layouts_match_header():
     from merging_gym import _native
 
-    # mg_params: 15 doubles + 5 doubles + 4 int32 + 2 doubles; mg_rec64: 20 doubles + 2 uint32
-    assert ctypes.sizeof(_native.Params) == 20 * 8 + 16 + 16
+    # mg_params: 15 doubles + 5 doubles + 4 int32 + 4 doubles; mg_rec64: 20 doubles + 2 uint32
+    assert ctypes.sizeof(_native.Params) == 20 * 8 + 16 + 32
     assert ctypes.sizeof(_native.State) == 7 * 8
     assert ctypes.sizeof(_native.Outputs) == 10 * 8
     assert ctypes.sizeof(_native.Traj) == 9 * 8
@@ -58,7 +58,30 @@ def test_default_params_are_the_reference_constants():
     assert list(p.action_speed) == [0.0, 10.0, 20.0, 30.0, 40.0]
     assert (p.veh_w, p.veh_h, p.timeout_steps) == (4, 8, 2501)
     assert p.angle0 == float(np.arctan2(1000, 30000))
-    assert p.inv_R == 1.0 / 30000.0 and p.inv_prediction_t == 1.0 / 3.0
+    assert p.inv_R == 1.0 / 30000.0
+    # mpc_1d's equality step (helper.py:152-191): n'P^-1 n and (P^-1 n)[0] for t = 3
+    assert (p.qp_nz, p.qp_z0) == (90.00000000000153, 30.000000000000544)
+    assert p.qp_inv_nz == 1.0 / p.qp_nz
+
+
+def test_qp_step_constants_reproduce_the_oracle_qp(coracle, golden):
+    """The kernel's u0 = (b / qp_nz) * qp_z0, b = vt - v0 (merging_hip.hip mpc_acc), is bit for
+    bit the first control of the oracle's full QP solve (Cholesky + the equality step), on the
+    golden mpc inputs and on every (action, speed) pair a step can meet."""
+    import numpy as np
+
+    from merging_gym import _native
+
+    p = _native.default_params()
+    rng = np.random.default_rng(5)
+    cases = list(zip(golden["mpc_x0"], golden["mpc_v0"], golden["mpc_vt"]))
+    cases += [(float(x), float(v), 10.0 * a) for x, v, a in
+              zip(rng.uniform(0, 1100, 4000), np.concatenate([rng.uniform(0, 45, 3000),
+                                                              rng.uniform(0, 1e-3, 1000)]),
+                  rng.integers(0, 5, 4000))]
+    for x0, v0, vt in cases:
+        ref = coracle.mpc_first_accel(float(x0), float(v0), 0.0, float(vt), 3.0)
+        assert ((float(vt) - float(v0)) / p.qp_nz) * p.qp_z0 == ref, (x0, v0, vt)
 
 
 def test_argument_errors_without_gpu():

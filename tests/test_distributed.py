@@ -47,3 +47,39 @@ def test_gather_episode_stats_gloo(tmp_path):
     assert torch.equal(res["cnt"], torch.cat(exp_cnt))
     s = summarize(res["ret"], res["cnt"])
     assert s["completed"] == int(torch.cat(exp_cnt)[:, 0].sum())
+
+
+def _summary_worker(rank, world, port, n_per_rank, out_path):
+    from merging_gym.distributed import PARTIAL_BYTES, gather_episode_summary, partial_stats
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = torch.Generator().manual_seed(10 + rank)
+    ret = torch.randn((n_per_rank, 2), generator=g, dtype=torch.float64)
+    cnt = torch.randint(0, 100, (n_per_rank, 4), generator=g, dtype=torch.int32)
+    assert partial_stats(ret, cnt).numel() * 8 == PARTIAL_BYTES
+    s = gather_episode_summary(ret, cnt)
+    torch.save(s, out_path + f".{rank}")
+    dist.destroy_process_group()
+
+
+def test_gather_episode_summary_gloo(tmp_path):
+    """The default collective: 48 bytes per rank, every rank gets the global summary, equal to
+    summarizing the concatenated per-env statistics (counts exactly, returns to fp64 rounding)."""
+    world, n = 2, 1500
+    out = str(tmp_path / "s")
+    port = 30500 + (os.getpid() % 1000)
+    mp.start_processes(_summary_worker, args=(world, port, n, out), nprocs=world, start_method="spawn")
+    got = [torch.load(out + f".{r}", weights_only=True) for r in range(world)]
+    assert got[0] == got[1]
+    rets, cnts = [], []
+    for r in range(world):
+        g = torch.Generator().manual_seed(10 + r)
+        rets.append(torch.randn((n, 2), generator=g, dtype=torch.float64))
+        cnts.append(torch.randint(0, 100, (n, 4), generator=g, dtype=torch.int32))
+    exp = summarize(torch.cat(rets), torch.cat(cnts))
+    for k, v in exp.items():
+        if k == "completed":
+            assert got[0][k] == v
+        else:
+            assert abs(got[0][k] - v) <= 1e-12 * max(1.0, abs(v)), k

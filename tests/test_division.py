@@ -1,4 +1,4 @@
-"""The kernel divides by R = 30000 and prediction_t = 3 as q = x*inv; r = fma(-q, d, x);
+"""The kernel divides by R = 30000 and by the QP constant n'P^-1 n = 90.00000000000153 as q = x*inv; r = fma(-q, d, x);
 fma(r, inv, q) (merging_hip.hip div_const). Check on the host that this is the correctly
 rounded quotient x / d, as the reference's Python division is."""
 
@@ -12,7 +12,8 @@ libm.fma.restype = ctypes.c_double
 libm.fma.argtypes = [ctypes.c_double] * 3
 
 
-@pytest.mark.parametrize("d,lo,hi", [(3.0, -45.0, 45.0), (30000.0, -5e3, 2e5)])
+@pytest.mark.parametrize("d,lo,hi", [(3.0, -45.0, 45.0), (30000.0, -5e3, 2e5),
+                                     (90.00000000000153, -45.0, 45.0)])
 def test_fma_corrected_division_is_correctly_rounded(d, lo, hi):
     rng = np.random.default_rng(int(d))
     xs = np.concatenate([rng.uniform(lo, hi, 60000),

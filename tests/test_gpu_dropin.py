@@ -1,11 +1,13 @@
 """Drop-in parity: merging_gym.make("merging_env-v0") (GPU-backed, list API) replays the
-reference's own traces (tests/golden) -- values, flags and Python value types."""
+reference's own traces (tests/golden) -- values, flags and Python value types. Flags are exact
+everywhere (the post-done merge-zone steps of the "past" trace included); floats agree to 1e-9
+(the golden traces were recorded with a KKT stand-in for quadprog, whose last bits differ from
+the Goldfarb-Idnani step the kernel reproduces)."""
 
 import numpy as np
 import pytest
 
 import merge_oracle as mo
-from test_gpu_parity import merge_zone
 
 pytestmark = pytest.mark.gpu
 
@@ -33,20 +35,15 @@ def env():
 @pytest.mark.parametrize("trace", TRACES)
 def test_replay_reference_trace(env, golden, trace):
     g = {k[len(trace) + 1:]: golden[k] for k in golden.files if k.startswith(trace + "_")}
-    flips = 0.0
     for k in range(len(g["a1"])):
         if g["reset"][k]:
             obs, rew, done, coll = env.reset(), [0.0, 0.0], False, False
-            flips = 0.0
         else:
             a2 = int(g["a2"][k])
             obs, rew, done, info = env.step(int(g["a1"][k]), None if a2 < 0 else a2)
             coll = info["collision"]
         assert isinstance(obs, list) and len(obs) == 10
-        if coll != bool(g["coll"][k]):
-            assert merge_zone(g["pos"][k][0], g["pos"][k][1]) and g["done"][k - 1], (trace, k)
-            flips += 10.0 if coll else -10.0
-            continue
+        assert coll == bool(g["coll"][k]), (trace, k)  # exact, the post-done merge zone included
         assert bool(done) == bool(g["done"][k]), (trace, k)
         assert (0 if env.winner is None else env.winner) == g["winner"][k], (trace, k)
         assert _types(obs, rew) == g["types"][k], (trace, k)
@@ -54,7 +51,7 @@ def test_replay_reference_trace(env, golden, trace):
         np.testing.assert_allclose(np.asarray(rew, float), g["rew"][k], rtol=0, atol=1e-9)
         np.testing.assert_allclose([env.state1["pos"], env.state2["pos"]], g["pos"][k], rtol=0, atol=1e-9)
         np.testing.assert_allclose([env.state1["acc"], env.state2["acc"]], g["acc"][k], rtol=0, atol=1e-9)
-        np.testing.assert_allclose([env.r1_accumulate - flips, env.r2_accumulate - flips], g["racc"][k],
+        np.testing.assert_allclose([env.r1_accumulate, env.r2_accumulate], g["racc"][k],
                                    rtol=0, atol=1e-9)
         assert env.time_stamp == g["time"][k]
 
@@ -64,7 +61,6 @@ def test_assigned_state_reaches_the_device(env, golden):
     ts = [0.0]
     for _ in range(2700):
         ts.append(ts[-1] + 0.2)
-    zone = merge_zone(golden["one_p"][:, 0], golden["one_p"][:, 1])
     for r in range(0, len(golden["one_a1"]), 13):
         env.reset()
         env.state1 = {"pos": float(golden["one_p"][r, 0]), "vel": float(golden["one_v"][r, 0]), "acc": 0.0}
@@ -76,9 +72,7 @@ def test_assigned_state_reaches_the_device(env, golden):
         env.r1_accumulate, env.r2_accumulate = map(float, golden["one_racc"][r])
         a2 = int(golden["one_a2"][r])
         obs, rew, done, info = env.step(int(golden["one_a1"][r]), None if a2 < 0 else a2)
-        if info["collision"] != bool(golden["one_coll"][r]):
-            assert zone[r], r
-            continue
+        assert info["collision"] == bool(golden["one_coll"][r]), r
         assert done == bool(golden["one_done_out"][r]), r
         np.testing.assert_allclose(obs, golden["one_obs"][r], rtol=0, atol=1e-9)
         np.testing.assert_allclose(rew, golden["one_rew"][r], rtol=0, atol=1e-9)
@@ -125,3 +119,38 @@ def test_action_types_accepted_like_dict_lookup(env):
         o, r, d, i = env.step(a1, a2)
         ro, rr, rd, ri = ref.step(int(a1), None if a2 is None else int(a2))
         np.testing.assert_allclose(o, ro, rtol=0, atol=1e-9)
+
+
+def test_gym_make_drives_the_gpu_env():
+    """gym.make("merging_env-v0").unwrapped through merging_gym's own registration (the gym 0.20
+    stand-in of tests/stubs on the path), as scripts/hdqn.py:26-33 / main.py:20-26 build it:
+    a 200-step random episode equals the oracle's, value for value."""
+    import os
+    import subprocess
+    import sys
+
+    from conftest import ROOT
+
+    code = r'''
+import gym, numpy as np, merging_gym, merge_oracle as mo
+env = gym.make("merging_env-v0").unwrapped
+assert type(env).__module__.startswith("merging_gym") and env.action_space.n == 5
+ref = mo.PyMergeEnv()
+assert env.reset() == ref.reset()
+rng = np.random.default_rng(8)
+for k in range(200):
+    a1, a2 = int(rng.integers(5)), (None if k % 5 == 0 else int(rng.integers(5)))
+    o, r, d, i = env.step(a1, a2)
+    ro, rr, rd, ri = ref.step(a1, a2)
+    np.testing.assert_allclose(o, ro, rtol=0, atol=1e-9)
+    np.testing.assert_allclose(r, rr, rtol=0, atol=1e-9)
+    assert (d, i, env.winner) == (rd, ri, ref.winner), k
+    if d:
+        env.reset(); ref.reset()
+print("ok")
+'''
+    env = dict(os.environ)
+    env["PYTHONPATH"] = os.pathsep.join([os.path.join(ROOT, "tests", "stubs"), os.path.join(ROOT, "merging-gym_amd"),
+                                         os.path.join(ROOT, "oracle")])
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0 and out.stdout.strip().endswith("ok"), out.stderr[-3000:]

@@ -164,8 +164,8 @@ def test_rollout_qnet_policy_and_transitions(torch, coracle, nets, opponent, n):
         d = o_done.astype(bool)
         np.testing.assert_allclose(traj["final_observation"][t][d], o_fobs[d].astype(np.float32), **OBS_TOL)
         obs_in = traj["obs"][t]
-    np.testing.assert_allclose(env.p1.cpu().numpy(), envs["pos1"], rtol=0, atol=1e-9)
-    np.testing.assert_allclose(env.ret2.cpu().numpy(), envs["r2_acc"], rtol=0, atol=1e-9)
+    np.testing.assert_array_equal(env.p1.cpu().numpy(), envs["pos1"])
+    np.testing.assert_array_equal(env.ret2.cpu().numpy(), envs["r2_acc"])
     assert env._step_idx == k0 + T
 
 
@@ -215,7 +215,7 @@ def test_rollout_qnet_invalid_greedy_actions(torch, coracle, nets, opponent):
         np.testing.assert_allclose(traj["final_observation"][t][d], o_fobs[d].astype(np.float32), **OBS_TOL)
     for name, src in (("pos1", env.p1), ("vel1", env.v1), ("pos2", env.p2), ("vel2", env.v2),
                       ("r1_acc", env.ret1), ("r2_acc", env.ret2)):
-        np.testing.assert_allclose(src.cpu().numpy(), envs[name], rtol=0, atol=1e-9, err_msg=name)
+        np.testing.assert_array_equal(src.cpu().numpy(), envs[name], err_msg=name)
     np.testing.assert_array_equal(env.steps.cpu().numpy(), np.minimum(envs["steps"], 0x1FFF))
     np.testing.assert_array_equal(env.winner.cpu().numpy(), envs["winner"])
 
@@ -225,3 +225,79 @@ def test_greedy_threshold_is_phi_of_episilo():
 
     assert greedy_threshold(0.7) == round(0.7580363477769270 * 2**32)
     assert greedy_threshold(50.0) == 2**32 and greedy_threshold(-50.0) == 0
+
+
+@pytest.mark.parametrize("opponent", ["none", "self"])
+def test_rollout_qnet_full_size(torch, coracle, nets, opponent):
+    """BASELINE config 5 at its own size: 2^20 envs x 16 steps in one launch (the kernel's
+    1,024-env blocks, both pipelined groups and the [T, N, .] trajectory indexing at full size).
+    Whole batch: actions in range, flags 0/1, no NaN, the step bookkeeping. 2,048 sampled global
+    env indices: every action is the epsilon-greedy choice (Philox draws exact, greedy = argmax
+    of the bf16 reference except near-ties) and every transition equals the C oracle's,
+    state bit for bit. Reference: scripts/main.py:99-112 (choose_action), :189-220 (the loop)."""
+    from merging_gym import MergeVecEnv
+    from merging_gym.policy import QNet, greedy_threshold
+
+    n, T, seed, k0, burn = 1 << 20, 16, 41, 900, 60
+    qnet = QNet.from_state_dict(nets["l1"], device="cuda:0")
+    env = MergeVecEnv(n, device="cuda:0")
+    for k in range(burn):  # mid-episode start, some envs already finished once
+        env.step_random(seed + 1, step_idx=k)
+    idx_np = np.sort(np.random.default_rng(3).choice(n, 2048, replace=False))
+    idx = torch.from_numpy(idx_np).cuda()
+    envs = coracle.new_envs(len(idx_np))
+    for name, src in (("pos1", env.p1), ("vel1", env.v1), ("pos2", env.p2), ("vel2", env.v2),
+                      ("r1_acc", env.ret1), ("r2_acc", env.ret2)):
+        envs[name] = src[idx].cpu().numpy()
+    envs["steps"] = env.steps[idx].cpu().numpy()
+    envs["winner"] = env.winner[idx].cpu().numpy()
+    envs["time_stamp"] = np.cumsum(np.full(2700, 0.2))[np.maximum(envs["steps"] - 1, 0)] * (envs["steps"] > 0)
+    obs_in = env.observe()[idx].cpu().numpy().copy()
+    ret_sum0, counts0 = env.ret_sum[idx].cpu().numpy(), env.counts[idx].cpu().numpy().astype(np.uint32)
+
+    traj = env.rollout_qnet(T, qnet, seed, opponent=opponent, first_step=k0)
+    # whole batch
+    a1, a2 = traj["a1"], traj["a2"]
+    assert int(a1.min()) >= 0 and int(a1.max()) <= 4
+    if opponent == "none":
+        assert bool((a2 == -1).all())
+    else:
+        assert int(a2.min()) >= 0 and int(a2.max()) <= 4
+    assert int(traj["flags"][..., 2:].max()) <= 1
+    assert not bool(torch.isnan(traj["obs"]).any()) and not bool(torch.isnan(traj["rew"]).any())
+    counts = env.counts.to(torch.int64)
+    assert bool((counts[:, 3] + env.steps.to(torch.int64) == burn + T).all())
+    assert int(traj["done"].sum()) > 1000  # episodes ended inside the window (autoreset path ran)
+    # sampled envs, step by step against the bf16 reference policy and the C oracle
+    sub = {k: (v[:, idx].cpu().numpy() if v is not None and v.dim() >= 2 and v.shape[1] == n else None)
+           for k, v in traj.items()}
+    thr = greedy_threshold(0.7)
+    stats = (ret_sum0.copy(), counts0.copy())
+    for t in range(T):
+        u = np.stack([coracle.philox_batch(1, int(gi), seed, k0 + t)[0] for gi in idx_np])
+        q = mo.qnet_reference(nets["l1"], obs_in, bf16=True)
+        greedy = u[:, 0].astype(np.uint64) < thr
+        exp1 = np.where(greedy, q.argmax(1), (u[:, 1].astype(np.uint64) * 5) >> 32)
+        ok1 = (sub["a1"][t] == exp1) | (greedy & _near_tie(q))
+        assert ok1.all(), (t, idx_np[~ok1][:5])
+        rnd2 = (u[:, 3].astype(np.uint64) * 5) >> 32
+        if opponent == "self":
+            q2 = mo.qnet_reference(nets["l1"], obs_in, bf16=True, swap=True)
+            g2 = u[:, 2].astype(np.uint64) < thr
+            ok2 = (sub["a2"][t] == np.where(g2, q2.argmax(1), rnd2)) | (g2 & _near_tie(q2))
+            assert ok2.all(), t
+        o_obs, o_rew, o_done, o_coll, _, o_fobs, err = coracle.step(
+            envs, sub["a1"][t], sub["a2"][t], autoreset=True, final_obs=True, stats=stats)
+        assert err == 0
+        np.testing.assert_array_equal(sub["done"][t], o_done.astype(bool), err_msg=str(t))
+        np.testing.assert_array_equal(sub["collision"][t], o_coll.astype(bool), err_msg=str(t))
+        np.testing.assert_allclose(sub["obs"][t], o_obs.astype(np.float32), **OBS_TOL)
+        np.testing.assert_allclose(sub["rew"][t], o_rew.astype(np.float32), **OBS_TOL)
+        d = o_done.astype(bool)
+        np.testing.assert_allclose(sub["final_observation"][t][d], o_fobs[d].astype(np.float32), **OBS_TOL)
+        obs_in = sub["obs"][t]
+    for name, src in (("pos1", env.p1), ("vel1", env.v1), ("pos2", env.p2), ("vel2", env.v2),
+                      ("r1_acc", env.ret1), ("r2_acc", env.ret2)):
+        np.testing.assert_array_equal(src[idx].cpu().numpy(), envs[name], err_msg=name)
+    np.testing.assert_array_equal(env.counts[idx].cpu().numpy().astype(np.uint32), stats[1])
+    np.testing.assert_array_equal(env.ret_sum[idx].cpu().numpy(), stats[0])

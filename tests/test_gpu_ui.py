@@ -6,7 +6,7 @@ same resets and steps run through the HIP step kernel, and each UI call draws th
 back from the device -- MergeEnv's step record, and row 0 of an 8-env MergeVecEnv stepped with
 the same actions -- through the same recording stand-in. Text and structure must be
 identical; coordinates agree to 1e-9 relative (the device state equals the reference's
-fp64 state up to the closed-form QP's last-bit rounding).
+fp64 state up to the last-bit rounding of the QP stand-in the golden traces were recorded with).
 """
 
 import json

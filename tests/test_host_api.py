@@ -51,3 +51,74 @@ def test_extend_env_is_the_print_stub(capsys):
     e.reset()
     e.step()
     assert "MergeEnvExtend" in capsys.readouterr().out
+
+
+def _stub_env():
+    import os
+    import sys
+
+    from conftest import ROOT
+
+    env = dict(os.environ)
+    env["PYTHONPATH"] = os.pathsep.join([os.path.join(ROOT, "tests", "stubs"),
+                                         os.path.join(ROOT, "merging-gym_amd")])
+    return sys.executable, env
+
+
+def test_gym_registration_through_the_package_import():
+    """With gym importable (the gym 0.20 stand-in in tests/stubs), importing merging_gym runs
+    its registration: the reference's ids resolve to the env classes, re-importing skips ids gym
+    already holds instead of failing, and gym.make builds the env (here without a GPU, so the
+    GPU-backed MergeEnv refuses loudly -- the drop-in itself is driven by test_gpu_dropin)."""
+    import subprocess
+
+    code = r'''
+import importlib, gym, merging_gym
+specs = gym.envs.registration.registry.env_specs
+assert {k: v.entry_point for k, v in specs.items()} == merging_gym.ENV_IDS, specs
+assert merging_gym.register_with_gym() == []          # already there: skipped
+importlib.reload(merging_gym)                         # a second import does not raise
+from merging_gym.envs import MergeEnv
+mod, attr = gym.spec("merging_env-v0").entry_point.split(":")
+assert getattr(importlib.import_module(mod), attr) is MergeEnv
+ext = gym.make("merging_env_extend-v0").unwrapped
+assert type(ext).__name__ == "MergeEnvExtend"
+import torch
+if not torch.cuda.is_available():
+    try:
+        gym.make("merging_env-v0")
+    except RuntimeError as e:
+        assert "no CPU fallback" in str(e)
+    else:
+        raise AssertionError("MergeEnv built without a GPU")
+print("ok")
+'''
+    exe, env = _stub_env()
+    out = subprocess.run([exe, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0 and out.stdout.strip().endswith("ok"), out.stderr[-2000:]
+
+
+def test_registration_errors_propagate():
+    """Only an id gym already holds is skipped; any other registration failure is raised."""
+    import types
+
+    calls = []
+
+    def register(id, entry_point):
+        calls.append(id)
+        raise ValueError("broken registry")
+
+    fake = types.SimpleNamespace(registry={"merging-v0": object()}, register=register)
+    with pytest.raises(ValueError, match="broken registry"):
+        merging_gym.register_with_gym(fake)
+    assert calls == ["merging_env-v0"]
+    ok = types.SimpleNamespace(registry={}, register=lambda id, entry_point: calls.append(id))
+    calls.clear()
+    assert merging_gym.register_with_gym(ok) == list(merging_gym.ENV_IDS) == calls
+
+
+def test_batched_action_space():
+    sp = spaces.batched_action_space(6)
+    assert sp.shape == (6,) and (sp.nvec == 5).all()
+    a = sp.sample()
+    assert sp.contains(a) and not sp.contains(np.full(6, 5)) and not sp.contains(np.zeros(5, np.int64))
