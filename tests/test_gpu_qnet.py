@@ -238,7 +238,7 @@ def test_rollout_qnet_full_size(torch, coracle, nets, opponent):
     from merging_gym import MergeVecEnv
     from merging_gym.policy import QNet, greedy_threshold
 
-    n, T, seed, k0, burn = 1 << 20, 16, 41, 900, 60
+    n, T, seed, k0, burn = 1 << 20, 16, 41, 900, 240
     qnet = QNet.from_state_dict(nets["l1"], device="cuda:0")
     env = MergeVecEnv(n, device="cuda:0")
     for k in range(burn):  # mid-episode start, some envs already finished once
