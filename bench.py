@@ -10,9 +10,10 @@ Philox keyed by the global index), with no collective inside the timed loop; aft
 RCCL all-gather of each rank's 48-byte statistics totals (timed separately).
 
 Before the W warm-up steps the batch is burned in (--burn-in steps, untimed, fused rollout
-launches) so the timed window sees the steady state: envs finishing every step, autoreset,
-final observations and statistics writes. The K timed launches are replayed from a HIP graph
-captured beforehand (--graph 1), so the window holds the kernels back to back.
+launches, then --burn-in-launches untimed one-step launches) so the timed window sees the
+steady state: envs finishing every step, autoreset, final observations and statistics writes.
+The K timed launches are host launches (the host enqueues one in ~4 us, the kernel takes ~25),
+or a HIP-graph replay with --graph 1.
 
 Rank 0 prints ONE JSON line: value = env-steps/s over all ranks (max-over-ranks time),
 roofline = algorithmic bytes per launch / mean kernel time (HIP events on the launch stream)
@@ -51,10 +52,15 @@ def parse():
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, one GPU per rank) or gloo (multi-rank rehearsal, ranks may share a GPU)")
-    ap.add_argument("--burn-in", type=int, default=320,
+    ap.add_argument("--burn-in", type=int, default=1024,
                     help="untimed steps (16-step fused rollouts) before the warm-up: steady state")
-    ap.add_argument("--graph", type=int, default=1,
-                    help="1: replay the K timed launches from a HIP graph captured before the window")
+    ap.add_argument("--burn-in-launches", type=int, default=48,
+                    help="untimed one-step launches closing the burn-in, so the clocks have left the "
+                         "rollout kernel's regime before the warm-up (tools/window_probe.py)")
+    ap.add_argument("--graph", type=int, default=0,
+                    help="1: replay the K timed launches from a HIP graph captured before the window "
+                         "(at K = 20 host launches measured 1.04x event time on the wall, the graph's "
+                         "first replay 1.04-1.07x: tools/window_probe.py)")
     ap.add_argument("--size2-envs", type=int, default=1 << 22,
                     help="envs of the post-Infinity-Cache leg (N = 1 only); 0 disables it")
     ap.add_argument("--size2-steps", type=int, default=100)
@@ -154,7 +160,7 @@ def size2_leg(args, torch):
     env = MergeVecEnv(E, device=torch.device("cuda", torch.cuda.current_device()), autoreset=True,
                       final_observation=True, episode_stats=True)
     k = burn_in(env, args.burn_in, args.seed, 0)
-    for _ in range(5):
+    for _ in range(max(5, args.burn_in_launches)):
         env.step_random(args.seed, step_idx=k)
         k += 1
     env.clear_statistics()
@@ -170,7 +176,8 @@ def size2_leg(args, torch):
     completed = int(env.counts[:, 0].sum())
     del env
     torch.cuda.empty_cache()
-    return {"envs": E, "steps": args.size2_steps, "burn_in_steps": args.burn_in, "kernel_ms": kernel_ms,
+    return {"envs": E, "steps": args.size2_steps, "burn_in_steps": args.burn_in + max(5, args.burn_in_launches),
+            "kernel_ms": kernel_ms,
             "value": E / (kernel_ms * 1e-3), "unit": "env-steps/s", "achieved": achieved, "peak": HBM_PEAK_GBPS,
             "unit_bw": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": load_pmc(E),
             "episodes_completed": completed}
@@ -392,6 +399,9 @@ def main():
 
     # steady state first: every env past its first episodes, some finishing at every step
     k0 = burn_in(env, args.burn_in, args.seed, 0)
+    for k in range(k0, k0 + args.burn_in_launches):
+        step(k)
+    k0 += args.burn_in_launches
     for k in range(k0, k0 + args.warmup):
         step(k)
     k0 += args.warmup
@@ -506,7 +516,7 @@ def main():
                                     "autoreset, episode statistics"),
                        "envs_per_gpu": E, "global_envs": world * E,
                        "parallelism": f"dp{world} (env shards, no per-step collective)"},
-            "burn_in_steps": args.burn_in,
+            "burn_in_steps": args.burn_in + args.burn_in_launches,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBPS) if achieved else None,
                          "traffic": pmc, "kernel": KERNEL_NAME,

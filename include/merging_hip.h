@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 7
+#define MG_ABI_VERSION 8
 #define MG_OBS_DIM 10   /* merging_env.py:75 observation_shape = (10) */
 #define MG_NUM_ACTIONS 5 /* merging_env.py:101-102 action_dict / Discrete(5) */
 #define MG_ACTION_NONE (-1) /* action2=None: the constant-speed "L0" opponent, merging_env.py:152 */
@@ -192,10 +192,21 @@ typedef struct mg_transitions {
                                then a1 = flags[4 row], done = flags[4 row + 2] */
 } mg_transitions;
 
-/* Completed-episode statistics, updated only when an env finishes (MG_AUTORESET). */
+/* Completed-episode statistics of one env, updated only when it finishes (MG_AUTORESET):
+ * the returns and counts the reference's training scripts log (hdqn.py:330-346,
+ * main.py:221-228). One 32-byte record per env, so a finishing env's read-modify-write touches
+ * one DRAM sector: as two arrays ([n,2] f64 + [n,4] u32, ABI <= 7) those scattered updates cost
+ * the one-step kernel 12 % of its time at 2^22 envs (tools/steady_probe.py). */
+typedef struct mg_episode_stats {
+  double ret[2];        /* sum of completed-episode returns (ego, opponent) */
+  uint32_t episodes;    /* completed episodes */
+  uint32_t collisions;  /* of which ended in a collision */
+  uint32_t ego_first;   /* of which the ego arrived first (winner == 1) */
+  uint32_t steps;       /* total steps of the completed episodes */
+} mg_episode_stats;
+
 typedef struct mg_stats {
-  double* ret_sum;   /* [n,2] sum of completed-episode returns (ego, opponent) */
-  uint32_t* counts;  /* [n,4] episodes, collisions, ego-first arrivals, total steps */
+  mg_episode_stats* rec;  /* [n] records, or NULL: no statistics */
 } mg_stats;
 
 int mg_abi_version(void);

@@ -54,6 +54,9 @@ namespace {
 #ifndef MG_SINCOS_COLD
 #define MG_SINCOS_COLD 1  // the |t| >= 1/16 sincos fallback as an out-of-line call
 #endif
+#ifndef MG_STATS_ATOMIC
+#define MG_STATS_ATOMIC 0  // episode statistics of the one-step kernel by no-return atomics (A/B)
+#endif
 #ifndef MG_QNET_SWP
 #define MG_QNET_SWP 1  // Q-net waves of the specialised kernel: software-pipelined hidden tiles
 #endif
@@ -523,20 +526,18 @@ __device__ __forceinline__ void stats_load(const mg_stats& St, int64_t i, EpStat
   s.dirty = false;
   s.r1 = s.r2 = 0.0;
   s.c = make_uint4(0u, 0u, 0u, 0u);
-  if (St.ret_sum) {
-    s.r1 = St.ret_sum[2 * i];
-    s.r2 = St.ret_sum[2 * i + 1];
+  if (St.rec) {
+    const double2 r = reinterpret_cast<const double2*>(St.rec + i)[0];
+    s.r1 = r.x;
+    s.r2 = r.y;
+    s.c = reinterpret_cast<const uint4*>(St.rec + i)[1];
   }
-  if (St.counts) s.c = reinterpret_cast<const uint4*>(St.counts)[i];
 }
 
 __device__ __forceinline__ void stats_store(const mg_stats& St, int64_t i, const EpStats& s) {
-  if (!s.dirty) return;
-  if (St.ret_sum) {
-    St.ret_sum[2 * i] = s.r1;
-    St.ret_sum[2 * i + 1] = s.r2;
-  }
-  if (St.counts) reinterpret_cast<uint4*>(St.counts)[i] = s.c;
+  if (!s.dirty || !St.rec) return;
+  reinterpret_cast<double2*>(St.rec + i)[0] = make_double2(s.r1, s.r2);
+  reinterpret_cast<uint4*>(St.rec + i)[1] = s.c;
 }
 
 // gym.vector autoreset: record the finished episode, keep its terminal observation, reset
@@ -554,19 +555,33 @@ __device__ __forceinline__ void finish_episode(const mg_params& P, Env& e, StepO
     sreg->c.w += e.steps;
     sreg->dirty = true;
   } else {
-    if (St.ret_sum) {
-      St.ret_sum[2 * i] += e.ret1;
-      St.ret_sum[2 * i + 1] += e.ret2;
+#if MG_STATS_ATOMIC
+    // no-return atomics: the finishing lane never waits on a load (one add per address per
+    // launch, so the sum is the same double the read-modify-write gives)
+    if (St.rec) {
+      mg_episode_stats* rec = St.rec + i;
+      unsafeAtomicAdd(&rec->ret[0], e.ret1);
+      unsafeAtomicAdd(&rec->ret[1], e.ret2);
+      atomicAdd(&rec->episodes, 1u);
+      if (r.coll) atomicAdd(&rec->collisions, 1u);
+      if (e.winner == 1) atomicAdd(&rec->ego_first, 1u);
+      atomicAdd(&rec->steps, e.steps);
     }
-    if (St.counts) {
-      uint4* c = reinterpret_cast<uint4*>(St.counts) + i;
-      uint4 cv = *c;
+#else
+    // one 32-byte record per env: a finishing env reads and writes one sector
+    if (St.rec) {
+      double2* rp = reinterpret_cast<double2*>(St.rec + i);
+      uint4* cp = reinterpret_cast<uint4*>(St.rec + i) + 1;
+      const double2 rv = *rp;
+      uint4 cv = *cp;
       cv.x += 1;
       cv.y += r.coll ? 1u : 0u;
       cv.z += e.winner == 1 ? 1u : 0u;
       cv.w += e.steps;
-      *c = cv;
+      *rp = make_double2(rv.x + e.ret1, rv.y + e.ret2);
+      *cp = cv;
     }
+#endif
   }
   if (final_obs_row) {
 #pragma unroll
@@ -864,8 +879,7 @@ __global__ __launch_bounds__(kBlock, MG_ROLLOUT_WAVES_PER_EU) void rollout_kerne
     __builtin_assume(R.T.obs != nullptr);
     __builtin_assume(R.T.rew != nullptr);
     __builtin_assume(R.T.flags != nullptr);
-    __builtin_assume(R.St.ret_sum != nullptr);
-    __builtin_assume(R.St.counts != nullptr);
+    __builtin_assume(R.St.rec != nullptr);
     __builtin_assume((R.flags & MG_AUTORESET) != 0);
   }
   const mg_params& P = R.P;
@@ -2017,7 +2031,7 @@ int launch_rollout(const Rollout& R, hipStream_t stream) {
 #ifndef MG_ROLLOUT_FULL
 #define MG_ROLLOUT_FULL 1  // A/B knob: 0 always launches the generic instance
 #endif
-  const bool full = MG_ROLLOUT_FULL && R.T.obs && R.T.rew && R.T.flags && R.St.ret_sum && R.St.counts &&
+  const bool full = MG_ROLLOUT_FULL && R.T.obs && R.T.rew && R.T.flags && R.St.rec &&
                     (R.flags & MG_AUTORESET);
   if (start || stop) {
     if (full)

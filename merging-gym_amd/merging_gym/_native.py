@@ -15,7 +15,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libmerging_hip.so"
 LIB_PATH = os.environ.get("MERGING_HIP_LIB", os.path.join(_HERE, LIB_NAME))
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 OBS_DIM = 10
 NUM_ACTIONS = 5
@@ -64,7 +64,10 @@ class Transitions(_c.Structure):
 
 
 class Stats(_c.Structure):
-    _fields_ = [("ret_sum", _P), ("counts", _P)]
+    _fields_ = [("rec", _P)]  # mg_episode_stats [n]: f64 ret[2], u32 episodes/collisions/ego_first/steps
+
+
+EPISODE_STATS_BYTES = 32
 
 
 # numpy view of struct mg_rec64 (168 bytes)

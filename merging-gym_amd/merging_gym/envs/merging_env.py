@@ -97,7 +97,7 @@ class MergeEnv(_EnvBase):
         self._out = _native.Outputs(None, None, None, None, None, None,
                                     ctypes.c_void_p(self._rec_dev.data_ptr()),
                                     ctypes.c_void_p(self._err.data_ptr()))
-        self._stats = _native.Stats(None, None)
+        self._stats = _native.Stats(None)
         self._a1 = ctypes.c_void_p(self._a_dev.data_ptr())
         self._a2 = ctypes.c_void_p(self._a_dev.data_ptr() + 1)
         # zero_copy: the kernel reads the two actions from, and writes its 168-byte record to,

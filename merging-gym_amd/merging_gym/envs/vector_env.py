@@ -102,8 +102,11 @@ class MergeVecEnv:
         self.won_mask = (torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
                          if won_mask else None)
         self.error = torch.zeros(1, dtype=torch.int32, device=dev)
-        self.ret_sum = torch.zeros((n, 2), dtype=torch.float64, device=dev) if episode_stats else None
-        self.counts = torch.zeros((n, 4), dtype=torch.int32, device=dev) if episode_stats else None
+        # one 32-byte mg_episode_stats record per env; ret_sum [N,2] f64 and counts [N,4] i32
+        # (episodes, collisions, ego-first arrivals, steps) are strided views of it
+        self._ep_stats = torch.zeros((n, 4), dtype=torch.float64, device=dev) if episode_stats else None
+        self.ret_sum = self._ep_stats[:, :2] if episode_stats else None
+        self.counts = self._ep_stats[:, 2:].view(torch.int32) if episode_stats else None
 
         ptr = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
         self._state = _native.State(*(ptr(t) for t in (self.p1, self.v1, self.p2, self.v2,
@@ -113,7 +116,7 @@ class MergeVecEnv:
                                     None if packed else ptr(self.coll), ptr(self.done_mask),
                                     ptr(self.final_obs), None, ptr(self.error), ptr(self.won_mask),
                                     ptr(self.flags))
-        self._stats = _native.Stats(ptr(self.ret_sum), ptr(self.counts))
+        self._stats = _native.Stats(ptr(self._ep_stats))
         self._flags = _native.AUTORESET if self.autoreset else 0
         self._step_idx = 0
         # pre-bound call arguments: a step costs one ctypes call and no allocations

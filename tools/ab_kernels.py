@@ -58,8 +58,7 @@ class Bed:
         self.coll = torch.empty(n, dtype=torch.uint8, device=dev)
         self.fobs = torch.empty((n, 10), device=dev)
         self.a = torch.empty((2, n), dtype=torch.int8, device=dev)
-        self.ret_sum = torch.zeros((n, 2), dtype=torch.float64, device=dev)
-        self.counts = torch.zeros((n, 4), dtype=torch.int32, device=dev)
+        self.ep_stats = torch.zeros((n, 4), dtype=torch.float64, device=dev)  # mg_episode_stats [n]
         self.tobs = torch.empty((T, n, 10), device=dev)
         self.trew = torch.empty((T, n, 2), device=dev)
         self.tdone = torch.empty((T, n), dtype=torch.uint8, device=dev)
@@ -72,7 +71,7 @@ class Bed:
         self.out = nat.Outputs(self.obs.data_ptr(), self.rew.data_ptr(), self.done.data_ptr(),
                                self.coll.data_ptr(), None, self.fobs.data_ptr(), None, None)
         self.stats = (nat.Stats() if os.environ.get("MG_AB_NOSTATS") == "1"
-                      else nat.Stats(self.ret_sum.data_ptr(), self.counts.data_ptr()))
+                      else nat.Stats(self.ep_stats.data_ptr()))
         self.twon = torch.zeros((T, (n + 63) // 64), dtype=torch.int64, device=dev)
         won = self.twon.data_ptr() if os.environ.get("MG_AB_WON") == "1" else None
         self.traj = nat.Traj(self.tobs.data_ptr(), self.trew.data_ptr(), self.tdone.data_ptr(),

@@ -57,9 +57,8 @@ def run(stagger):
     out = nat.Outputs(ptr(t["obs"]), ptr(t["rew"]), ptr(t["done"]), ptr(t["coll"]), None, ptr(t["fobs"]), None,
                       None, None)
     if a.stats:
-        keep_stats = (torch.zeros((n, 2), dtype=torch.float64, device="cuda"),
-                      torch.zeros((n, 4), dtype=torch.int32, device="cuda"))
-        stats = nat.Stats(ptr(keep_stats[0]), ptr(keep_stats[1]))
+        keep_stats = torch.zeros((n, 4), dtype=torch.float64, device="cuda")  # mg_episode_stats [n]
+        stats = nat.Stats(ptr(keep_stats))
     else:
         stats = nat.Stats()
     s = torch.cuda.current_stream().cuda_stream
