@@ -57,6 +57,21 @@ namespace {
 #ifndef MG_STATS_ATOMIC
 #define MG_STATS_ATOMIC 0  // episode statistics of the one-step kernel by no-return atomics (A/B)
 #endif
+#ifndef MG_QNET_FOLD_BIAS
+#define MG_QNET_FOLD_BIAS 1  // Q-net biases carried in the padded K slots (no bias loads, zero-start accumulators)
+#endif
+#ifndef MG_QNET_XPF
+#define MG_QNET_XPF 1  // Q-net waves: W2 fragments prefetched across hidden tiles, W3 one ahead
+#endif
+#ifndef MG_QNET_UNROLL
+#define MG_QNET_UNROLL 1  // Q-net waves: hidden-tile loop fully unrolled
+#endif
+#ifndef MG_QNET_STAMPS
+#define MG_QNET_STAMPS 0  // diagnostic build: phase clocks of the specialised Q-net kernel
+#endif
+#ifndef MG_QNET_WS_SREG
+#define MG_QNET_WS_SREG 1  // specialised Q-net kernel: env waves hold episode statistics in registers
+#endif
 #ifndef MG_QNET_SWP
 #define MG_QNET_SWP 1  // Q-net waves of the specialised kernel: software-pipelined hidden tiles
 #endif
@@ -946,9 +961,24 @@ constexpr int kQS1 = 24, kQS2 = 232, kQS3 = 136;                   // row stride
 constexpr int kQOffW2 = kQH1 * kQS1 * 2;                           // ds_read_b128 lane group hits
 constexpr int kQOffW3 = kQOffW2 + kQH2 * kQS2 * 2;                 // 16 distinct 4-bank slots
 constexpr int kQOffB1 = kQOffW3 + kQOut * kQS3 * 2;
+#if MG_QNET_FOLD_BIAS
+// Biases ride in the padded K slots (see qnet_pack_kernel): no bias section, no bias loads.
+constexpr int kQOffB2 = kQOffB1, kQOffB3 = kQOffB1;
+constexpr int kQNetBytes = kQOffB1;                                // 78,848 B
+#else
 constexpr int kQOffB2 = kQOffB1 + kQH1 * 4;
 constexpr int kQOffB3 = kQOffB2 + kQH2 * 4;
 constexpr int kQNetBytes = kQOffB3 + kQOut * 4;                    // 80,384 B
+#endif
+// Folded biases: every bias b is split into three bf16 parts hi + mid + lo == b exactly (8
+// significant bits each: 24 = fp32's), stored as three weight columns whose inputs are 1.0:
+// layer-1 inputs 13..15, hidden-1 units 200..202 and hidden-2 units 100..102 (W1 / W2 rows
+// that output exactly 1.0). The matrix cores then add the fp32 bias inside the K sum (summation
+// order is the only difference from a bias-initialised accumulator).
+constexpr int kQBiasIn = 13;    // first of the three layer-1 input slots holding 1.0
+constexpr int kQOne1 = 200;     // hidden-1 units 200..202 = 1.0
+constexpr int kQOne2 = 100;     // hidden-2 units 100..102 = 1.0
+constexpr int kQMaxIn = MG_QNET_FOLD_BIAS ? kQBiasIn : 16;  // widest net input
 constexpr int kQBlock = MG_QNET_BLOCK;                             // waves sharing one LDS copy
 // specialised kernel: 4 Q-net waves + MG_QNET_WS_ENV_WAVES env waves; each env lane steps
 // MG_QNET_WS_ILP envs per phase, so a group is 64 x env waves x ILP envs and a block holds two
@@ -1006,7 +1036,13 @@ __device__ __forceinline__ bf16x8 qnet_input(const float* row, bool swap, int h)
     pr[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{v[a], v[b]}, bf16x2));
   }
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+#if MG_QNET_FOLD_BIAS
+  // features 8..15 = x8, x9, 0, 0, 0, 1, 1, 1 (the 1.0 inputs of b1's three parts)
+  static_assert(kQBiasIn == 13 && kObs == 10, "bias slots 13..15 follow the 10 features");
+  const u32x4 w = h ? u32x4{pr[4], 0u, 0x3F800000u, 0x3F803F80u} : u32x4{pr[0], pr[1], pr[2], pr[3]};
+#else
   const u32x4 w = h ? u32x4{pr[4], 0u, 0u, 0u} : u32x4{pr[0], pr[1], pr[2], pr[3]};
+#endif
   return __builtin_bit_cast(bf16x8, w);
 }
 
@@ -1041,6 +1077,49 @@ __global__ void qnet_pack_kernel(const float* w1, const float* b1, const float* 
   float* pb2 = reinterpret_cast<float*>(packed + kQOffB2);
   float* pb3 = reinterpret_cast<float*>(packed + kQOffB3);
   int e = idx;
+#if MG_QNET_FOLD_BIAS
+  // part p (0 hi, 1 mid, 2 lo) of the three-way bf16 split of b (hi + mid + lo == b)
+  auto part = [](float b, int p) {
+    const float hi = static_cast<float>(static_cast<__bf16>(b));
+    const float r = b - hi;
+    const float mid = static_cast<float>(static_cast<__bf16>(r));
+    return p == 0 ? hi : p == 1 ? mid : r - mid;
+  };
+  if (e < kQH1 * kQS1) {  // W1[m][k]: natural k order (the input features), then b1's parts
+    const int m = e / kQS1, k = e % kQS1;
+    float v = 0.f;
+    if (m < 200 && k < in_dim) v = w1[m * in_dim + k];
+    else if (m < 200 && k >= kQBiasIn && k < kQBiasIn + 3) v = part(b1[m], k - kQBiasIn);
+    else if (m >= kQOne1 && m < kQOne1 + 3 && k == kQBiasIn) v = 1.f;  // hidden-1 units = 1.0
+    pw1[e] = static_cast<__bf16>(v);
+    return;
+  }
+  e -= kQH1 * kQS1;
+  if (e < kQH2 * kQS2) {  // W2[m][c]: columns in the accumulator's k order, then b2's parts
+    const int m = e / kQS2, c = e % kQS2;
+    const int src = 16 * (c / 16) + qnet_krow(c % 16);
+    float v = 0.f;
+    if (c < kQH1) {
+      if (m < 100 && src < 200) v = w2[m * 200 + src];
+      else if (m < 100 && src >= kQOne1 && src < kQOne1 + 3) v = part(b2[m], src - kQOne1);
+      else if (m >= kQOne2 && m < kQOne2 + 3 && src == kQOne1) v = 1.f;  // hidden-2 units = 1.0
+    }
+    pw2[e] = static_cast<__bf16>(v);
+    return;
+  }
+  e -= kQH2 * kQS2;
+  if (e < kQOut * kQS3) {  // W3[m][c], then b3's parts
+    const int m = e / kQS3, c = e % kQS3;
+    const int src = 16 * (c / 16) + qnet_krow(c % 16);
+    float v = 0.f;
+    if (m < out_dim && c < kQH2) {
+      if (src < 100) v = w3[m * 100 + src];
+      else if (src >= kQOne2 && src < kQOne2 + 3) v = part(b3[m], src - kQOne2);
+    }
+    pw3[e] = static_cast<__bf16>(v);
+  }
+  (void)pb1; (void)pb2; (void)pb3;
+#else
   if (e < kQH1 * kQS1) {  // W1[m][k]: natural k order (the input features)
     const int m = e / kQS1, k = e % kQS1;
     pw1[e] = static_cast<__bf16>((m < 200 && k < in_dim) ? w1[m * in_dim + k] : 0.f);
@@ -1066,11 +1145,17 @@ __global__ void qnet_pack_kernel(const float* w1, const float* b1, const float* 
   if (e < kQH2) { pb2[e] = e < 100 ? b2[e] : 0.f; return; }
   e -= kQH2;
   if (e < kQOut) pb3[e] = e < out_dim ? b3[e] : 0.f;
+#endif
 }
 
 // The 16 bias values of a 32-row accumulator tile as laid out in lane half h: register q
 // holds row (q & 3) + 8 (q >> 2) + 4 h, i.e. four float4 runs.
 __device__ __forceinline__ f32x16 bias_tile(const float* b, int h) {
+#if MG_QNET_FOLD_BIAS
+  (void)b;
+  (void)h;
+  return f32x16{};  // the bias is inside the K sum
+#endif
   f32x16 t;
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
@@ -1253,8 +1338,16 @@ __device__ __forceinline__ void qnet_forward_swp(const uint8_t* net, const float
   // (a constant at both call sites: the last tile is peeled, so no branch per ReLU piece).
   // nk: 16-unit k-blocks of the tile that hold real units -- the last tile's second block
   // (units 208-223) is all padding, zero weights times zero activations, so it is skipped.
+#if MG_QNET_XPF
+  // Fragments carried across hidden tiles (MG_QNET_XPF): the next tile's first W2 fragment is
+  // loaded under this tile's last MFMA pair, and layer 3's W3 fragments one pair ahead, so no
+  // MFMA waits on an LDS round trip at a tile boundary.
+  bf16x8 a2n = w2frag(0, 0);
+#endif
   auto tile_step = [&](int mt, bool more, int nk) __attribute__((always_inline)) {
+#if !MG_QNET_XPF
     bf16x8 a2n = w2frag(mt, 0);
+#endif
     if (more) layer1(mt + 1, c0, c1);
     uint32_t nx[16];  // next tile's packed ReLU pairs, built between this tile's MFMAs
 #pragma unroll
@@ -1265,6 +1358,9 @@ __device__ __forceinline__ void qnet_forward_swp(const uint8_t* net, const float
       const bf16x8 a2 = a2n;
       const int jn = nk == 2 ? j + 1 : j + 2;
       if (jn < 8) a2n = w2frag(mt, jn);
+#if MG_QNET_XPF
+      else if (more) a2n = w2frag(mt + 1, 0);
+#endif
       __builtin_amdgcn_sched_barrier(0);
       acc2a[m2] = mfma32(a2, hb[sk], acc2a[m2]);
       acc2b[m2] = mfma32(a2, hb[2 + sk], acc2b[m2]);
@@ -1286,21 +1382,29 @@ __device__ __forceinline__ void qnet_forward_swp(const uint8_t* net, const float
   constexpr int kLast = kQH1 / 32 - 1;
   static_assert(16 * (2 * kLast + 1) >= kQH1Real && 32 * kLast < kQH1Real,
                 "only the last hidden tile's second k-block is padding");
+  // Fully unrolled (MG_QNET_UNROLL): the first MFMA into each layer-2 accumulator then takes
+  // an inline zero instead of 128 zeroing moves per forward, and the fragments built for the
+  // next tile land in their final registers instead of being rotated by moves every iteration.
+#if MG_QNET_UNROLL
+#pragma unroll
+#else
 #pragma unroll 1
+#endif
   for (int mt = 0; mt < kLast; ++mt) tile_step(mt, true, 2);
   tile_step(kLast, false, 1);
   f32x16 acc3_0 = bias_tile(B3, h), acc3_1 = bias_tile(B3 + zb, h);
+  auto w3frag = [&](int kb) { return *reinterpret_cast<const bf16x8*>(W3 + r * kQS3 + 16 * kb + 8 * h); };
+  constexpr int kK3 = (kQH2Real + 15) / 16;  // 16-unit k-blocks of layer 3 holding real units (7)
+  bf16x8 a3n = w3frag(0);
 #pragma unroll
-  for (int m2 = 0; m2 < kQH2 / 32; ++m2) {
-    const bf16x8 ha[2] = {relu_bf16(acc2a[m2], 0), relu_bf16(acc2a[m2], 1)};
-    const bf16x8 hbb[2] = {relu_bf16(acc2b[m2], 0), relu_bf16(acc2b[m2], 1)};
-#pragma unroll
-    for (int sk = 0; sk < 2; ++sk) {
-      if (16 * (2 * m2 + sk) >= kQH2Real) continue;  // units 112-127: padding only
-      const bf16x8 a3 = *reinterpret_cast<const bf16x8*>(W3 + r * kQS3 + 16 * (2 * m2 + sk) + 8 * h);
-      acc3_0 = mfma32(a3, ha[sk], acc3_0);
-      acc3_1 = mfma32(a3, hbb[sk], acc3_1);
-    }
+  for (int kb = 0; kb < kK3; ++kb) {
+    const int m2 = kb >> 1, sk = kb & 1;
+    const bf16x8 a3 = a3n;
+    if (kb + 1 < kK3) a3n = w3frag(kb + 1);
+    const bf16x8 ha = relu_bf16(acc2a[m2], sk);
+    const bf16x8 hbb = relu_bf16(acc2b[m2], sk);
+    acc3_0 = mfma32(a3, ha, acc3_0);
+    acc3_1 = mfma32(a3, hbb, acc3_1);
   }
   // rows 0-3 of the env of lane 32t + r sit in lane half 0 of tile t, rows 4-7 in half 1
 #pragma unroll
@@ -1338,7 +1442,8 @@ __global__ __launch_bounds__(kBlock) void qnet_forward_kernel(const uint8_t* net
     const int64_t i = base + (j >> 4);
     const int k = j & 15;
     const int src = swap ? (k + kObs / 2) % kObs : k;
-    tile[j] = (i < n && k < in_dim) ? x[i * in_dim + src] : 0.f;
+    tile[j] = (i < n && k < in_dim) ? x[i * in_dim + src]
+              : (MG_QNET_FOLD_BIAS && k >= kQBiasIn && k < kQBiasIn + 3) ? 1.f : 0.f;
   }
   __syncthreads();
   float q[8];
@@ -1410,7 +1515,7 @@ template <int OPP, int N>
 __device__ __forceinline__ void qnet_policy_step_n(const QRollout& R, Env (&e)[N], StepOut (&r)[N],
                                                    int64_t i0, const bool (&live)[N], int t,
                                                    const int (&greedy1)[N], const int (&greedy2)[N],
-                                                   bool (&won)[N]) {
+                                                   bool (&won)[N], EpStats* sreg = nullptr) {
   const uint64_t step = R.first_step + t;
   int a1[N], a2[N];
 #pragma unroll
@@ -1439,7 +1544,8 @@ __device__ __forceinline__ void qnet_policy_step_n(const QRollout& R, Env (&e)[N
     store_step_bytes(R.T, row, a1[j], a2[j], r[j].done, r[j].coll);
     won[j] = e[j].winner == 1;
     if ((R.flags & MG_AUTORESET) && r[j].done)
-      finish_episode(R.P, e[j], r[j], R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i);
+      finish_episode(R.P, e[j], r[j], R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i,
+                     sreg ? sreg + j : nullptr);
   }
 }
 
@@ -1518,6 +1624,37 @@ __global__ __launch_bounds__(kQBlock, MG_QNET_WAVES_PER_EU) void qnet_rollout_ke
   if (live) store_env(R.S, i, e);
 }
 
+#if MG_QNET_STAMPS
+// Diagnostic build only (-DMG_QNET_STAMPS=1, tools/qnet_stamps.py): per role, shader-clock
+// cycles spent working in a phase and waiting at its closing barrier, summed over waves.
+// [0] Q work, [1] Q wait, [2] env work, [3] env wait, [4] phases x waves, [5] memtime, [6] realtime
+__device__ unsigned long long g_qstamps[8];
+struct PhaseClock {
+  unsigned long long work = 0, wait = 0, t = 0;
+  __device__ void start() { t = __builtin_amdgcn_s_memtime(); }
+  __device__ void before_barrier() {
+    const unsigned long long n = __builtin_amdgcn_s_memtime();
+    work += n - t;
+    t = n;
+  }
+  __device__ void after_barrier() {
+    const unsigned long long n = __builtin_amdgcn_s_memtime();
+    wait += n - t;
+    t = n;
+  }
+  __device__ void flush(int role, int phases) {
+    if ((threadIdx.x & 63) == 0) {
+      atomicAdd(&g_qstamps[2 * role], work);
+      atomicAdd(&g_qstamps[2 * role + 1], wait);
+      if (role == 0) atomicAdd(&g_qstamps[4], static_cast<unsigned long long>(phases));
+    }
+  }
+};
+#define MG_STAMP(x) x
+#else
+#define MG_STAMP(x)
+#endif
+
 // The same T steps with the waves specialised: waves 0-3 run only the Q-net (matrix cores +
 // ReLU), waves 4-7 only the fp64 env step, so each SIMD pairs a matrix-heavy wave with a
 // vector-heavy one (waves w and w + 4 share a SIMD). The block's 512 envs are two groups
@@ -1549,6 +1686,7 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
     // (roles are whole waves, so s_barrier pairs up; the two loops keep each role's live
     // registers apart -- in one loop the env state sat beside the accumulators and spilled)
     __syncthreads();
+    MG_STAMP(PhaseClock clk; clk.start(); unsigned long long m0 = clk.t; unsigned long long r0 = __builtin_amdgcn_s_memrealtime();)
     for (int p = 0; p < phases; ++p) {
       if (p < 2 * R.num_steps) {
 #pragma unroll 1
@@ -1563,8 +1701,17 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
           }
         }
       }
+      MG_STAMP(clk.before_barrier();)
       __syncthreads();
+      MG_STAMP(clk.after_barrier();)
     }
+#if MG_QNET_STAMPS
+    clk.flush(0, phases);
+    if (tid == 0) {
+      atomicAdd(&g_qstamps[5], __builtin_amdgcn_s_memtime() - m0);
+      atomicAdd(&g_qstamps[6], __builtin_amdgcn_s_memrealtime() - r0);
+    }
+#endif
     return;
   }
   // env lane: envs lbase + 64 j + lane (j < kIlp) of group 0 (e0) and of group 1 (e1)
@@ -1572,15 +1719,25 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
   Env e0[kIlp], e1[kIlp];
   StepOut r[kIlp];
   bool live0[kIlp], live1[kIlp];
+#if MG_QNET_WS_SREG
+  // episode statistics held in registers for the launch: a finishing env's read-modify-write
+  // would wait (s_waitcnt vmcnt(0)) for every store the wave still has in flight
+  EpStats s0[kIlp], s1[kIlp];
+#endif
 #pragma unroll
   for (int j = 0; j < kIlp; ++j) {
     const int la = lbase + 64 * j + lane, lb = kHalf + la;
     live0[j] = qnet_load_env(R, base + la, e0[j], tile + la * kObs);
     live1[j] = qnet_load_env(R, base + lb, e1[j], tile + lb * kObs);
+#if MG_QNET_WS_SREG
+    stats_load(R.St, live0[j] ? base + la : 0, s0[j]);
+    stats_load(R.St, live1[j] ? base + lb : 0, s1[j]);
+#endif
 #pragma unroll
     for (int k = 0; k < kObs; ++k) r[j].o[k] = 0.0;
   }
   __syncthreads();
+  MG_STAMP(PhaseClock clk; clk.start();)
   for (int p = 0; p < phases; ++p) {
     if (p > 0) {
       const int g = (p - 1) & 1, t = (p - 1) >> 1;
@@ -1593,10 +1750,17 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
       }
       bool won[kIlp];
       // wave-uniform branch: each group's envs stay in named registers
+#if MG_QNET_WS_SREG
+      if (g == 0)
+        qnet_policy_step_n<OPP, kIlp>(R, e0, r, base + local0 + lane, live0, t, greedy1, greedy2, won, s0);
+      else
+        qnet_policy_step_n<OPP, kIlp>(R, e1, r, base + local0 + lane, live1, t, greedy1, greedy2, won, s1);
+#else
       if (g == 0)
         qnet_policy_step_n<OPP, kIlp>(R, e0, r, base + local0 + lane, live0, t, greedy1, greedy2, won);
       else
         qnet_policy_step_n<OPP, kIlp>(R, e1, r, base + local0 + lane, live1, t, greedy1, greedy2, won);
+#endif
       const int64_t wbase = base + local0;
 #pragma unroll
       for (int j = 0; j < kIlp; ++j) {
@@ -1610,13 +1774,20 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
                              R.T.obs ? R.T.obs + (static_cast<int64_t>(t) * R.n + wbase) * kObs : nullptr,
                              wrows);
     }
+    MG_STAMP(clk.before_barrier();)
     __syncthreads();
+    MG_STAMP(clk.after_barrier();)
   }
+  MG_STAMP(clk.flush(1, phases);)
 #pragma unroll
   for (int j = 0; j < kIlp; ++j) {
     const int la = lbase + 64 * j + lane;
     if (live0[j]) store_env(R.S, base + la, e0[j]);
     if (live1[j]) store_env(R.S, base + kHalf + la, e1[j]);
+#if MG_QNET_WS_SREG
+    if (live0[j]) stats_store(R.St, base + la, s0[j]);
+    if (live1[j]) stats_store(R.St, base + kHalf + la, s1[j]);
+#endif
   }
 }
 
@@ -2096,6 +2267,16 @@ extern "C" {
 
 int mg_abi_version(void) { return MG_ABI_VERSION; }
 
+#if MG_QNET_STAMPS
+// diagnostic build only: copy out (and clear) the Q-net kernel's phase clocks
+int mg_debug_qstamps(unsigned long long* out8) {
+  hipError_t e = hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_qstamps), sizeof(unsigned long long) * 8);
+  if (e != hipSuccess) return static_cast<int>(e);
+  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  return static_cast<int>(hipMemcpyToSymbol(HIP_SYMBOL(g_qstamps), z, sizeof(z)));
+}
+#endif
+
 int mg_time_next_launch(void* start_event, void* stop_event) {
   g_ev_start = static_cast<hipEvent_t>(start_event);
   g_ev_stop = static_cast<hipEvent_t>(stop_event);
@@ -2210,8 +2391,10 @@ int mg_qnet_pack(const float* fc1_w, const float* fc1_b, const float* fc2_w, con
                  void* packed, void* stream) {
   if (!fc1_w || !fc1_b || !fc2_w || !fc2_b || !out_w || !out_b || !packed)
     return fail(hipErrorInvalidValue, "%s", "mg_qnet_pack: NULL pointer");
-  if (in_dim < 1 || in_dim > 16 || out_dim < 1 || out_dim > 8)
-    return fail(hipErrorInvalidValue, "%s", "mg_qnet_pack: need 1 <= in_dim <= 16, 1 <= out_dim <= 8");
+  if (in_dim < 1 || in_dim > kQMaxIn || out_dim < 1 || out_dim > 8)
+    return fail(hipErrorInvalidValue, "%s",
+                MG_QNET_FOLD_BIAS ? "mg_qnet_pack: need 1 <= in_dim <= 13, 1 <= out_dim <= 8"
+                                  : "mg_qnet_pack: need 1 <= in_dim <= 16, 1 <= out_dim <= 8");
   if (reinterpret_cast<uintptr_t>(packed) & 15)
     return fail(hipErrorInvalidValue, "%s", "mg_qnet_pack: packed buffer must be 16-byte aligned");
   const int total = kQH1 * kQS1 + kQH2 * kQS2 + kQOut * kQS3 + kQH1 + kQH2 + kQOut;
@@ -2225,8 +2408,10 @@ int mg_qnet_forward(const void* packed, const float* x, int32_t in_dim, int32_t 
                     int64_t n, void* stream) {
   if (!packed || !x || !q) return fail(hipErrorInvalidValue, "%s", "mg_qnet_forward: NULL pointer");
   if (n < 0) return fail(hipErrorInvalidValue, "%s", "n < 0");
-  if (in_dim < 1 || in_dim > 16 || (swap_halves && in_dim != kObs))
-    return fail(hipErrorInvalidValue, "%s", "mg_qnet_forward: need 1 <= in_dim <= 16 (swap_halves: in_dim 10)");
+  if (in_dim < 1 || in_dim > kQMaxIn || (swap_halves && in_dim != kObs))
+    return fail(hipErrorInvalidValue, "%s",
+                MG_QNET_FOLD_BIAS ? "mg_qnet_forward: need 1 <= in_dim <= 13 (swap_halves: in_dim 10)"
+                                  : "mg_qnet_forward: need 1 <= in_dim <= 16 (swap_halves: in_dim 10)");
   if (reinterpret_cast<uintptr_t>(packed) & 15)
     return fail(hipErrorInvalidValue, "%s", "packed net must be 16-byte aligned");
   if (n == 0) return 0;

@@ -74,7 +74,8 @@ class QNet:
         """Q-values [N, out_dim] of inputs [N, in_dim] (device tensor), computed by
         mg_qnet_forward: observations for main.py's Net (in_dim 10; swap_halves feeds the
         opponent's view, main.py:199), goal states [goal] + state for hdqn.py's lower-level Net
-        (in_dim 11, :145, :291), or any other width up to 16 (e.g. Goal_DQN's meta-net, 10 -> 3)."""
+        (in_dim 11, :145, :291), or any other width up to 13 (e.g. Goal_DQN's meta-net, 10 -> 3); the three
+        input slots past 13 carry the folded first-layer bias."""
         import torch
 
         obs = obs.to(self.device, torch.float32).contiguous()
