@@ -54,23 +54,8 @@ namespace {
 #ifndef MG_SINCOS_COLD
 #define MG_SINCOS_COLD 1  // the |t| >= 1/16 sincos fallback as an out-of-line call
 #endif
-#ifndef MG_STATS_ATOMIC
-#define MG_STATS_ATOMIC 0  // episode statistics of the one-step kernel by no-return atomics (A/B)
-#endif
-#ifndef MG_QNET_FOLD_BIAS
-#define MG_QNET_FOLD_BIAS 1  // Q-net biases carried in the padded K slots (no bias loads, zero-start accumulators)
-#endif
-#ifndef MG_QNET_XPF
-#define MG_QNET_XPF 1  // Q-net waves: W2 fragments prefetched across hidden tiles, W3 one ahead
-#endif
-#ifndef MG_QNET_UNROLL
-#define MG_QNET_UNROLL 1  // Q-net waves: hidden-tile loop fully unrolled
-#endif
 #ifndef MG_QNET_STAMPS
 #define MG_QNET_STAMPS 0  // diagnostic build: phase clocks of the specialised Q-net kernel
-#endif
-#ifndef MG_QNET_WS_SREG
-#define MG_QNET_WS_SREG 1  // specialised Q-net kernel: env waves hold episode statistics in registers
 #endif
 #ifndef MG_QNET_SWP
 #define MG_QNET_SWP 1  // Q-net waves of the specialised kernel: software-pipelined hidden tiles
@@ -570,19 +555,6 @@ __device__ __forceinline__ void finish_episode(const mg_params& P, Env& e, StepO
     sreg->c.w += e.steps;
     sreg->dirty = true;
   } else {
-#if MG_STATS_ATOMIC
-    // no-return atomics: the finishing lane never waits on a load (one add per address per
-    // launch, so the sum is the same double the read-modify-write gives)
-    if (St.rec) {
-      mg_episode_stats* rec = St.rec + i;
-      unsafeAtomicAdd(&rec->ret[0], e.ret1);
-      unsafeAtomicAdd(&rec->ret[1], e.ret2);
-      atomicAdd(&rec->episodes, 1u);
-      if (r.coll) atomicAdd(&rec->collisions, 1u);
-      if (e.winner == 1) atomicAdd(&rec->ego_first, 1u);
-      atomicAdd(&rec->steps, e.steps);
-    }
-#else
     // one 32-byte record per env: a finishing env reads and writes one sector
     if (St.rec) {
       double2* rp = reinterpret_cast<double2*>(St.rec + i);
@@ -596,7 +568,6 @@ __device__ __forceinline__ void finish_episode(const mg_params& P, Env& e, StepO
       *rp = make_double2(rv.x + e.ret1, rv.y + e.ret2);
       *cp = cv;
     }
-#endif
   }
   if (final_obs_row) {
 #pragma unroll
@@ -960,33 +931,25 @@ constexpr int kQH1Real = 200, kQH2Real = 100;                      // main.py:30
 constexpr int kQS1 = 24, kQS2 = 232, kQS3 = 136;                   // row strides (bf16): every
 constexpr int kQOffW2 = kQH1 * kQS1 * 2;                           // ds_read_b128 lane group hits
 constexpr int kQOffW3 = kQOffW2 + kQH2 * kQS2 * 2;                 // 16 distinct 4-bank slots
-constexpr int kQOffB1 = kQOffW3 + kQOut * kQS3 * 2;
-#if MG_QNET_FOLD_BIAS
-// Biases ride in the padded K slots (see qnet_pack_kernel): no bias section, no bias loads.
-constexpr int kQOffB2 = kQOffB1, kQOffB3 = kQOffB1;
-constexpr int kQNetBytes = kQOffB1;                                // 78,848 B
-#else
-constexpr int kQOffB2 = kQOffB1 + kQH1 * 4;
-constexpr int kQOffB3 = kQOffB2 + kQH2 * 4;
-constexpr int kQNetBytes = kQOffB3 + kQOut * 4;                    // 80,384 B
-#endif
-// Folded biases: every bias b is split into three bf16 parts hi + mid + lo == b exactly (8
-// significant bits each: 24 = fp32's), stored as three weight columns whose inputs are 1.0:
-// layer-1 inputs 13..15, hidden-1 units 200..202 and hidden-2 units 100..102 (W1 / W2 rows
-// that output exactly 1.0). The matrix cores then add the fp32 bias inside the K sum (summation
-// order is the only difference from a bias-initialised accumulator).
-constexpr int kQBiasIn = 13;    // first of the three layer-1 input slots holding 1.0
-constexpr int kQOne1 = 200;     // hidden-1 units 200..202 = 1.0
-constexpr int kQOne2 = 100;     // hidden-2 units 100..102 = 1.0
-constexpr int kQMaxIn = MG_QNET_FOLD_BIAS ? kQBiasIn : 16;  // widest net input
+constexpr int kQNetBytes = kQOffW3 + kQOut * kQS3 * 2;             // 78,848 B
+// Biases are folded into the padded K slots: each bias b is split into three bf16 parts
+// hi + mid + lo == b exactly (8 significant bits each, 24 = fp32's), stored as three weight
+// columns whose inputs are 1.0 -- layer-1 inputs 13..15, hidden-1 units 200..202 and hidden-2
+// units 100..102 (W1 / W2 rows that output exactly 1.0). The matrix cores add the fp32 bias
+// inside the K sum, so there are no bias loads and every accumulator starts at an inline zero
+// (a bias-initialised accumulator cost 4 ds_read_b128 per tile and the zeroing or bias moves;
+// folding measured -5..8 % on the config-5 kernel). Summation order is the only difference.
+constexpr int kQBiasIn = 13;       // first of the three layer-1 input slots holding 1.0
+constexpr int kQOne1 = 200;        // hidden-1 units 200..202 = 1.0
+constexpr int kQOne2 = 100;        // hidden-2 units 100..102 = 1.0
+constexpr int kQMaxIn = kQBiasIn;  // widest net input: 13
 constexpr int kQBlock = MG_QNET_BLOCK;                             // waves sharing one LDS copy
 // specialised kernel: 4 Q-net waves + MG_QNET_WS_ENV_WAVES env waves; each env lane steps
 // MG_QNET_WS_ILP envs per phase, so a group is 64 x env waves x ILP envs and a block holds two
 constexpr int kQWsThreads = 64 * (4 + MG_QNET_WS_ENV_WAVES);
 constexpr int kQWsWavesPerSimd = (4 + MG_QNET_WS_ENV_WAVES) / 4;
 constexpr int kQWsEnvs = 2 * 64 * MG_QNET_WS_ENV_WAVES * MG_QNET_WS_ILP;
-static_assert(kQOffW2 % 16 == 0 && kQOffW3 % 16 == 0 && kQOffB1 % 16 == 0 && kQOffB2 % 16 == 0 &&
-                  kQOffB3 % 16 == 0 && kQNetBytes % 16 == 0,
+static_assert(kQOffW2 % 16 == 0 && kQOffW3 % 16 == 0 && kQNetBytes % 16 == 0,
               "packed Q-net sections must stay 16-byte aligned");
 
 // hardware k (0..15) within a 16-block -> hidden unit within that block (see above)
@@ -999,29 +962,30 @@ __host__ __device__ constexpr int qnet_krow(int kk) {
 // bit set is a negative int16 (and -0.0 becomes +0.0), so max_i16(x, 0) is exactly ReLU --
 // 4 v_cvt_pk_bf16_f32 + 4 v_pk_max_i16 instead of 8 v_max_f32 + 4 converts.
 typedef short i16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ bf16x8 relu_bf16(const f32x16& c, int s) {
-  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-  bf16x8 out;
-#pragma unroll
-  for (int j = 0; j < 8; j += 2) {
-    // a 2-wide fptrunc selects ONE v_cvt_pk_bf16_f32 (scalar casts cost 2 converts + a perm)
-    const bf16x2 p = __builtin_convertvector(f32x2{c[8 * s + j], c[8 * s + j + 1]}, bf16x2);
-    i16x2 v = __builtin_bit_cast(i16x2, p);
-    const i16x2 zero = {0, 0};
-    v = __builtin_elementwise_max(v, zero);
-    const bf16x2 q = __builtin_bit_cast(bf16x2, v);
-    out[j] = q[0];
-    out[j + 1] = q[1];
-  }
-  return out;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+// ReLU + bf16 pack of two accumulator values: one v_cvt_pk_bf16_f32 + one v_pk_max_i16
+// (a 2-wide fptrunc selects ONE convert; scalar casts cost 2 converts + a perm).
+__device__ __forceinline__ uint32_t relu_pair(float x, float y) {
+  i16x2 v = __builtin_bit_cast(i16x2, __builtin_convertvector(f32x2{x, y}, bf16x2));
+  const i16x2 zero = {0, 0};
+  v = __builtin_elementwise_max(v, zero);
+  return __builtin_bit_cast(uint32_t, v);
 }
 
-// Layer-1 B fragment of one env: features k = 8h .. 8h+7 of its observation row (zero past
-// 10), in the swapped order state[5:] + state[:5] when swap (main.py:199). The row is read
-// with five unconditional ds_read_b64 and converted pairwise; the lane half picks its pairs
-// with selects (per-element conditional loads cost a full LDS wait each).
+__device__ __forceinline__ bf16x8 relu_bf16(const f32x16& c, int s) {
+  const int b = 8 * s;
+  return __builtin_bit_cast(bf16x8, u32x4{relu_pair(c[b], c[b + 1]), relu_pair(c[b + 2], c[b + 3]),
+                                          relu_pair(c[b + 4], c[b + 5]), relu_pair(c[b + 6], c[b + 7])});
+}
+
+// Layer-1 B fragment of one env: features k = 8h .. 8h+7 of its observation row, in the
+// swapped order state[5:] + state[:5] when swap (main.py:199); features 8..15 are x8, x9, 0, 0,
+// 0, 1, 1, 1 (the 1.0 inputs of b1's three parts). The row is read with five unconditional
+// ds_read_b64 and converted pairwise; the lane half picks its pairs with selects (per-element
+// conditional loads cost a full LDS wait each).
 __device__ __forceinline__ bf16x8 qnet_input(const float* row, bool swap, int h) {
-  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
   float v[kObs];
 #pragma unroll
   for (int k = 0; k < kObs / 2; ++k) {
@@ -1035,25 +999,17 @@ __device__ __forceinline__ bf16x8 qnet_input(const float* row, bool swap, int h)
     const int a = swap ? (2 * k + 5) % kObs : 2 * k, b = swap ? (2 * k + 6) % kObs : 2 * k + 1;
     pr[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{v[a], v[b]}, bf16x2));
   }
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-#if MG_QNET_FOLD_BIAS
-  // features 8..15 = x8, x9, 0, 0, 0, 1, 1, 1 (the 1.0 inputs of b1's three parts)
   static_assert(kQBiasIn == 13 && kObs == 10, "bias slots 13..15 follow the 10 features");
   const u32x4 w = h ? u32x4{pr[4], 0u, 0x3F800000u, 0x3F803F80u} : u32x4{pr[0], pr[1], pr[2], pr[3]};
-#else
-  const u32x4 w = h ? u32x4{pr[4], 0u, 0u, 0u} : u32x4{pr[0], pr[1], pr[2], pr[3]};
-#endif
   return __builtin_bit_cast(bf16x8, w);
 }
 
-// Layer-1 B fragment from a 16-float row (in_dim <= 16, zero padded): features 8h .. 8h+7.
-// The standalone forward takes any input width this way, e.g. hdqn.py's goal states
+// Layer-1 B fragment from a 16-float row (in_dim <= 13, zero padded, 1.0 at 13..15): features
+// 8h .. 8h+7. The standalone forward takes any input width this way, e.g. hdqn.py's goal states
 // [goal] + state (11 values, :291) for its lower-level Net(NUM_STATES + 1, NUM_ACTIONS) (:145).
 __device__ __forceinline__ bf16x8 qnet_input_wide(const float* row16, int h) {
-  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
   const f32x4 lo = reinterpret_cast<const f32x4*>(row16 + 8 * h)[0];
   const f32x4 hi = reinterpret_cast<const f32x4*>(row16 + 8 * h)[1];
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   const u32x4 w = {__builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{lo[0], lo[1]}, bf16x2)),
                    __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{lo[2], lo[3]}, bf16x2)),
                    __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{hi[0], hi[1]}, bf16x2)),
@@ -1065,19 +1021,14 @@ __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
-// Packs fp32 torch Linear weights (row-major [out][in]) into the kernel layout.
+// Packs fp32 torch Linear weights (row-major [out][in]) and biases into the kernel layout.
 __global__ void qnet_pack_kernel(const float* w1, const float* b1, const float* w2, const float* b2,
                                  const float* w3, const float* b3, int in_dim, int out_dim,
                                  uint8_t* packed) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  int e = blockIdx.x * blockDim.x + threadIdx.x;
   __bf16* pw1 = reinterpret_cast<__bf16*>(packed);
   __bf16* pw2 = reinterpret_cast<__bf16*>(packed + kQOffW2);
   __bf16* pw3 = reinterpret_cast<__bf16*>(packed + kQOffW3);
-  float* pb1 = reinterpret_cast<float*>(packed + kQOffB1);
-  float* pb2 = reinterpret_cast<float*>(packed + kQOffB2);
-  float* pb3 = reinterpret_cast<float*>(packed + kQOffB3);
-  int e = idx;
-#if MG_QNET_FOLD_BIAS
   // part p (0 hi, 1 mid, 2 lo) of the three-way bf16 split of b (hi + mid + lo == b)
   auto part = [](float b, int p) {
     const float hi = static_cast<float>(static_cast<__bf16>(b));
@@ -1088,8 +1039,8 @@ __global__ void qnet_pack_kernel(const float* w1, const float* b1, const float* 
   if (e < kQH1 * kQS1) {  // W1[m][k]: natural k order (the input features), then b1's parts
     const int m = e / kQS1, k = e % kQS1;
     float v = 0.f;
-    if (m < 200 && k < in_dim) v = w1[m * in_dim + k];
-    else if (m < 200 && k >= kQBiasIn && k < kQBiasIn + 3) v = part(b1[m], k - kQBiasIn);
+    if (m < kQH1Real && k < in_dim) v = w1[m * in_dim + k];
+    else if (m < kQH1Real && k >= kQBiasIn && k < kQBiasIn + 3) v = part(b1[m], k - kQBiasIn);
     else if (m >= kQOne1 && m < kQOne1 + 3 && k == kQBiasIn) v = 1.f;  // hidden-1 units = 1.0
     pw1[e] = static_cast<__bf16>(v);
     return;
@@ -1100,8 +1051,8 @@ __global__ void qnet_pack_kernel(const float* w1, const float* b1, const float* 
     const int src = 16 * (c / 16) + qnet_krow(c % 16);
     float v = 0.f;
     if (c < kQH1) {
-      if (m < 100 && src < 200) v = w2[m * 200 + src];
-      else if (m < 100 && src >= kQOne1 && src < kQOne1 + 3) v = part(b2[m], src - kQOne1);
+      if (m < kQH2Real && src < kQH1Real) v = w2[m * kQH1Real + src];
+      else if (m < kQH2Real && src >= kQOne1 && src < kQOne1 + 3) v = part(b2[m], src - kQOne1);
       else if (m >= kQOne2 && m < kQOne2 + 3 && src == kQOne1) v = 1.f;  // hidden-2 units = 1.0
     }
     pw2[e] = static_cast<__bf16>(v);
@@ -1113,64 +1064,16 @@ __global__ void qnet_pack_kernel(const float* w1, const float* b1, const float* 
     const int src = 16 * (c / 16) + qnet_krow(c % 16);
     float v = 0.f;
     if (m < out_dim && c < kQH2) {
-      if (src < 100) v = w3[m * 100 + src];
+      if (src < kQH2Real) v = w3[m * kQH2Real + src];
       else if (src >= kQOne2 && src < kQOne2 + 3) v = part(b3[m], src - kQOne2);
     }
     pw3[e] = static_cast<__bf16>(v);
   }
-  (void)pb1; (void)pb2; (void)pb3;
-#else
-  if (e < kQH1 * kQS1) {  // W1[m][k]: natural k order (the input features)
-    const int m = e / kQS1, k = e % kQS1;
-    pw1[e] = static_cast<__bf16>((m < 200 && k < in_dim) ? w1[m * in_dim + k] : 0.f);
-    return;
-  }
-  e -= kQH1 * kQS1;
-  if (e < kQH2 * kQS2) {  // W2[m][c]: columns in the accumulator's k order
-    const int m = e / kQS2, c = e % kQS2;
-    const int src = 16 * (c / 16) + qnet_krow(c % 16);
-    pw2[e] = static_cast<__bf16>((m < 100 && c < kQH1 && src < 200) ? w2[m * 200 + src] : 0.f);
-    return;
-  }
-  e -= kQH2 * kQS2;
-  if (e < kQOut * kQS3) {
-    const int m = e / kQS3, c = e % kQS3;
-    const int src = 16 * (c / 16) + qnet_krow(c % 16);
-    pw3[e] = static_cast<__bf16>((m < out_dim && c < kQH2 && src < 100) ? w3[m * 100 + src] : 0.f);
-    return;
-  }
-  e -= kQOut * kQS3;
-  if (e < kQH1) { pb1[e] = e < 200 ? b1[e] : 0.f; return; }
-  e -= kQH1;
-  if (e < kQH2) { pb2[e] = e < 100 ? b2[e] : 0.f; return; }
-  e -= kQH2;
-  if (e < kQOut) pb3[e] = e < out_dim ? b3[e] : 0.f;
-#endif
-}
-
-// The 16 bias values of a 32-row accumulator tile as laid out in lane half h: register q
-// holds row (q & 3) + 8 (q >> 2) + 4 h, i.e. four float4 runs.
-__device__ __forceinline__ f32x16 bias_tile(const float* b, int h) {
-#if MG_QNET_FOLD_BIAS
-  (void)b;
-  (void)h;
-  return f32x16{};  // the bias is inside the K sum
-#endif
-  f32x16 t;
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const f32x4 v = *reinterpret_cast<const f32x4*>(b + 8 * g + 4 * h);
-    t[4 * g] = v[0];
-    t[4 * g + 1] = v[1];
-    t[4 * g + 2] = v[2];
-    t[4 * g + 3] = v[3];
-  }
-  return t;
 }
 
 // A zero the compiler cannot see through. Added to the LDS addresses of loop-invariant
-// weight / bias loads so they are issued where they are used: hoisted out of the tile and
-// time loops, they stay live across them and push the kernel into scratch.
+// weight loads so they are issued where they are used: hoisted out of the tile and time loops,
+// they stay live across them and push the kernel into scratch.
 __device__ __forceinline__ int opaque_zero() {
   int z = 0;
   asm volatile("" : "+v"(z));
@@ -1184,56 +1087,55 @@ __device__ __forceinline__ void qnet_to_lds(const uint8_t* net, uint8_t* lds) {
   for (int j = threadIdx.x; j < kQNetBytes / 16; j += blockDim.x) dst[j] = src[j];
 }
 
+// Rows 0-3 of the env of lane 32t + r sit in registers 0-3 of lane half 0 of column tile t,
+// rows 4-7 in lane half 1: swap halves across the wave.
+__device__ __forceinline__ void qnet_gather_q(const f32x16& acc3_0, const f32x16& acc3_1, int h,
+                                              float (&q)[8]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float own = h ? acc3_1[j] : acc3_0[j];
+    const float send = h ? acc3_0[j] : acc3_1[j];
+    const float got = __shfl_xor(send, 32);
+    q[j] = h ? got : own;
+    q[4 + j] = h ? own : got;
+  }
+}
+
 // Q-values of this lane's env (rows 0..7) from the block's f32 observation tile in LDS.
 // row0 = tile row of this wave's lane 0. swap = the opponent's view state[5:] + state[:5]
 // (scripts/main.py:199, human_player.py:40-41). Every lane of the wave must call it.
 // WIDE: tile rows are 16 floats (qnet_input_wide) instead of the 10-float observations.
+// Compact form (the hidden-tile loop not unrolled) for the uniform kernel and the standalone
+// forward; the specialised kernel's Q-net waves run qnet_forward_swp.
 template <bool WIDE = false>
 __device__ __forceinline__ void qnet_forward(const uint8_t* net, const float* tile, int row0,
                                              bool swap, float (&q)[8]) {
-  const __bf16* W1_ = reinterpret_cast<const __bf16*>(net);
-  const __bf16* W2_ = reinterpret_cast<const __bf16*>(net + kQOffW2);
-  const __bf16* W3_ = reinterpret_cast<const __bf16*>(net + kQOffW3);
-  const float* B1_ = reinterpret_cast<const float*>(net + kQOffB1);
-  const float* B2_ = reinterpret_cast<const float*>(net + kQOffB2);
-  const float* B3_ = reinterpret_cast<const float*>(net + kQOffB3);
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-
   // Both N-tiles in the same hidden-tile iteration: two independent MFMA -> VALU -> MFMA
   // chains per wave and one W2 fragment load per pair of MFMAs (one N-tile at a time, with 4
   // accumulators instead of 8, measured 7-12 % slower).
-  f32x16 acc3_0, acc3_1;
+  f32x16 acc3_0 = {}, acc3_1 = {};
   {
     const int z = opaque_zero();
-    const __bf16* W1 = W1_ + z;
-    const __bf16* W2 = W2_ + z;
-    const __bf16* W3 = W3_ + z;
-    const float* B1 = B1_ + z;
-    const float* B2 = B2_ + z;
-    const float* B3 = B3_ + z;
+    const __bf16* W1 = reinterpret_cast<const __bf16*>(net) + z;
+    const __bf16* W2 = reinterpret_cast<const __bf16*>(net + kQOffW2) + z;
+    const __bf16* W3 = reinterpret_cast<const __bf16*>(net + kQOffW3) + z;
     const bf16x8 xb0 = WIDE ? qnet_input_wide(tile + (row0 + r) * 16, h)
                             : qnet_input(tile + (row0 + r) * kObs, swap, h);
     const bf16x8 xb1 = WIDE ? qnet_input_wide(tile + (row0 + 32 + r) * 16, h)
                             : qnet_input(tile + (row0 + 32 + r) * kObs, swap, h);
-    f32x16 acc2a[4], acc2b[4];
-    // each accumulator loads its bias from LDS itself: sharing one load costs 16 v_mov per tile
-    const int zb = opaque_zero();
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      acc2a[m] = bias_tile(B2 + 32 * m, h);
-      acc2b[m] = bias_tile(B2 + 32 * m + zb, h);
-    }
+    f32x16 acc2a[4] = {}, acc2b[4] = {};
 #pragma unroll 1
     for (int mt = 0; mt < kQH1 / 32; ++mt) {
       const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(W1 + (32 * mt + r) * kQS1 + 8 * h);
-      const f32x16 bt = bias_tile(B1 + 32 * mt, h);
       auto w2frag = [&](int m2, int sk) {
         return *reinterpret_cast<const bf16x8*>(W2 + (32 * m2 + r) * kQS2 + 16 * (2 * mt + sk) +
                                                 8 * h);
       };
       bf16x8 a2cur = w2frag(0, 0);
-      const f32x16 c0 = mfma32(a1, xb0, bt);
-      const f32x16 c1 = mfma32(a1, xb1, bt);
+      const f32x16 zero = {};
+      const f32x16 c0 = mfma32(a1, xb0, zero);
+      const f32x16 c1 = mfma32(a1, xb1, zero);
       const bf16x8 ha[2] = {relu_bf16(c0, 0), relu_bf16(c0, 1)};
       const bf16x8 hb[2] = {relu_bf16(c1, 0), relu_bf16(c1, 1)};
 #pragma unroll
@@ -1250,7 +1152,6 @@ __device__ __forceinline__ void qnet_forward(const uint8_t* net, const float* ti
         }
       }
     }
-    acc3_0 = acc3_1 = bias_tile(B3, h);
 #pragma unroll
     for (int m2 = 0; m2 < kQH2 / 32; ++m2) {
       const bf16x8 ha[2] = {relu_bf16(acc2a[m2], 0), relu_bf16(acc2a[m2], 1)};
@@ -1264,90 +1165,44 @@ __device__ __forceinline__ void qnet_forward(const uint8_t* net, const float* ti
       }
     }
   }
-
-  // Column r of N-tile t is the env of lane 32t + r. Rows 0-3 sit in registers 0-3 of lane
-  // half 0, rows 4-7 in registers 0-3 of lane half 1: swap halves across the wave.
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float own = h ? acc3_1[j] : acc3_0[j];
-    const float send = h ? acc3_0[j] : acc3_1[j];
-    const float got = __shfl_xor(send, 32);
-    q[j] = h ? got : own;
-    q[4 + j] = h ? own : got;
-  }
+  qnet_gather_q(acc3_0, acc3_1, h, q);
 }
 
-// ReLU + bf16 pack of two accumulator values: one v_cvt_pk_bf16_f32 + one v_pk_max_i16.
-__device__ __forceinline__ uint32_t relu_pair(float x, float y) {
-  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-  i16x2 v = __builtin_bit_cast(i16x2, __builtin_convertvector(f32x2{x, y}, bf16x2));
-  const i16x2 zero = {0, 0};
-  v = __builtin_elementwise_max(v, zero);
-  return __builtin_bit_cast(uint32_t, v);
-}
-
-// qnet_forward (pair mode) software-pipelined over the hidden tiles, for a wave that runs
-// only the Q-net (qnet_rollout_ws_kernel has the registers for it): layer 1 of hidden tile
-// mt + 1 is issued ahead of layer 2 of tile mt, and its ReLU is computed in pieces between
-// tile mt's layer-2 MFMAs, so the vector work runs while the matrix pipe is busy instead of
-// between dependent MFMAs.
+// qnet_forward (pair mode) software-pipelined over the hidden tiles and fully unrolled, for a
+// wave that runs only the Q-net (qnet_rollout_ws_kernel has the registers for it): layer 1 of
+// hidden tile mt + 1 is issued ahead of layer 2 of tile mt, and its ReLU is computed in pieces
+// between tile mt's layer-2 MFMAs, so the vector work runs while the matrix pipe is busy
+// instead of between dependent MFMAs. Unrolled, the first MFMA into each layer-2 accumulator
+// takes an inline zero and the fragments built for the next tile land in their final
+// registers (rolled, 128 zeroing moves per forward plus ~14 rotation moves per tile: -5..7 %).
 __device__ __forceinline__ void qnet_forward_swp(const uint8_t* net, const float* tile, int row0,
                                                  bool swap, float (&q)[8]) {
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int z = opaque_zero();
   const __bf16* W1 = reinterpret_cast<const __bf16*>(net) + z;
   const __bf16* W2 = reinterpret_cast<const __bf16*>(net + kQOffW2) + z;
   const __bf16* W3 = reinterpret_cast<const __bf16*>(net + kQOffW3) + z;
-  const float* B1 = reinterpret_cast<const float*>(net + kQOffB1) + z;
-  const float* B2 = reinterpret_cast<const float*>(net + kQOffB2) + z;
-  const float* B3 = reinterpret_cast<const float*>(net + kQOffB3) + z;
   const bf16x8 xb0 = qnet_input(tile + (row0 + r) * kObs, swap, h);
   const bf16x8 xb1 = qnet_input(tile + (row0 + 32 + r) * kObs, swap, h);
-  f32x16 acc2a[4], acc2b[4];
-  const int zb = opaque_zero();
-#pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    acc2a[m] = bias_tile(B2 + 32 * m, h);
-    acc2b[m] = bias_tile(B2 + 32 * m + zb, h);
-  }
+  f32x16 acc2a[4] = {}, acc2b[4] = {};
+  const f32x16 zero = {};
   auto layer1 = [&](int mt, f32x16& c0, f32x16& c1) {
     const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(W1 + (32 * mt + r) * kQS1 + 8 * h);
-    const f32x16 bt = bias_tile(B1 + 32 * mt, h);
-    c0 = mfma32(a1, xb0, bt);
-    c1 = mfma32(a1, xb1, bt);
-  };
-  // hb[f]: f = 0, 1 -> column tile 0 k-steps 0, 1; f = 2, 3 -> column tile 1
-  auto relu_all = [&](const f32x16& c0, const f32x16& c1, bf16x8 (&hb)[4]) {
-#pragma unroll
-    for (int f = 0; f < 4; ++f) {
-      const f32x16& c = f < 2 ? c0 : c1;
-      const int b = 8 * (f & 1);
-      hb[f] = __builtin_bit_cast(bf16x8, u32x4{relu_pair(c[b], c[b + 1]), relu_pair(c[b + 2], c[b + 3]),
-                                               relu_pair(c[b + 4], c[b + 5]), relu_pair(c[b + 6], c[b + 7])});
-    }
+    c0 = mfma32(a1, xb0, zero);
+    c1 = mfma32(a1, xb1, zero);
   };
   f32x16 c0, c1;
-  bf16x8 hb[4];
   layer1(0, c0, c1);
-  relu_all(c0, c1, hb);
+  // hb[f]: f = 0, 1 -> column tile 0 k-steps 0, 1; f = 2, 3 -> column tile 1
+  bf16x8 hb[4] = {relu_bf16(c0, 0), relu_bf16(c0, 1), relu_bf16(c1, 0), relu_bf16(c1, 1)};
   auto w2frag = [&](int mt, int j) {
     return *reinterpret_cast<const bf16x8*>(W2 + (32 * (j >> 1) + r) * kQS2 + 16 * (2 * mt + (j & 1)) + 8 * h);
   };
   // one hidden tile: its layer 2, with the next tile's layer 1 + ReLU folded in when `more`
-  // (a constant at both call sites: the last tile is peeled, so no branch per ReLU piece).
-  // nk: 16-unit k-blocks of the tile that hold real units -- the last tile's second block
-  // (units 208-223) is all padding, zero weights times zero activations, so it is skipped.
-#if MG_QNET_XPF
-  // Fragments carried across hidden tiles (MG_QNET_XPF): the next tile's first W2 fragment is
-  // loaded under this tile's last MFMA pair, and layer 3's W3 fragments one pair ahead, so no
-  // MFMA waits on an LDS round trip at a tile boundary.
-  bf16x8 a2n = w2frag(0, 0);
-#endif
+  // (a constant at every call site). nk: 16-unit k-blocks of the tile that hold real units --
+  // the last tile's second block (units 208-223) is all padding, so it is skipped.
   auto tile_step = [&](int mt, bool more, int nk) __attribute__((always_inline)) {
-#if !MG_QNET_XPF
     bf16x8 a2n = w2frag(mt, 0);
-#endif
     if (more) layer1(mt + 1, c0, c1);
     uint32_t nx[16];  // next tile's packed ReLU pairs, built between this tile's MFMAs
 #pragma unroll
@@ -1358,9 +1213,6 @@ __device__ __forceinline__ void qnet_forward_swp(const uint8_t* net, const float
       const bf16x8 a2 = a2n;
       const int jn = nk == 2 ? j + 1 : j + 2;
       if (jn < 8) a2n = w2frag(mt, jn);
-#if MG_QNET_XPF
-      else if (more) a2n = w2frag(mt + 1, 0);
-#endif
       __builtin_amdgcn_sched_barrier(0);
       acc2a[m2] = mfma32(a2, hb[sk], acc2a[m2]);
       acc2b[m2] = mfma32(a2, hb[2 + sk], acc2b[m2]);
@@ -1382,39 +1234,24 @@ __device__ __forceinline__ void qnet_forward_swp(const uint8_t* net, const float
   constexpr int kLast = kQH1 / 32 - 1;
   static_assert(16 * (2 * kLast + 1) >= kQH1Real && 32 * kLast < kQH1Real,
                 "only the last hidden tile's second k-block is padding");
-  // Fully unrolled (MG_QNET_UNROLL): the first MFMA into each layer-2 accumulator then takes
-  // an inline zero instead of 128 zeroing moves per forward, and the fragments built for the
-  // next tile land in their final registers instead of being rotated by moves every iteration.
-#if MG_QNET_UNROLL
 #pragma unroll
-#else
-#pragma unroll 1
-#endif
   for (int mt = 0; mt < kLast; ++mt) tile_step(mt, true, 2);
   tile_step(kLast, false, 1);
-  f32x16 acc3_0 = bias_tile(B3, h), acc3_1 = bias_tile(B3 + zb, h);
+  // layer 3 over the k-blocks holding real units (96..111 carries units 100..102 = 1.0 too;
+  // 112..127 is padding), its W3 fragments one ahead
+  f32x16 acc3_0 = {}, acc3_1 = {};
   auto w3frag = [&](int kb) { return *reinterpret_cast<const bf16x8*>(W3 + r * kQS3 + 16 * kb + 8 * h); };
-  constexpr int kK3 = (kQH2Real + 15) / 16;  // 16-unit k-blocks of layer 3 holding real units (7)
+  constexpr int kK3 = (kQH2Real + 15) / 16;
   bf16x8 a3n = w3frag(0);
 #pragma unroll
   for (int kb = 0; kb < kK3; ++kb) {
     const int m2 = kb >> 1, sk = kb & 1;
     const bf16x8 a3 = a3n;
     if (kb + 1 < kK3) a3n = w3frag(kb + 1);
-    const bf16x8 ha = relu_bf16(acc2a[m2], sk);
-    const bf16x8 hbb = relu_bf16(acc2b[m2], sk);
-    acc3_0 = mfma32(a3, ha, acc3_0);
-    acc3_1 = mfma32(a3, hbb, acc3_1);
+    acc3_0 = mfma32(a3, relu_bf16(acc2a[m2], sk), acc3_0);
+    acc3_1 = mfma32(a3, relu_bf16(acc2b[m2], sk), acc3_1);
   }
-  // rows 0-3 of the env of lane 32t + r sit in lane half 0 of tile t, rows 4-7 in half 1
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float own = h ? acc3_1[j] : acc3_0[j];
-    const float send = h ? acc3_0[j] : acc3_1[j];
-    const float got = __shfl_xor(send, 32);
-    q[j] = h ? got : own;
-    q[4 + j] = h ? own : got;
-  }
+  qnet_gather_q(acc3_0, acc3_1, h, q);
 }
 
 __device__ __forceinline__ int argmax_first(const float (&q)[8], int out_dim) {
@@ -1443,7 +1280,7 @@ __global__ __launch_bounds__(kBlock) void qnet_forward_kernel(const uint8_t* net
     const int k = j & 15;
     const int src = swap ? (k + kObs / 2) % kObs : k;
     tile[j] = (i < n && k < in_dim) ? x[i * in_dim + src]
-              : (MG_QNET_FOLD_BIAS && k >= kQBiasIn && k < kQBiasIn + 3) ? 1.f : 0.f;
+              : (k >= kQBiasIn && k < kQBiasIn + 3) ? 1.f : 0.f;
   }
   __syncthreads();
   float q[8];
@@ -1515,7 +1352,7 @@ template <int OPP, int N>
 __device__ __forceinline__ void qnet_policy_step_n(const QRollout& R, Env (&e)[N], StepOut (&r)[N],
                                                    int64_t i0, const bool (&live)[N], int t,
                                                    const int (&greedy1)[N], const int (&greedy2)[N],
-                                                   bool (&won)[N], EpStats* sreg = nullptr) {
+                                                   bool (&won)[N]) {
   const uint64_t step = R.first_step + t;
   int a1[N], a2[N];
 #pragma unroll
@@ -1544,8 +1381,7 @@ __device__ __forceinline__ void qnet_policy_step_n(const QRollout& R, Env (&e)[N
     store_step_bytes(R.T, row, a1[j], a2[j], r[j].done, r[j].coll);
     won[j] = e[j].winner == 1;
     if ((R.flags & MG_AUTORESET) && r[j].done)
-      finish_episode(R.P, e[j], r[j], R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i,
-                     sreg ? sreg + j : nullptr);
+      finish_episode(R.P, e[j], r[j], R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i);
   }
 }
 
@@ -1719,20 +1555,11 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
   Env e0[kIlp], e1[kIlp];
   StepOut r[kIlp];
   bool live0[kIlp], live1[kIlp];
-#if MG_QNET_WS_SREG
-  // episode statistics held in registers for the launch: a finishing env's read-modify-write
-  // would wait (s_waitcnt vmcnt(0)) for every store the wave still has in flight
-  EpStats s0[kIlp], s1[kIlp];
-#endif
 #pragma unroll
   for (int j = 0; j < kIlp; ++j) {
     const int la = lbase + 64 * j + lane, lb = kHalf + la;
     live0[j] = qnet_load_env(R, base + la, e0[j], tile + la * kObs);
     live1[j] = qnet_load_env(R, base + lb, e1[j], tile + lb * kObs);
-#if MG_QNET_WS_SREG
-    stats_load(R.St, live0[j] ? base + la : 0, s0[j]);
-    stats_load(R.St, live1[j] ? base + lb : 0, s1[j]);
-#endif
 #pragma unroll
     for (int k = 0; k < kObs; ++k) r[j].o[k] = 0.0;
   }
@@ -1750,17 +1577,10 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
       }
       bool won[kIlp];
       // wave-uniform branch: each group's envs stay in named registers
-#if MG_QNET_WS_SREG
-      if (g == 0)
-        qnet_policy_step_n<OPP, kIlp>(R, e0, r, base + local0 + lane, live0, t, greedy1, greedy2, won, s0);
-      else
-        qnet_policy_step_n<OPP, kIlp>(R, e1, r, base + local0 + lane, live1, t, greedy1, greedy2, won, s1);
-#else
       if (g == 0)
         qnet_policy_step_n<OPP, kIlp>(R, e0, r, base + local0 + lane, live0, t, greedy1, greedy2, won);
       else
         qnet_policy_step_n<OPP, kIlp>(R, e1, r, base + local0 + lane, live1, t, greedy1, greedy2, won);
-#endif
       const int64_t wbase = base + local0;
 #pragma unroll
       for (int j = 0; j < kIlp; ++j) {
@@ -1784,10 +1604,6 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
     const int la = lbase + 64 * j + lane;
     if (live0[j]) store_env(R.S, base + la, e0[j]);
     if (live1[j]) store_env(R.S, base + kHalf + la, e1[j]);
-#if MG_QNET_WS_SREG
-    if (live0[j]) stats_store(R.St, base + la, s0[j]);
-    if (live1[j]) stats_store(R.St, base + kHalf + la, s1[j]);
-#endif
   }
 }
 
@@ -2392,9 +2208,7 @@ int mg_qnet_pack(const float* fc1_w, const float* fc1_b, const float* fc2_w, con
   if (!fc1_w || !fc1_b || !fc2_w || !fc2_b || !out_w || !out_b || !packed)
     return fail(hipErrorInvalidValue, "%s", "mg_qnet_pack: NULL pointer");
   if (in_dim < 1 || in_dim > kQMaxIn || out_dim < 1 || out_dim > 8)
-    return fail(hipErrorInvalidValue, "%s",
-                MG_QNET_FOLD_BIAS ? "mg_qnet_pack: need 1 <= in_dim <= 13, 1 <= out_dim <= 8"
-                                  : "mg_qnet_pack: need 1 <= in_dim <= 16, 1 <= out_dim <= 8");
+    return fail(hipErrorInvalidValue, "%s", "mg_qnet_pack: need 1 <= in_dim <= 13, 1 <= out_dim <= 8");
   if (reinterpret_cast<uintptr_t>(packed) & 15)
     return fail(hipErrorInvalidValue, "%s", "mg_qnet_pack: packed buffer must be 16-byte aligned");
   const int total = kQH1 * kQS1 + kQH2 * kQS2 + kQOut * kQS3 + kQH1 + kQH2 + kQOut;
@@ -2409,9 +2223,7 @@ int mg_qnet_forward(const void* packed, const float* x, int32_t in_dim, int32_t 
   if (!packed || !x || !q) return fail(hipErrorInvalidValue, "%s", "mg_qnet_forward: NULL pointer");
   if (n < 0) return fail(hipErrorInvalidValue, "%s", "n < 0");
   if (in_dim < 1 || in_dim > kQMaxIn || (swap_halves && in_dim != kObs))
-    return fail(hipErrorInvalidValue, "%s",
-                MG_QNET_FOLD_BIAS ? "mg_qnet_forward: need 1 <= in_dim <= 13 (swap_halves: in_dim 10)"
-                                  : "mg_qnet_forward: need 1 <= in_dim <= 16 (swap_halves: in_dim 10)");
+    return fail(hipErrorInvalidValue, "%s", "mg_qnet_forward: need 1 <= in_dim <= 13 (swap_halves: in_dim 10)");
   if (reinterpret_cast<uintptr_t>(packed) & 15)
     return fail(hipErrorInvalidValue, "%s", "packed net must be 16-byte aligned");
   if (n == 0) return 0;
