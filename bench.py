@@ -61,6 +61,8 @@ def parse():
                     help="1: replay the K timed launches from a HIP graph captured before the window "
                          "(at K = 20 host launches measured 1.04x event time on the wall, the graph's "
                          "first replay 1.04-1.07x: tools/window_probe.py)")
+    ap.add_argument("--sync-spin", type=int, default=1,
+                    help="1: hipDeviceScheduleSpin (synchronize spins instead of yielding the host thread)")
     ap.add_argument("--size2-envs", type=int, default=1 << 22,
                     help="envs of the post-Infinity-Cache leg (N = 1 only); 0 disables it")
     ap.add_argument("--size2-steps", type=int, default=100)
@@ -373,8 +375,21 @@ def dropin_leg(seed: int):
     return out
 
 
+def sync_spin():
+    """hipDeviceScheduleSpin for this process, before the HIP context exists: a synchronize then
+    spins on the host instead of yielding, so the host thread that issues the timed launches is
+    awake when the window opens (tools/window_probe.py)."""
+    import ctypes
+
+    try:
+        return ctypes.CDLL("libamdhip64.so").hipSetDeviceFlags(ctypes.c_uint(1))  # hipDeviceScheduleSpin
+    except OSError:
+        return None
+
+
 def main():
     args = parse()
+    spin_rc = sync_spin() if args.sync_spin else None
     import torch
     import torch.distributed as dist
 
@@ -525,6 +540,7 @@ def main():
                          "timing": ("HIP events recorded on the launch stream around the K timed launches "
                                     f"({'one HIP-graph replay' if args.graph else 'K host launches'}), / K"),
                          "kernel_ms_dispatch_sample": dispatch_ms, "host_enqueue_ms_per_launch": host_ms,
+                         "host_sync": "spin" if spin_rc == 0 else "default",
                          "wall_over_kernel": (elapsed / args.steps * 1e3) / kernel_ms if kernel_ms else None,
                          "traffic_rule": "2 x FETCH_SIZE + WRITE_SIZE per launch, profiles/pmc_traffic.json"},
             "episodes": episodes,

@@ -926,12 +926,17 @@ __global__ __launch_bounds__(kBlock, MG_ROLLOUT_WAVES_PER_EU) void rollout_kerne
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int kQH1 = 224, kQH2 = 128, kQOut = 32;                 // padded 200, 100, out
+constexpr int kQH1 = 224, kQH2 = 128;                              // padded 200, 100
 constexpr int kQH1Real = 200, kQH2Real = 100;                      // main.py:30-47 Net widths
 constexpr int kQS1 = 24, kQS2 = 232, kQS3 = 136;                   // row strides (bf16): every
-constexpr int kQOffW2 = kQH1 * kQS1 * 2;                           // ds_read_b128 lane group hits
-constexpr int kQOffW3 = kQOffW2 + kQH2 * kQS2 * 2;                 // 16 distinct 4-bank slots
-constexpr int kQNetBytes = kQOffW3 + kQOut * kQS3 * 2;             // 78,848 B
+// Stored rows: only up to the last row that can be non-zero plus one zero row (W1: units
+// 0..202 + zero row 203; W2: 0..102 + zero row 103; W3: outputs 0..7 + zero row 8). A lane
+// whose tile row lies past them reads the zero row instead (qrow*), so two packed nets fit one
+// CU's LDS beside the observation tiles (the h-DQN kernel).
+constexpr int kQR1 = 204, kQR2 = 104, kQR3 = 9;                    // stored rows per matrix
+constexpr int kQOffW2 = kQR1 * kQS1 * 2;                           // ds_read_b128 lane group hits
+constexpr int kQOffW3 = kQOffW2 + kQR2 * kQS2 * 2;                 // 16 distinct 4-bank slots
+constexpr int kQNetBytes = kQOffW3 + kQR3 * kQS3 * 2;              // 60,496 B
 // Biases are folded into the padded K slots: each bias b is split into three bf16 parts
 // hi + mid + lo == b exactly (8 significant bits each, 24 = fp32's), stored as three weight
 // columns whose inputs are 1.0 -- layer-1 inputs 13..15, hidden-1 units 200..202 and hidden-2
@@ -951,6 +956,10 @@ constexpr int kQWsWavesPerSimd = (4 + MG_QNET_WS_ENV_WAVES) / 4;
 constexpr int kQWsEnvs = 2 * 64 * MG_QNET_WS_ENV_WAVES * MG_QNET_WS_ILP;
 static_assert(kQOffW2 % 16 == 0 && kQOffW3 % 16 == 0 && kQNetBytes % 16 == 0,
               "packed Q-net sections must stay 16-byte aligned");
+
+__device__ __forceinline__ int qrow1(int m) { return m < kQR1 ? m : kQR1 - 1; }
+__device__ __forceinline__ int qrow2(int m) { return m < kQR2 ? m : kQR2 - 1; }
+__device__ __forceinline__ int qrow3(int m) { return m < kQR3 ? m : kQR3 - 1; }
 
 // hardware k (0..15) within a 16-block -> hidden unit within that block (see above)
 __host__ __device__ constexpr int qnet_krow(int kk) {
@@ -1036,7 +1045,7 @@ __global__ void qnet_pack_kernel(const float* w1, const float* b1, const float* 
     const float mid = static_cast<float>(static_cast<__bf16>(r));
     return p == 0 ? hi : p == 1 ? mid : r - mid;
   };
-  if (e < kQH1 * kQS1) {  // W1[m][k]: natural k order (the input features), then b1's parts
+  if (e < kQR1 * kQS1) {  // W1[m][k]: natural k order (the input features), then b1's parts
     const int m = e / kQS1, k = e % kQS1;
     float v = 0.f;
     if (m < kQH1Real && k < in_dim) v = w1[m * in_dim + k];
@@ -1045,8 +1054,8 @@ __global__ void qnet_pack_kernel(const float* w1, const float* b1, const float* 
     pw1[e] = static_cast<__bf16>(v);
     return;
   }
-  e -= kQH1 * kQS1;
-  if (e < kQH2 * kQS2) {  // W2[m][c]: columns in the accumulator's k order, then b2's parts
+  e -= kQR1 * kQS1;
+  if (e < kQR2 * kQS2) {  // W2[m][c]: columns in the accumulator's k order, then b2's parts
     const int m = e / kQS2, c = e % kQS2;
     const int src = 16 * (c / 16) + qnet_krow(c % 16);
     float v = 0.f;
@@ -1058,8 +1067,8 @@ __global__ void qnet_pack_kernel(const float* w1, const float* b1, const float* 
     pw2[e] = static_cast<__bf16>(v);
     return;
   }
-  e -= kQH2 * kQS2;
-  if (e < kQOut * kQS3) {  // W3[m][c], then b3's parts
+  e -= kQR2 * kQS2;
+  if (e < kQR3 * kQS3) {  // W3[m][c], then b3's parts
     const int m = e / kQS3, c = e % kQS3;
     const int src = 16 * (c / 16) + qnet_krow(c % 16);
     float v = 0.f;
@@ -1127,9 +1136,9 @@ __device__ __forceinline__ void qnet_forward(const uint8_t* net, const float* ti
     f32x16 acc2a[4] = {}, acc2b[4] = {};
 #pragma unroll 1
     for (int mt = 0; mt < kQH1 / 32; ++mt) {
-      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(W1 + (32 * mt + r) * kQS1 + 8 * h);
+      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(W1 + qrow1(32 * mt + r) * kQS1 + 8 * h);
       auto w2frag = [&](int m2, int sk) {
-        return *reinterpret_cast<const bf16x8*>(W2 + (32 * m2 + r) * kQS2 + 16 * (2 * mt + sk) +
+        return *reinterpret_cast<const bf16x8*>(W2 + qrow2(32 * m2 + r) * kQS2 + 16 * (2 * mt + sk) +
                                                 8 * h);
       };
       bf16x8 a2cur = w2frag(0, 0);
@@ -1159,7 +1168,7 @@ __device__ __forceinline__ void qnet_forward(const uint8_t* net, const float* ti
 #pragma unroll
       for (int sk = 0; sk < 2; ++sk) {
         const bf16x8 a3 =
-            *reinterpret_cast<const bf16x8*>(W3 + r * kQS3 + 16 * (2 * m2 + sk) + 8 * h);
+            *reinterpret_cast<const bf16x8*>(W3 + qrow3(r) * kQS3 + 16 * (2 * m2 + sk) + 8 * h);
         acc3_0 = mfma32(a3, ha[sk], acc3_0);
         acc3_1 = mfma32(a3, hb[sk], acc3_1);
       }
@@ -1187,7 +1196,7 @@ __device__ __forceinline__ void qnet_forward_swp(const uint8_t* net, const float
   f32x16 acc2a[4] = {}, acc2b[4] = {};
   const f32x16 zero = {};
   auto layer1 = [&](int mt, f32x16& c0, f32x16& c1) {
-    const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(W1 + (32 * mt + r) * kQS1 + 8 * h);
+    const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(W1 + qrow1(32 * mt + r) * kQS1 + 8 * h);
     c0 = mfma32(a1, xb0, zero);
     c1 = mfma32(a1, xb1, zero);
   };
@@ -1196,7 +1205,7 @@ __device__ __forceinline__ void qnet_forward_swp(const uint8_t* net, const float
   // hb[f]: f = 0, 1 -> column tile 0 k-steps 0, 1; f = 2, 3 -> column tile 1
   bf16x8 hb[4] = {relu_bf16(c0, 0), relu_bf16(c0, 1), relu_bf16(c1, 0), relu_bf16(c1, 1)};
   auto w2frag = [&](int mt, int j) {
-    return *reinterpret_cast<const bf16x8*>(W2 + (32 * (j >> 1) + r) * kQS2 + 16 * (2 * mt + (j & 1)) + 8 * h);
+    return *reinterpret_cast<const bf16x8*>(W2 + qrow2(32 * (j >> 1) + r) * kQS2 + 16 * (2 * mt + (j & 1)) + 8 * h);
   };
   // one hidden tile: its layer 2, with the next tile's layer 1 + ReLU folded in when `more`
   // (a constant at every call site). nk: 16-unit k-blocks of the tile that hold real units --
@@ -1240,7 +1249,7 @@ __device__ __forceinline__ void qnet_forward_swp(const uint8_t* net, const float
   // layer 3 over the k-blocks holding real units (96..111 carries units 100..102 = 1.0 too;
   // 112..127 is padding), its W3 fragments one ahead
   f32x16 acc3_0 = {}, acc3_1 = {};
-  auto w3frag = [&](int kb) { return *reinterpret_cast<const bf16x8*>(W3 + r * kQS3 + 16 * kb + 8 * h); };
+  auto w3frag = [&](int kb) { return *reinterpret_cast<const bf16x8*>(W3 + qrow3(r) * kQS3 + 16 * kb + 8 * h); };
   constexpr int kK3 = (kQH2Real + 15) / 16;
   bf16x8 a3n = w3frag(0);
 #pragma unroll
@@ -2211,7 +2220,7 @@ int mg_qnet_pack(const float* fc1_w, const float* fc1_b, const float* fc2_w, con
     return fail(hipErrorInvalidValue, "%s", "mg_qnet_pack: need 1 <= in_dim <= 13, 1 <= out_dim <= 8");
   if (reinterpret_cast<uintptr_t>(packed) & 15)
     return fail(hipErrorInvalidValue, "%s", "mg_qnet_pack: packed buffer must be 16-byte aligned");
-  const int total = kQH1 * kQS1 + kQH2 * kQS2 + kQOut * kQS3 + kQH1 + kQH2 + kQOut;
+  const int total = kQR1 * kQS1 + kQR2 * kQS2 + kQR3 * kQS3;
   hipLaunchKernelGGL(qnet_pack_kernel, dim3((total + 255) / 256), dim3(256), 0,
                      static_cast<hipStream_t>(stream), fc1_w, fc1_b, fc2_w, fc2_b, out_w, out_b,
                      in_dim, out_dim, static_cast<uint8_t*>(packed));
