@@ -282,6 +282,56 @@ def qnet_leg(env, args, world, dist, torch, opponent):
             "agreement_sample": int(x.shape[0])}
 
 
+HDQN_USEFUL_FLOP = 2 * (10 * 200 + 200 * 100 + 100 * 3) + 2 * (11 * 200 + 200 * 100 + 100 * 5)  # meta + lower
+
+
+def hdqn_leg(env, args, world, dist, torch):
+    """hdqn.py's acting loop (scripts/hdqn.py:280-323) fused with the env step (mg_rollout_hdqn):
+    per env-step Goal_DQN's meta-net (10 -> 3) on the next state and the lower-level Net
+    (11 -> 5) on the goal state, both bf16 MFMA, L0 opponent. The nets are seeded draws with
+    hdqn.py:41-47's initialisation (no h-DQN checkpoint ships with the reference)."""
+    import numpy as np
+
+    from merging_gym.policy import NUM_GOALS, QNet
+
+    rng = np.random.default_rng(0)
+
+    def net(i, o):
+        sd = {}
+        for name, (a, b) in zip(("fc1", "fc2", "out"), [(200, i), (100, 200), (o, 100)]):
+            sd[f"{name}.weight"] = rng.uniform(0, 1, (a, b)).astype(np.float32)
+            sd[f"{name}.bias"] = rng.uniform(-b ** -0.5, b ** -0.5, a).astype(np.float32)
+        return QNet.from_state_dict(sd, device=env.device)
+
+    meta, lower = net(10, NUM_GOALS), net(11, 5)
+    T, L, E = args.rollout_steps, args.qnet_launches, env.num_envs
+    k = 40_000_000
+    for _ in range(max(1, args.leg_warmup)):
+        env.rollout_hdqn(T, meta, lower, args.seed, first_step=k, final_observation=False)
+        k += T
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    ev0.record()
+    for j in range(L):
+        env.rollout_hdqn(T, meta, lower, args.seed, first_step=k, final_observation=False)
+        k += T
+    ev1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / L
+    per_s = E * T / (kernel_ms * 1e-3)
+    return {"kernel": "hdqn_rollout_kernel<0>", "opponent": "none", "steps_per_launch": T, "launches": L,
+            "dtype": "bf16 (fp32 accumulate)", "value": world * E * T * L / elapsed, "unit": "env-steps/s",
+            "ms_per_step": elapsed / (L * T) * 1e3, "kernel_ms_mean": kernel_ms,
+            "useful_tflops": HDQN_USEFUL_FLOP * per_s / 1e12, "peak_tflops": MFMA_BF16_PEAK_TFLOPS,
+            "frac_useful": HDQN_USEFUL_FLOP * per_s / 1e12 / MFMA_BF16_PEAK_TFLOPS}
+
+
 def replay_algorithmic_bytes(n, T, kept, done_rows, capacity):
     """Bytes mg_replay_store must move at minimum: every obs row once (40) + the trajectory's
     interleaved (a1, a2, done, collision) word (4: a and done are read from it) + won bits (read by
@@ -504,6 +554,10 @@ def main():
     if args.qnet_launches > 0 and args.rollout_steps > 0:
         qnet = [qnet_leg(env, args, world, dist, torch, opp) for opp in ("none", "self")]
 
+    hdqn = None
+    if args.qnet_launches > 0 and args.rollout_steps > 0:
+        hdqn = hdqn_leg(env, args, world, dist, torch)
+
     size2 = None
     if world == 1 and args.size2_envs > 0 and args.size2_envs != E:
         size2 = size2_leg(args, torch)
@@ -551,6 +605,8 @@ def main():
             line["replay"] = replay
         if qnet is not None:
             line["qnet_policy"] = qnet
+        if hdqn is not None:
+            line["hdqn_policy"] = hdqn
         if size2 is not None:
             line["size_2p22"] = size2
         if world == 1 and not args.no_cpu_baseline:

@@ -24,6 +24,9 @@
  *                     replaces the callers' per-step collection loop (scripts/main.py:192-220)
  *   mg_rollout_qnet T steps with the epsilon-greedy DQN policy fused in (bf16 MFMA): replaces
  *                     DQN.choose_action (scripts/main.py:99-112, hdqn.py:165-177) + env.step
+ *   mg_rollout_hdqn   T steps of hdqn.py's acting loop (meta-net goal, lower net on [goal] + state,
+ *                     goal_status intrinsic reward) fused with the env step: replaces
+ *                     Goal_DQN.choose_goal / HDQN.choose_action + env.step (hdqn.py:280-323)
  *   mg_qnet_pack / mg_qnet_forward / mg_qnet_packed_bytes: the Q-net Net (main.py:30-47,
  *                     hdqn.py:38-55) in the kernel's packed bf16 layout, and its forward pass
  *   mg_abi_version, mg_last_error, mg_params_default, mg_time_next_launch: library plumbing
@@ -49,7 +52,7 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 8
+#define MG_ABI_VERSION 9
 #define MG_OBS_DIM 10   /* merging_env.py:75 observation_shape = (10) */
 #define MG_NUM_ACTIONS 5 /* merging_env.py:101-102 action_dict / Discrete(5) */
 #define MG_ACTION_NONE (-1) /* action2=None: the constant-speed "L0" opponent, merging_env.py:152 */
@@ -250,15 +253,16 @@ int mg_rollout_random(const mg_params* params, const mg_state* state, const mg_t
  * A packed Q-net is one device buffer of mg_qnet_packed_bytes() bytes (16-byte aligned) made by
  * mg_qnet_pack from the fp32 torch tensors fc1.weight [200,in], fc1.bias [200], fc2.weight
  * [100,200], fc2.bias [100], out.weight [out,100], out.bias [out] (device pointers, row-major).
- * Weights are stored as bf16, biases as fp32; hidden sizes are the reference's 200 and 100;
- * 1 <= in_dim <= 16, 1 <= out_dim <= 8. */
+ * Weights are stored as bf16; each fp32 bias as three bf16 parts (hi + mid + lo == bias exactly)
+ * in padded K slots whose inputs are 1.0, so the matrix cores add it inside the K sum; hidden
+ * sizes are the reference's 200 and 100; 1 <= in_dim <= 13, 1 <= out_dim <= 8. */
 size_t mg_qnet_packed_bytes(void);
 int mg_qnet_pack(const float* fc1_w, const float* fc1_b, const float* fc2_w, const float* fc2_b,
                  const float* out_w, const float* out_b, int32_t in_dim, int32_t out_dim,
                  void* packed, void* stream);
 
 /* q[n,8] fp32 = Net(x[n,in_dim]) with bf16 operands and fp32 accumulation (rows >= out_dim are
- * padding; in_dim is the net's, 1..16: 10 for main.py's Net on observations, 11 for hdqn.py's
+ * padding; in_dim is the net's, 1..13: 10 for main.py's Net on observations, 11 for hdqn.py's
  * lower-level Net on goal states [goal] + state, :145, :291). swap_halves != 0 (in_dim 10 only)
  * feeds the opponent's view x[5:] + x[:5] (main.py:199). */
 int mg_qnet_forward(const void* packed, const float* x, int32_t in_dim, int32_t swap_halves, float* q,
@@ -277,6 +281,37 @@ int mg_rollout_qnet(const mg_params* params, const mg_state* state, const mg_tra
                     uint64_t first_step, int32_t num_steps, const void* net, int32_t out_dim,
                     uint64_t greedy_threshold, int32_t opponent_mode,
                     uint64_t opp_greedy_threshold, uint32_t flags, void* stream);
+
+/* ---- h-DQN acting loop (scripts/hdqn.py:280-323) ----------------------------------------------
+ * The per-step outputs of mg_rollout_hdqn besides mg_traj, [T, n] fp32 each (NULL skips one):
+ * exactly the goal columns and intrinsic reward hdqn.py's lower-level store_transition takes
+ * (:291, :304, :314, :316) -- feed them to mg_replay_store as mg_transitions.goal / next_goal /
+ * reward for the 24-float goal rows. */
+typedef struct mg_hdqn_traj {
+  float* goal;       /* goal of step t's goal state [goal] + state (:291) */
+  float* next_goal;  /* goal Goal_DQN chose on step t's next state (:303; the terminal one at an
+                        episode end), the row's next goal */
+  float* reward;     /* 1.0 if next_goal == goal_status(state) else 0.0 (:314) */
+} mg_hdqn_traj;
+
+/* num_steps steps of hdqn.py's inner loop in ONE launch (opponent L0 or uniform random): per env
+ * and step, the lower-level Net (lower_net: in 11, out 5) acts epsilon-greedily on the goal
+ * state [goal] + state, the env steps, Goal_DQN's meta-net (meta_net: in 10, out num_goals)
+ * chooses the next goal epsilon-greedily on the next state, goal_status gives the intrinsic
+ * reward, and a fresh goal is chosen when that goal is already reached or the episode ended
+ * (:320-322, :278-283; reset_goal = the meta-net's argmax on the reset observation, which the
+ * caller computes once). goal [n] int8 holds each env's current goal across launches (< 0: none
+ * yet -- chosen by the meta-net at the first step). Random draws: Philox4x32-10 with key seed,
+ * counter (env_offset + i, first_step + t) for the action and next goal (x, y, z, w = explore,
+ * action, explore, goal) and counter ((env_offset + i) ^ 2^63, first_step + t) for a fresh goal
+ * (x, y) and the uniform opponent (z); a launch's first fresh goals use step first_step - 1.
+ * Greedy when the explore draw < greedy_threshold (np.random.randn() <= EPISILO, :84, :168).
+ * traj as mg_rollout_qnet; opponent_mode 0 (None) or 1 (uniform). */
+int mg_rollout_hdqn(const mg_params* params, const mg_state* state, const mg_traj* traj,
+                    const mg_hdqn_traj* htraj, const mg_stats* stats, int8_t* goal, int64_t n,
+                    int64_t env_offset, uint64_t seed, uint64_t first_step, int32_t num_steps,
+                    const void* meta_net, int32_t num_goals, const void* lower_net, int32_t reset_goal,
+                    uint64_t greedy_threshold, int32_t opponent_mode, uint32_t flags, void* stream);
 
 /* ---- replay memory (scripts/main.py:91-92, :115-119, :130-135) --------------------------------
  * rows: [capacity, row_floats] fp32 device buffer, row = [s(10), a, r, s'(10)] like

@@ -1184,15 +1184,24 @@ __device__ __forceinline__ void qnet_forward(const uint8_t* net, const float* ti
 // instead of between dependent MFMAs. Unrolled, the first MFMA into each layer-2 accumulator
 // takes an inline zero and the fragments built for the next tile land in their final
 // registers (rolled, 128 zeroing moves per forward plus ~14 rotation moves per tile: -5..7 %).
+// The forward from the layer-1 B fragments of the wave's two 32-env column tiles (xb0: envs
+// row0 + r, xb1: envs row0 + 32 + r, k-half h = lane >> 5), for callers that build the input
+// themselves (the h-DQN kernel's goal states and terminal observations).
+__device__ __forceinline__ void qnet_mlp_swp(const uint8_t* net, bf16x8 xb0, bf16x8 xb1, float (&q)[8]);
+
 __device__ __forceinline__ void qnet_forward_swp(const uint8_t* net, const float* tile, int row0,
                                                  bool swap, float (&q)[8]) {
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  qnet_mlp_swp(net, qnet_input(tile + (row0 + r) * kObs, swap, h),
+               qnet_input(tile + (row0 + 32 + r) * kObs, swap, h), q);
+}
+
+__device__ __forceinline__ void qnet_mlp_swp(const uint8_t* net, bf16x8 xb0, bf16x8 xb1, float (&q)[8]) {
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int z = opaque_zero();
   const __bf16* W1 = reinterpret_cast<const __bf16*>(net) + z;
   const __bf16* W2 = reinterpret_cast<const __bf16*>(net + kQOffW2) + z;
   const __bf16* W3 = reinterpret_cast<const __bf16*>(net + kQOffW3) + z;
-  const bf16x8 xb0 = qnet_input(tile + (row0 + r) * kObs, swap, h);
-  const bf16x8 xb1 = qnet_input(tile + (row0 + 32 + r) * kObs, swap, h);
   f32x16 acc2a[4] = {}, acc2b[4] = {};
   const f32x16 zero = {};
   auto layer1 = [&](int mt, f32x16& c0, f32x16& c1) {
@@ -1614,6 +1623,257 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
     if (live0[j]) store_env(R.S, base + la, e0[j]);
     if (live1[j]) store_env(R.S, base + kHalf + la, e1[j]);
   }
+}
+
+// ============================================================================ h-DQN acting loop
+// hdqn.py's inner loop (scripts/hdqn.py:280-323) in one launch: Goal_DQN's meta-net picks the
+// sub-goal on every next state (:303), the lower-level Net acts on the goal state
+// [goal] + state (:291-292), goal_status (:223-237) gives the intrinsic reward (:314) and ends
+// the inner loop (:320-322), after which -- and after every episode end (:278-283, the outer
+// loops) -- a fresh goal is chosen. Both nets live in LDS (compact packing, 2 x 60.5 KB).
+//
+// Per env-step k (global step index) the Philox4x32-10 streams are
+//   A = Philox(counter (gi, k)):            x ego explore draw, y ego random action,
+//                                           z goal explore draw, w random goal (the goal
+//                                           chosen on the step's next state, :303)
+//   B = Philox(counter (gi ^ 2^63, k)):     x, y the same for a fresh goal (after a goal was
+//                                           reached or the episode ended, :283), z the uniform
+//                                           opponent's action (opponent_mode 1)
+// and a launch whose env has no goal yet (goal[i] < 0) starts it with B of step first_step - 1.
+// Roles as in qnet_rollout_ws_kernel: waves 0-3 run both nets (meta then lower, one 64-env tile
+// each per phase), waves 4-7 the fp64 env step (one env per lane), on two groups of 256 envs
+// pipelined over 2T + 2 phases: Q(A,0) | Q(B,0) + E(A,0) | ... | Q(A,T) + E(B,T-1) | Q(B,T).
+// Q(X,t) finishes step t-1's goal logic (meta on its next state: the terminal observation where
+// the episode ended, kept in LDS as bf16 pairs) and picks step t's action; E(X,t) steps.
+struct HRollout {
+  mg_params P;
+  mg_state S;
+  mg_traj T;
+  mg_hdqn_traj H;
+  mg_stats St;
+  int8_t* goal;  // [n] in / out
+  const uint8_t* meta;
+  const uint8_t* lower;
+  uint64_t seed;
+  uint64_t first_step;
+  uint64_t greedy_thr;
+  int64_t env_offset;
+  int64_t n;
+  int32_t num_steps;
+  int32_t num_goals;
+  int32_t reset_goal;
+  uint32_t flags;
+};
+
+constexpr int kHEnvs = 512;              // envs per block: two groups of 256
+constexpr int kHHalf = kHEnvs / 2;
+constexpr uint8_t kHGreedy = 0xFF;       // draw byte: take the greedy choice
+
+// goal_status (hdqn.py:223-237) of an fp32 observation: dx1 = o[0], v2 = o[9]
+__device__ __forceinline__ int goal_status(const obs_t (&o)[kObs]) {
+  const float dx1 = static_cast<float>(o[0]), v2 = static_cast<float>(o[9]);
+  return dx1 < -0.5f * v2 ? 0 : (dx1 < 0.5f * v2 ? 1 : 2);
+}
+
+__device__ __forceinline__ uint8_t draw_byte(uint32_t explore, uint32_t pick, uint64_t thr, int k) {
+  return static_cast<uint8_t>(static_cast<uint64_t>(explore) < thr
+                                  ? kHGreedy
+                                  : (static_cast<uint64_t>(pick) * static_cast<uint64_t>(k)) >> 32);
+}
+
+__device__ __forceinline__ uint4 philox_env_step(uint64_t gi, uint64_t step, uint64_t seed) {
+  return philox4x32_10(make_uint4(static_cast<uint32_t>(gi), static_cast<uint32_t>(gi >> 32),
+                                  static_cast<uint32_t>(step), static_cast<uint32_t>(step >> 32)),
+                       static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32));
+}
+
+// lower-net input of one env: goal state [goal] + state (hdqn.py:291), features 0..10, zero at
+// 11..12 and the bias inputs 1.0 at 13..15
+__device__ __forceinline__ bf16x8 qnet_input_goal(const float* row, int goal, int h) {
+  float v[kObs];
+#pragma unroll
+  for (int k = 0; k < kObs / 2; ++k) {
+    const f32x2 t = reinterpret_cast<const f32x2*>(row)[k];
+    v[2 * k] = t[0];
+    v[2 * k + 1] = t[1];
+  }
+  auto pk = [](float a, float b) { return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2)); };
+  const u32x4 w = h ? u32x4{pk(v[7], v[8]), pk(v[9], 0.f), 0x3F800000u, 0x3F803F80u}
+                    : u32x4{pk(static_cast<float>(goal), v[0]), pk(v[1], v[2]), pk(v[3], v[4]), pk(v[5], v[6])};
+  return __builtin_bit_cast(bf16x8, w);
+}
+
+// meta-net input of one env from its bf16-pair side row (the terminal observation)
+__device__ __forceinline__ bf16x8 qnet_input_pairs(const uint32_t* side, int h) {
+  return __builtin_bit_cast(bf16x8, h ? u32x4{side[4], 0u, 0x3F800000u, 0x3F803F80u}
+                                      : u32x4{side[0], side[1], side[2], side[3]});
+}
+
+template <int OPP>
+__global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds_meta[kQNetBytes];
+  __shared__ __attribute__((aligned(16))) uint8_t lds_lower[kQNetBytes];
+  __shared__ __attribute__((aligned(16))) float tile[kHEnvs * kObs];    // s' (reset obs where done)
+  __shared__ __attribute__((aligned(16))) uint32_t side[kHEnvs * 5];    // terminal obs, bf16 pairs
+  __shared__ uint8_t b_act[kHEnvs], b_goal[kHEnvs], b_done[kHEnvs], b_st_old[kHEnvs],
+      b_st_new[kHEnvs], b_dg[kHEnvs], b_df[kHEnvs];
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kHEnvs;
+  const int T = R.num_steps;
+  const int phases = 2 * T + 2;
+  {
+    const f32x4* s1 = reinterpret_cast<const f32x4*>(R.meta);
+    const f32x4* s2 = reinterpret_cast<const f32x4*>(R.lower);
+    f32x4* d1 = reinterpret_cast<f32x4*>(lds_meta);
+    f32x4* d2 = reinterpret_cast<f32x4*>(lds_lower);
+    for (int j = tid; j < kQNetBytes / 16; j += blockDim.x) {
+      d1[j] = s1[j];
+      d2[j] = s2[j];
+    }
+  }
+  if (wave < 4) {
+    // ---------------------------------------------------------------- the two nets
+    __syncthreads();
+    const int r = lane & 31, h = lane >> 5;
+    for (int p = 0; p < phases; ++p) {
+      const int g = p & 1, t = p >> 1;
+      const int row0 = g * kHHalf + 64 * wave;  // this wave's 64 envs: rows row0 + lane
+      const int j = row0 + lane;
+      const int64_t i = base + j;
+      const bool live = i < R.n;
+      const int goal_prev = static_cast<int8_t>(b_goal[j]);
+      int goal_t;
+      const bool need_meta = t > 0 || __ballot(live && goal_prev < 0) != 0;
+      int gstar = 0;
+      if (need_meta) {  // meta-net on the next state of step t - 1 (on s_0 for a launch's first goals)
+        const bool d0 = t > 0 && b_done[row0 + r], d1 = t > 0 && b_done[row0 + 32 + r];
+        const bf16x8 x0 = d0 ? qnet_input_pairs(side + (row0 + r) * 5, h)
+                             : qnet_input(tile + (row0 + r) * kObs, false, h);
+        const bf16x8 x1 = d1 ? qnet_input_pairs(side + (row0 + 32 + r) * 5, h)
+                             : qnet_input(tile + (row0 + 32 + r) * kObs, false, h);
+        float q[8];
+        qnet_mlp_swp(lds_meta, x0, x1, q);
+        gstar = argmax_first(q, R.num_goals);
+      }
+      const int df = b_df[j];
+      if (t > 0) {  // hdqn.py:303-322 for step t - 1
+        const int dg = b_dg[j];
+        const int goal2 = dg == kHGreedy ? gstar : dg;
+        const bool done = b_done[j] != 0;
+        const bool brk = done || goal2 == b_st_new[j];
+        goal_t = done ? (df == kHGreedy ? R.reset_goal : df) : (brk ? (df == kHGreedy ? gstar : df) : goal2);
+        if (live) {
+          const int64_t row = static_cast<int64_t>(t - 1) * R.n + i;
+          if (R.H.next_goal) st_out(R.H.next_goal + row, static_cast<float>(goal2));
+          if (R.H.reward) st_out(R.H.reward + row, goal2 == b_st_old[j] ? 1.0f : 0.0f);
+        }
+      } else {
+        goal_t = goal_prev >= 0 ? goal_prev : (df == kHGreedy ? gstar : df);
+      }
+      if (t < T) {
+        b_goal[j] = static_cast<uint8_t>(goal_t);
+        if (live && R.H.goal) st_out(R.H.goal + static_cast<int64_t>(t) * R.n + i, static_cast<float>(goal_t));
+        wave_lds_sync();  // the wave's goals are in LDS before the lanes read their column envs'
+        float q[8];
+        qnet_mlp_swp(lds_lower, qnet_input_goal(tile + (row0 + r) * kObs, b_goal[row0 + r], h),
+                     qnet_input_goal(tile + (row0 + 32 + r) * kObs, b_goal[row0 + 32 + r], h), q);
+        b_act[j] = static_cast<uint8_t>(argmax_first(q, MG_NUM_ACTIONS));
+      } else if (live) {
+        R.goal[i] = static_cast<int8_t>(goal_t);  // the next launch's starting goal
+      }
+      __syncthreads();
+    }
+    return;
+  }
+  // ------------------------------------------------------------------ the env step
+  const int ew = wave - 4;
+  Env e[2];
+  StepOut r[2];
+  bool live[2];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int j = g * kHHalf + 64 * ew + lane;
+    const int64_t i = base + j;
+    live[g] = i < R.n;
+    double o[kObs];
+    if (live[g]) {
+      e[g] = load_env(R.S, i);
+      double x1, y1, x2, y2;
+      lon2coord(R.P, e[g].p1, true, x1, y1);
+      lon2coord(R.P, e[g].p2, false, x2, y2);
+      observe(R.P, e[g].p1, e[g].v1, e[g].p2, e[g].v2, x1, y1, x2, y2, o);
+    } else {  // a defined state, stepped but never stored
+      e[g].p1 = e[g].p2 = R.P.start_point;
+      e[g].v1 = e[g].v2 = R.P.start_vel;
+      e[g].ret1 = e[g].ret2 = 0.0;
+      e[g].steps = 0;
+      e[g].winner = 0;
+      e[g].done = false;
+#pragma unroll
+      for (int k = 0; k < kObs; ++k) o[k] = 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < kObs; ++k) r[g].o[k] = static_cast<obs_t>(o[k]);
+    float2* t2 = reinterpret_cast<float2*>(tile + j * kObs);
+#pragma unroll
+    for (int k = 0; k < kObs / 2; ++k) t2[k] = make_float2(static_cast<float>(r[g].o[2 * k]), static_cast<float>(r[g].o[2 * k + 1]));
+    const uint64_t gi = static_cast<uint64_t>(R.env_offset + i);
+    const uint4 fb = philox_env_step(gi ^ (uint64_t{1} << 63), R.first_step - 1, R.seed);
+    b_df[j] = draw_byte(fb.x, fb.y, R.greedy_thr, R.num_goals);
+    b_goal[j] = live[g] ? static_cast<uint8_t>(R.goal[i]) : 0;
+    b_done[j] = 0;
+  }
+  __syncthreads();
+  for (int p = 0; p < phases; ++p) {
+    if (p > 0 && ((p - 1) >> 1) < T) {
+      const int g = (p - 1) & 1, t = (p - 1) >> 1;
+      const int j = g * kHHalf + 64 * ew + lane;
+      const int64_t i = base + j;
+      const int64_t wbase = base + g * kHHalf + 64 * ew;
+      const uint64_t gi = static_cast<uint64_t>(R.env_offset + i), k = R.first_step + t;
+      const uint4 ua = philox_env_step(gi, k, R.seed);
+      const uint4 ub = philox_env_step(gi ^ (uint64_t{1} << 63), k, R.seed);
+      const int a1 = static_cast<uint64_t>(ua.x) < R.greedy_thr ? static_cast<int>(b_act[j]) : action_from_u32(ua.y);
+      const int a2 = OPP == 1 ? action_from_u32(ub.z) : MG_ACTION_NONE;
+      auto step = [&](Env& ev, StepOut& rv, bool lv) __attribute__((always_inline)) {
+        b_st_old[j] = static_cast<uint8_t>(goal_status(rv.o));  // status of the state acted on
+        env_step(R.P, ev, a1, a2, rv);
+        const int64_t row = static_cast<int64_t>(t) * R.n + i;
+        if (lv) {
+          if (R.T.rew) st_out(reinterpret_cast<f32x2*>(R.T.rew) + row, f32x2{static_cast<float>(rv.r1), static_cast<float>(rv.r2)});
+          store_step_bytes(R.T, row, a1, a2, rv.done, rv.coll);
+        }
+        b_done[j] = rv.done ? 1 : 0;
+        b_st_new[j] = static_cast<uint8_t>(goal_status(rv.o));
+        b_dg[j] = draw_byte(ua.z, ua.w, R.greedy_thr, R.num_goals);
+        b_df[j] = draw_byte(ub.x, ub.y, R.greedy_thr, R.num_goals);
+        const bool won = lv && ev.winner == 1;
+        const int64_t rem = R.n - wbase;
+        store_won_mask(R.T.won_mask, won, t, R.n, wbase, rem <= 0 ? 0 : (rem < 64 ? static_cast<int>(rem) : 64));
+        if (lv && (R.flags & MG_AUTORESET) && rv.done) {
+          uint32_t* sd = side + j * 5;  // the terminal observation for the meta-net
+#pragma unroll
+          for (int q2 = 0; q2 < kObs / 2; ++q2)
+            sd[q2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(
+                                                      f32x2{static_cast<float>(rv.o[2 * q2]), static_cast<float>(rv.o[2 * q2 + 1])}, bf16x2));
+          finish_episode(R.P, ev, rv, R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i);
+        }
+        const int64_t wrem = R.n - wbase;
+        wave_store_obs(tile + (g * kHHalf + 64 * ew) * kObs, rv.o,
+                       R.T.obs ? R.T.obs + (static_cast<int64_t>(t) * R.n + wbase) * kObs : nullptr,
+                       wrem <= 0 ? 0 : (wrem < 64 ? static_cast<int>(wrem) : 64));
+      };
+      if (g == 0)
+        step(e[0], r[0], live[0]);
+      else
+        step(e[1], r[1], live[1]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+    if (live[g]) store_env(R.S, base + g * kHHalf + 64 * ew + lane, e[g]);
 }
 
 __global__ __launch_bounds__(kBlock) void reset_kernel(const mg_params P, const mg_state S,
@@ -2306,6 +2566,54 @@ int mg_rollout_qnet(const mg_params* params, const mg_state* state, const mg_tra
 #undef MG_LAUNCH_Q
 #undef MG_QKERNEL
   return finish_launch("mg_rollout_qnet");
+}
+
+int mg_rollout_hdqn(const mg_params* params, const mg_state* state, const mg_traj* traj,
+                    const mg_hdqn_traj* htraj, const mg_stats* stats, int8_t* goal, int64_t n,
+                    int64_t env_offset, uint64_t seed, uint64_t first_step, int32_t num_steps,
+                    const void* meta_net, int32_t num_goals, const void* lower_net, int32_t reset_goal,
+                    uint64_t greedy_threshold, int32_t opponent_mode, uint32_t flags, void* stream) {
+  mg_outputs none{};
+  if (int e = check_common(params, state, &none, n)) return e;
+  if (!traj) return fail(hipErrorInvalidValue, "%s", "traj is NULL (pass a zeroed mg_traj)");
+  if (!goal) return fail(hipErrorInvalidValue, "%s", "goal is NULL (an [n] int8 device array)");
+  if (!meta_net || !lower_net || ((reinterpret_cast<uintptr_t>(meta_net) | reinterpret_cast<uintptr_t>(lower_net)) & 15))
+    return fail(hipErrorInvalidValue, "%s", "meta_net / lower_net must be 16-byte aligned packed Q-nets");
+  if (num_steps < 0 || num_goals < 1 || num_goals > 8 || reset_goal < 0 || reset_goal >= num_goals)
+    return fail(hipErrorInvalidValue, "%s", "need num_steps >= 0, 1 <= num_goals <= 8, 0 <= reset_goal < num_goals");
+  if (opponent_mode < 0 || opponent_mode > 1)
+    return fail(hipErrorInvalidValue, "%s", "opponent_mode must be 0 (None) or 1 (uniform)");
+  if ((traj->obs && (reinterpret_cast<uintptr_t>(traj->obs) & 15)) ||
+      (traj->final_obs && (reinterpret_cast<uintptr_t>(traj->final_obs) & 7)) ||
+      (traj->rew && (reinterpret_cast<uintptr_t>(traj->rew) & 7)) ||
+      (reinterpret_cast<uintptr_t>(traj->flags) & 3))
+    return fail(hipErrorInvalidValue, "%s", "traj.obs must be 16-byte, rew/final_obs 8-byte, flags 4-byte aligned");
+  if (n == 0 || num_steps == 0) return 0;
+  HRollout R{};
+  R.P = *params;
+  R.S = *state;
+  R.T = *traj;
+  if (htraj) R.H = *htraj;
+  if (stats) R.St = *stats;
+  R.goal = goal;
+  R.meta = static_cast<const uint8_t*>(meta_net);
+  R.lower = static_cast<const uint8_t*>(lower_net);
+  R.seed = seed;
+  R.first_step = first_step;
+  R.greedy_thr = greedy_threshold;
+  R.env_offset = env_offset;
+  R.n = n;
+  R.num_steps = num_steps;
+  R.num_goals = num_goals;
+  R.reset_goal = reset_goal;
+  R.flags = flags;
+  const unsigned blocks = static_cast<unsigned>((n + kHEnvs - 1) / kHEnvs);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (opponent_mode == 0)
+    hipLaunchKernelGGL(hdqn_rollout_kernel<0>, dim3(blocks), dim3(512), 0, st, R);
+  else
+    hipLaunchKernelGGL(hdqn_rollout_kernel<1>, dim3(blocks), dim3(512), 0, st, R);
+  return finish_launch("mg_rollout_hdqn");
 }
 
 size_t mg_replay_scratch_bytes(int64_t n, int32_t num_steps) {

@@ -15,7 +15,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libmerging_hip.so"
 LIB_PATH = os.environ.get("MERGING_HIP_LIB", os.path.join(_HERE, LIB_NAME))
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 OBS_DIM = 10
 NUM_ACTIONS = 5
@@ -61,6 +61,10 @@ class Traj(_c.Structure):
 class Transitions(_c.Structure):
     _fields_ = [(n, _P) for n in ("obs_first", "obs", "final_obs", "a1", "rew", "done", "won_mask", "goal",
                                   "next_goal", "reward", "flags")]
+
+
+class HdqnTraj(_c.Structure):
+    _fields_ = [(n, _P) for n in ("goal", "next_goal", "reward")]
 
 
 class Stats(_c.Structure):
@@ -109,6 +113,9 @@ def _load():
     lib.mg_rollout_qnet.argtypes = [PP, SP, _c.POINTER(Traj), STP, _c.c_int64, _c.c_int64, _c.c_uint64,
                                     _c.c_uint64, _c.c_int32, _P, _c.c_int32, _c.c_uint64, _c.c_int32,
                                     _c.c_uint64, _c.c_uint32, _P]
+    lib.mg_rollout_hdqn.argtypes = [PP, SP, _c.POINTER(Traj), _c.POINTER(HdqnTraj), STP, _P, _c.c_int64,
+                                    _c.c_int64, _c.c_uint64, _c.c_uint64, _c.c_int32, _P, _c.c_int32, _P,
+                                    _c.c_int32, _c.c_uint64, _c.c_int32, _c.c_uint32, _P]
     lib.mg_time_next_launch.argtypes = [_P, _P]
     lib.mg_replay_scratch_bytes.argtypes = [_c.c_int64, _c.c_int32]
     lib.mg_replay_scratch_bytes.restype = _c.c_size_t
@@ -118,7 +125,7 @@ def _load():
                                      _P, _c.c_int64, _P]
     for f in (lib.mg_step, lib.mg_step_random, lib.mg_reset, lib.mg_observe, lib.mg_rollout_random,
               lib.mg_time_next_launch, lib.mg_qnet_pack, lib.mg_qnet_forward, lib.mg_rollout_qnet,
-              lib.mg_replay_store, lib.mg_replay_sample):
+              lib.mg_rollout_hdqn, lib.mg_replay_store, lib.mg_replay_sample):
         f.restype = _c.c_int
     v = lib.mg_abi_version()
     if v != ABI_VERSION:

@@ -307,6 +307,47 @@ class MergeVecEnv:
         self._step_idx = k0 + T
         return buf["_result"]
 
+    def rollout_hdqn(self, num_steps: int, meta, lower, seed: int, opponent: str = "none",
+                     episilo: float = 0.7, first_step=None, final_observation: bool = True,
+                     won_mask: bool = False):
+        """`num_steps` steps of hdqn.py's inner loop (scripts/hdqn.py:280-323) in one launch:
+        Goal_DQN's meta-net (`meta`, a QNet 10 -> num_goals) picks each env's sub-goal on every
+        next state, the lower-level Net (`lower`, a QNet 11 -> 5) acts epsilon-greedily on the
+        goal state [goal] + state, goal_status gives the intrinsic reward, and a fresh goal is
+        chosen once a goal is reached or an episode ends. opponent: "none" (L0, hdqn.py's default
+        Strategy_OP) or "uniform". Each env's current goal persists across launches in
+        `self.hdqn_goal` ([N] int8, -1 = none yet). Returns rollout_random's [T, N, ...] dict
+        plus "goal", "next_goal" and "reward" ([T, N] fp32: the goal columns and the intrinsic
+        reward of HDQN.store_transition's rows, :316 -- ReplayRing(goal=True).store_rollout takes
+        them as they are)."""
+        from ..policy import greedy_threshold
+
+        torch, nat = self._torch, self._nat
+        T, n = int(num_steps), self.num_envs
+        mode = {"none": 0, "uniform": 1}[opponent]
+        if meta.in_dim != _OBS_DIM or lower.in_dim != _OBS_DIM + 1 or lower.out_dim != nat.NUM_ACTIONS:
+            raise ValueError("need hdqn.py's nets: meta-net in_dim 10, lower-level Net in_dim 11 -> 5")
+        k0 = self._step_idx if first_step is None else int(first_step)
+        buf = self._traj(T, final_observation, won_mask)
+        hb = getattr(self, "_hdqn_bufs", None)
+        if hb is None or hb["goal"].shape[0] != T:
+            hb = {k: torch.empty((T, n), dtype=torch.float32, device=self.device)
+                  for k in ("goal", "next_goal", "reward")}
+            hb["_h"] = nat.HdqnTraj(*(hb[k].data_ptr() for k in ("goal", "next_goal", "reward")))
+            self._hdqn_bufs = hb
+        if getattr(self, "hdqn_goal", None) is None:
+            self.hdqn_goal = torch.full((n,), -1, dtype=torch.int8, device=self.device)
+        rc = nat.lib.mg_rollout_hdqn(
+            self._p_ref, self._s_ref, ctypes.byref(buf["_traj"]), ctypes.byref(hb["_h"]), self._st_ref,
+            self.hdqn_goal.data_ptr(), n, self.env_offset, seed & 0xFFFFFFFFFFFFFFFF, k0 & 0xFFFFFFFFFFFFFFFF,
+            T, meta.packed.data_ptr(), meta.out_dim, lower.packed.data_ptr(), meta.reset_argmax(),
+            greedy_threshold(episilo), mode, self._flags, self._stream())
+        nat.check(rc, "mg_rollout_hdqn")
+        self._step_idx = k0 + T
+        out = dict(buf["_result"])
+        out.update(goal=hb["goal"], next_goal=hb["next_goal"], reward=hb["reward"])
+        return out
+
     def observe(self):
         """Observation of the current state without stepping (merging_env.py:118-132)."""
         out = self._nat.Outputs(self._out.obs, None, None, self._out.coll)
@@ -375,6 +416,8 @@ class MergeVecEnv:
         sd["env_offset"] = self.env_offset
         if self.ret_sum is not None:
             sd["ret_sum"], sd["counts"] = self.ret_sum.clone(), self.counts.clone()
+        if getattr(self, "hdqn_goal", None) is not None:
+            sd["hdqn_goal"] = self.hdqn_goal.clone()  # rollout_hdqn's current goals
         return sd
 
     def load_state_dict(self, sd):
@@ -390,6 +433,8 @@ class MergeVecEnv:
         if self.ret_sum is not None and "ret_sum" in sd:
             self.ret_sum.copy_(self._torch.as_tensor(sd["ret_sum"]))
             self.counts.copy_(self._torch.as_tensor(sd["counts"]))
+        if "hdqn_goal" in sd:
+            self.hdqn_goal = self._torch.as_tensor(sd["hdqn_goal"]).to(self.device, self._torch.int8).clone()
 
     def close(self):
         pass

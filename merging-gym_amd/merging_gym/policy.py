@@ -65,6 +65,19 @@ class QNet:
         _native.check(_native.lib.mg_qnet_pack(*(t.data_ptr() for t in ts), self.in_dim, self.out_dim,
                                                self.packed.data_ptr(), stream), "mg_qnet_pack")
 
+    def reset_argmax(self) -> int:
+        """argmax of this net on the reset observation (merging_env.py:208-230), computed once on
+        the device: the greedy goal Goal_DQN picks after every episode end (hdqn.py:278-283),
+        which mg_rollout_hdqn takes as a constant."""
+        if getattr(self, "_reset_argmax", None) is None:
+            from .envs.vector_env import MergeVecEnv
+
+            if self.in_dim != 10:
+                raise ValueError("reset_argmax needs a net on the 10-value observation")
+            one = MergeVecEnv(1, device=self.device, final_observation=False, episode_stats=False)
+            self._reset_argmax = int(self.forward(one.reset())[0].argmax())
+        return self._reset_argmax
+
     @classmethod
     def from_state_dict(cls, sd, device=None):
         return cls(sd["fc1.weight"], sd["fc1.bias"], sd["fc2.weight"], sd["fc2.bias"], sd["out.weight"],

@@ -107,3 +107,119 @@ def test_batched_hdqn_inner_loop(coracle):
     np.testing.assert_array_equal(ring.memory.cpu().numpy(), mem)
     s, a, r, s2 = ring.sample(128, seed=1, draw=2)  # learn()'s slices, hdqn.py:196-199
     assert s.shape == (128, 11) and s2.shape == (128, 11) and a.shape == (128, 1) and r.shape == (128, 1)
+
+
+def _status(o):
+    """goal_status (hdqn.py:223-237) of fp32 observation rows [N, 10]."""
+    dx1, v2 = o[:, 0], o[:, 9]
+    return np.where(dx1 < np.float32(-0.5) * v2, 0, np.where(dx1 < np.float32(0.5) * v2, 1, 2))
+
+
+def _pick(u, k):  # floor(k u / 2^32)
+    return ((u.astype(np.uint64) * np.uint64(k)) >> np.uint64(32)).astype(np.int64)
+
+
+@pytest.mark.parametrize("n", [2048, 1000])
+def test_fused_hdqn_rollout(coracle, n):
+    """mg_rollout_hdqn -- hdqn.py:280-323 in one launch -- against the loop restated on the CPU:
+    every transition equals the C oracle's given the kernel's actions; every action, next goal and
+    fresh goal is the epsilon-greedy choice its Philox draws make with the bf16-emulated nets'
+    argmax (near-ties excused); the intrinsic reward is goal_status's; the goal ring the
+    trajectory feeds equals the oracle's replay_store bit for bit. Starts mid-episode, so goals
+    are reached and episodes end inside the launch; a second launch continues the goals."""
+    import torch
+
+    from merging_gym import MergeVecEnv, ReplayRing
+    from merging_gym.policy import NUM_GOALS, QNet, greedy_threshold
+
+    T, seed, dev = 24, 9, "cuda:0"
+    rng = np.random.default_rng(21)
+    meta_sd, lower_sd = _net(rng, 10, NUM_GOALS), _net(rng, 11, 5)
+    meta, lower = QNet.from_state_dict(meta_sd, device=dev), QNet.from_state_dict(lower_sd, device=dev)
+    thr = greedy_threshold()
+    env = MergeVecEnv(n, device=dev, final_observation=True)
+    k0 = 190
+    for k in range(k0):
+        env.step_random(5, opponent_random=False, step_idx=k)
+    envs = coracle.new_envs(n)
+    for name, src in (("pos1", env.p1), ("vel1", env.v1), ("pos2", env.p2), ("vel2", env.v2),
+                      ("r1_acc", env.ret1), ("r2_acc", env.ret2)):
+        envs[name] = src.cpu().numpy()
+    envs["steps"] = env.steps.cpu().numpy()
+    envs["winner"] = env.winner.cpu().numpy()
+    envs["time_stamp"] = np.cumsum(np.full(2700, 0.2))[np.maximum(envs["steps"] - 1, 0)] * (envs["steps"] > 0)
+    obs = env.observe().cpu().numpy().copy()
+    reset_goal = meta.reset_argmax()
+    q_reset = mo.qnet_reference(meta_sd, coracle.reset(coracle.new_envs(1)).astype(np.float32), bf16=True)
+    assert reset_goal == q_reset.argmax(1)[0] or _near_tie(q_reset)[0]
+    fresh_off = -(1 << 63)  # counter (env ^ 2^63, step): the fresh-goal stream
+    goal_prev = None
+    rows = {k: [] for k in ("obs0", "obs", "fobs", "a1", "rew", "done", "goal", "goal2", "r_int")}
+    ring = ReplayRing(4 * n * T, device=dev, goal=True)
+    for launch in range(2):
+        obs_first = obs.copy()
+        tr = env.rollout_hdqn(T, meta, lower, seed, first_step=k0)
+        g = {k: tr[k].cpu().numpy().copy() for k in ("goal", "next_goal", "reward")}
+        a1_all, done_all = tr["a1"].cpu().numpy().copy(), tr["done"].cpu().numpy().copy()
+        o_all, fo_all, rew_all = (tr[k].cpu().numpy().copy() for k in ("obs", "final_observation", "rew"))
+        ring.store_rollout(torch.from_numpy(obs_first).to(dev), tr, skip_ego_won=False, goal=tr["goal"],
+                           next_goal=tr["next_goal"], reward=tr["reward"])
+        # the launch's first goals: carried over, or a fresh choice with step k0 - 1's draw
+        if goal_prev is None:
+            fb = coracle.philox_batch(n, fresh_off, seed, k0 - 1)
+            qm = mo.qnet_reference(meta_sd, obs, bf16=True)
+            exp = np.where(fb[:, 0] < thr, qm.argmax(1), _pick(fb[:, 1], NUM_GOALS))
+            ok = (g["goal"][0] == exp) | ((fb[:, 0] < thr) & _near_tie(qm))
+        else:
+            ok = g["goal"][0] == goal_prev
+        assert ok.all(), launch
+        for t in range(T):
+            k = k0 + t
+            ua = coracle.philox_batch(n, 0, seed, k)
+            ub = coracle.philox_batch(n, fresh_off, seed, k)
+            goal_t = g["goal"][t].astype(np.int64)
+            x = np.concatenate([goal_t[:, None].astype(np.float32), obs], axis=1)  # [goal] + state
+            q1 = mo.qnet_reference(lower_sd, x, bf16=True)
+            greedy = ua[:, 0] < thr
+            exp_a = np.where(greedy, q1.argmax(1), _pick(ua[:, 1], 5))
+            assert ((a1_all[t] == exp_a) | (greedy & _near_tie(q1))).all(), (launch, t)
+            o_obs, o_rew, o_done, o_coll, _, o_fobs, err = coracle.step(envs, a1_all[t].astype(np.int8), None,
+                                                                        autoreset=True, final_obs=True)
+            assert err == 0
+            np.testing.assert_array_equal(done_all[t], o_done.astype(bool), err_msg=str(t))
+            np.testing.assert_allclose(o_all[t], o_obs.astype(np.float32), **OBS_TOL)
+            np.testing.assert_allclose(rew_all[t], o_rew.astype(np.float32), **OBS_TOL)
+            d = done_all[t]
+            np.testing.assert_allclose(fo_all[t][d], o_fobs[d].astype(np.float32), **OBS_TOL)
+            s2 = np.where(d[:, None], fo_all[t], o_all[t])  # the next state, terminal where done
+            q2 = mo.qnet_reference(meta_sd, s2, bf16=True)
+            gg = ua[:, 2] < thr
+            exp_g2 = np.where(gg, q2.argmax(1), _pick(ua[:, 3], NUM_GOALS))
+            g2 = g["next_goal"][t].astype(np.int64)
+            assert ((g2 == exp_g2) | (gg & _near_tie(q2))).all(), (launch, t)
+            np.testing.assert_array_equal(g["reward"][t], (g2 == _status(obs)).astype(np.float32))
+            # the goal of the next step: kept, or fresh once reached / after an episode end
+            brk = d | (g2 == _status(s2))
+            gf = ub[:, 0] < thr
+            fresh = np.where(gf, np.where(d, reset_goal, q2.argmax(1)), _pick(ub[:, 1], NUM_GOALS))
+            exp_next = np.where(brk, fresh, g2)
+            nxt = g["goal"][t + 1] if t + 1 < T else env.hdqn_goal.cpu().numpy().astype(np.int64)
+            assert ((nxt == exp_next) | (brk & gf & ~d & _near_tie(q2))).all(), (launch, t)
+            for key, v in (("obs0", obs), ("obs", o_all[t]), ("fobs", fo_all[t]), ("a1", a1_all[t]),
+                           ("rew", rew_all[t]), ("done", d), ("goal", g["goal"][t]), ("goal2", g["next_goal"][t]),
+                           ("r_int", g["reward"][t])):
+                rows[key].append(v.copy())
+            obs = o_all[t]
+        goal_prev = env.hdqn_goal.cpu().numpy().astype(np.int64)
+        k0 += T
+    assert np.stack(rows["done"]).any() and (np.stack(rows["r_int"]) == 1).any()
+    assert (np.stack(rows["goal"]) != np.stack(rows["goal2"])).any()
+    mem = np.zeros((ring.capacity, 24), np.float32)
+    c = 0
+    for t in range(len(rows["obs"])):
+        c = mo.replay_store(mem, c, rows["obs0"][t], rows["obs"][t][None], rows["a1"][t][None].astype(np.int8),
+                            rows["rew"][t][None], rows["done"][t][None], rows["fobs"][t][None], None,
+                            skip_ego_won=False, goal=rows["goal"][t][None], next_goal=rows["goal2"][t][None],
+                            reward=rows["r_int"][t][None])
+    assert ring.memory_counter == c == 2 * n * T
+    np.testing.assert_array_equal(ring.memory.cpu().numpy(), mem)
