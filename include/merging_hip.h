@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 9
+#define MG_ABI_VERSION 10
 #define MG_OBS_DIM 10   /* merging_env.py:75 observation_shape = (10) */
 #define MG_NUM_ACTIONS 5 /* merging_env.py:101-102 action_dict / Discrete(5) */
 #define MG_ACTION_NONE (-1) /* action2=None: the constant-speed "L0" opponent, merging_env.py:152 */
@@ -229,10 +229,11 @@ void mg_params_default(mg_params* p);
 int mg_step(const mg_params* params, const mg_state* state, const int8_t* a1, const int8_t* a2,
             const mg_outputs* out, const mg_stats* stats, int64_t n, uint32_t flags, void* stream);
 
-/* As mg_step, with actions drawn on the device: Philox4x32-10, key = seed, counter =
- * (env_offset + env index, step_idx) -- a shard of a larger batch passes its first global
- * env index as env_offset and draws the same actions it would draw unsharded;
- * a1 = floor(5 u0 / 2^32), a2 = floor(5 u1 / 2^32) when opponent_random != 0, else None.
+/* As mg_step, with actions drawn on the device: w = word (step_idx mod 4) of Philox4x32-10
+ * (key = seed, counter = (env_offset + env index, step_idx div 4)) -- one call covers four
+ * steps of a rollout; a shard of a larger batch passes its first global env index as
+ * env_offset and draws the same actions it would draw unsharded. opponent_random != 0: the
+ * pair x = floor(25 w / 2^32), a1 = x / 5, a2 = x % 5; else a1 = floor(5 w / 2^32), a2 None.
  * If a1_out / a2_out are non-NULL the actions used are written there (-1 for None). */
 int mg_step_random(const mg_params* params, const mg_state* state, int8_t* a1_out,
                    int8_t* a2_out, const mg_outputs* out, const mg_stats* stats, int64_t n,

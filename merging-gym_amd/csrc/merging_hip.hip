@@ -332,21 +332,40 @@ struct StepOut {
   int bad;  // 1: action1 invalid, 2: action2 invalid (the reference's KeyError)
 };
 
-// opaque_key: a uniform key the compiler cannot hoist. In a multi-step loop the 20 round keys
-// are then scalar adds at each use instead of loop invariants spilled into VGPR lanes (one
-// v_readlane, a vector instruction, per round): -2 % per rollout step (A/B); the one-step
-// kernel is better without it.
-__device__ __forceinline__ void draw_actions(uint64_t gi, uint64_t step, uint64_t seed,
-                                             int opp_random, int& a1, int& a2,
-                                             bool opaque_key = false) {
+// The random-policy action stream: step k of global env gi uses word (k mod 4) of
+// u = Philox4x32-10(counter (gi, k div 4), key seed) -- one call covers four steps, so a T-step
+// rollout pays a quarter of the 40 quarter-rate 32-bit multiplies per env-step that one call
+// per step cost (Philox was a third of the rollout kernel's VALU time). With both players
+// random, x = floor(25 w / 2^32) is the action pair, a1 = x div 5, a2 = x mod 5 (25 equally
+// likely pairs up to a 25 / 2^32 bias); with the None opponent a1 = floor(5 w / 2^32).
+__device__ __forceinline__ uint4 philox_block(uint64_t gi, uint64_t block, uint64_t seed,
+                                              bool opaque_key = false) {
   uint32_t k0 = static_cast<uint32_t>(seed), k1 = static_cast<uint32_t>(seed >> 32);
+  // opaque_key: a uniform key the compiler cannot hoist. In a multi-step loop the 20 round keys
+  // are then scalar adds at each use instead of loop invariants spilled into VGPR lanes (one
+  // v_readlane, a vector instruction, per round): -2 % per rollout step (A/B).
   if (opaque_key) asm volatile("" : "+s"(k0), "+s"(k1));
-  const uint4 u = philox4x32_10(
-      make_uint4(static_cast<uint32_t>(gi), static_cast<uint32_t>(gi >> 32),
-                 static_cast<uint32_t>(step), static_cast<uint32_t>(step >> 32)),
-      k0, k1);
-  a1 = action_from_u32(u.x);
-  a2 = opp_random ? action_from_u32(u.y) : MG_ACTION_NONE;
+  return philox4x32_10(make_uint4(static_cast<uint32_t>(gi), static_cast<uint32_t>(gi >> 32),
+                                  static_cast<uint32_t>(block), static_cast<uint32_t>(block >> 32)),
+                       k0, k1);
+}
+
+__device__ __forceinline__ uint32_t philox_word(const uint4& u, uint64_t step) {
+  // word step & 3 by a 64-bit select and shift on values: no indexed private array, no branch
+  const uint64_t lo = (static_cast<uint64_t>(u.y) << 32) | u.x, hi = (static_cast<uint64_t>(u.w) << 32) | u.z;
+  return static_cast<uint32_t>(((step & 2) ? hi : lo) >> (32 * (step & 1)));
+}
+
+__device__ __forceinline__ void actions_from_word(uint32_t w, int opp_random, int& a1, int& a2) {
+  const uint32_t x = static_cast<uint32_t>((static_cast<uint64_t>(w) * 25u) >> 32);  // 0..24
+  const int b1 = static_cast<int>((x * 13u) >> 6);                                     // x div 5
+  a1 = opp_random ? b1 : action_from_u32(w);
+  a2 = opp_random ? static_cast<int>(x) - 5 * b1 : MG_ACTION_NONE;
+}
+
+__device__ __forceinline__ void draw_actions(uint64_t gi, uint64_t step, uint64_t seed, int opp_random,
+                                             int& a1, int& a2) {
+  actions_from_word(philox_word(philox_block(gi, step >> 2, seed), step), opp_random, a1, a2);
 }
 
 // time_stamp += dT; done if time_stamp > 500 (:141-143). The fp64 clock first exceeds 500
@@ -886,12 +905,15 @@ __global__ __launch_bounds__(kBlock, MG_ROLLOUT_WAVES_PER_EU) void rollout_kerne
   }
   StepOut r;
   bool won = false;
+  uint4 u = make_uint4(0u, 0u, 0u, 0u);  // the Philox block of the current four steps
   for (int t = 0; t < R.num_steps; ++t) {
     const int64_t row = static_cast<int64_t>(t) * R.n + i;
+    const uint64_t k = R.first_step + t;
+    if (t == 0 || (k & 3) == 0)  // wave-uniform
+      u = philox_block(static_cast<uint64_t>(R.env_offset + i), k >> 2, R.seed, /*opaque_key=*/true);
     if (live) {
       int a1, a2;
-      draw_actions(static_cast<uint64_t>(R.env_offset + i), R.first_step + t, R.seed, R.opp_random,
-                   a1, a2, /*opaque_key=*/true);
+      actions_from_word(philox_word(u, k), R.opp_random, a1, a2);
       env_step(P, e, a1, a2, r);  // Philox actions are always valid
       if (R.T.rew)
         st_out(reinterpret_cast<f32x2*>(R.T.rew) + row,

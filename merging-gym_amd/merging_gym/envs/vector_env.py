@@ -219,9 +219,9 @@ class MergeVecEnv:
 
     def step_random(self, seed: int, opponent_random: bool = True, step_idx=None,
                     record_actions: bool = True):
-        """One step with actions drawn on the GPU (Philox4x32-10 keyed by seed, counter =
-        (global env index, step index)). The actions used land in self.a1_buf / a2_buf (always,
-        when they are views of self.flags)."""
+        """One step with actions drawn on the GPU (word step mod 4 of Philox4x32-10 keyed by seed,
+        counter = (global env index, step index div 4); mg_step_random). The actions used land in
+        self.a1_buf / a2_buf (always, when they are views of self.flags)."""
         k = self._step_idx if step_idx is None else int(step_idx)
         rc = self._nat.lib.mg_step_random(
             self._p_ref, self._s_ref, self._a1_ptr if record_actions else None,

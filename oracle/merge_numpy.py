@@ -100,14 +100,18 @@ def philox4x32_10(c0, c1, c2, c3, seed: int):
 
 
 def random_actions(gidx, seed: int, step: int, opponent_random: bool = True):
-    """a1 = floor(5 u0 / 2^32), a2 = floor(5 u1 / 2^32) or -1 (None), per global env index."""
+    """Word w = step mod 4 of Philox(counter (gi, step div 4)) per global env index; both random:
+    x = floor(25 w / 2^32), a1 = x // 5, a2 = x % 5; opponent None: a1 = floor(5 w / 2^32), a2 = -1
+    (the device stream, mg_step_random)."""
     g = gidx.astype(np.uint64)
     z = np.zeros_like(g)
-    u0, u1, _, _ = philox4x32_10(g & _MASK, g >> _S32, z + np.uint64(step & 0xFFFFFFFF),
-                                 z + np.uint64(step >> 32), seed)
-    a1 = ((u0 * np.uint64(5)) >> _S32).astype(np.int64)
-    a2 = ((u1 * np.uint64(5)) >> _S32).astype(np.int64) if opponent_random else np.full(len(g), -1)
-    return a1, a2
+    blk = step >> 2
+    u = philox4x32_10(g & _MASK, g >> _S32, z + np.uint64(blk & 0xFFFFFFFF), z + np.uint64(blk >> 32), seed)
+    w = u[step & 3]
+    if opponent_random:
+        x = ((w * np.uint64(25)) >> _S32).astype(np.int64)
+        return x // 5, x % 5
+    return ((w * np.uint64(5)) >> _S32).astype(np.int64), np.full(len(g), -1)
 
 
 class NumpyMergeBatch:

@@ -255,14 +255,25 @@ void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t
   out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
+/* The device's random-policy stream (include/merging_hip.h, mg_step_random): step k of env gi
+ * uses word k mod 4 of Philox4x32-10(counter (gi, k div 4)); both players random: the pair
+ * x = floor(25 w / 2^32), a1 = x / 5, a2 = x % 5; opponent None: a1 = floor(5 w / 2^32). */
 static void draw_actions(int64_t gi, uint64_t seed, uint64_t step, int opp_random, int* a1, int* a2) {
-  const uint32_t c[4] = {(uint32_t)gi, (uint32_t)((uint64_t)gi >> 32), (uint32_t)step,
-                         (uint32_t)(step >> 32)};
+  const uint64_t blk = step >> 2;
+  const uint32_t c[4] = {(uint32_t)gi, (uint32_t)((uint64_t)gi >> 32), (uint32_t)blk,
+                         (uint32_t)(blk >> 32)};
   const uint32_t k[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
   uint32_t u[4];
   oracle_philox4x32_10(c, k, u);
-  *a1 = (int)(((uint64_t)u[0] * 5u) >> 32);
-  *a2 = opp_random ? (int)(((uint64_t)u[1] * 5u) >> 32) : -1;
+  const uint64_t w = u[step & 3];
+  if (opp_random) {
+    const int x = (int)((w * 25u) >> 32);
+    *a1 = x / 5;
+    *a2 = x % 5;
+  } else {
+    *a1 = (int)((w * 5u) >> 32);
+    *a2 = -1;
+  }
 }
 
 void oracle_random_actions(int64_t n, int64_t env_offset, uint64_t seed, uint64_t step,

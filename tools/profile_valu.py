@@ -1,0 +1,49 @@
+"""Workload for rocprofv3 --pmc passes on the compute side of the kernels (tools/pmc_valu.sh):
+2^20 envs in steady state, then 8 launches each of mg_step_random, the fused random rollout
+(T = 16), the config-5 Q-net rollout (ego, T = 16) and the h-DQN rollout (T = 16).
+tools/valu_summary.py turns the counters into per-kernel VALU busy fractions and instruction
+mixes per env-step."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "merging-gym_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from merging_gym import MergeVecEnv  # noqa: E402
+from merging_gym.policy import QNet  # noqa: E402
+
+env = MergeVecEnv(1 << 20, device="cuda:0", final_observation=False)
+k = bench.burn_in(env, 1024, 7, 0)
+for j in range(8):
+    env.step_random(7, step_idx=k)
+    k += 1
+for j in range(8):
+    env.rollout_random(16, 7, first_step=k, final_observation=False, won_mask=False)
+    k += 16
+f = np.load(os.path.join(ROOT, "tests", "golden", "dqn_checkpoints.npz"))
+qnet = QNet.from_state_dict({kk.split("/", 1)[1]: f[kk] for kk in f.files if kk.startswith("l1/")}, device="cuda:0")
+for j in range(8):
+    env.rollout_qnet(16, qnet, 7, first_step=k, final_observation=False, won_mask=False)
+    k += 16
+rng = np.random.default_rng(0)
+
+
+def net(i, o):
+    sd = {}
+    for name, (a, b) in zip(("fc1", "fc2", "out"), [(200, i), (100, 200), (o, 100)]):
+        sd[f"{name}.weight"] = rng.uniform(0, 1, (a, b)).astype(np.float32)
+        sd[f"{name}.bias"] = rng.uniform(-b ** -0.5, b ** -0.5, a).astype(np.float32)
+    return QNet.from_state_dict(sd, device="cuda:0")
+
+
+meta, lower = net(10, 3), net(11, 5)
+for j in range(8):
+    env.rollout_hdqn(16, meta, lower, 7, first_step=k, final_observation=False)
+    k += 16
+torch.cuda.synchronize()
+print("ok")
