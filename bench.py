@@ -131,6 +131,26 @@ def load_pmc(envs: int):
         return None
 
 
+def load_valu():
+    """Per-kernel VALU-issue figures from the committed rocprofv3 summary (tools/pmc_valu.sh +
+    tools/valu_summary.py -> profiles/valu_busy.json): VALUBusy = VALU issue cycles of every SIMD
+    over the kernel's GPU time, the ceiling of a kernel whose arithmetic, not its bytes, sets
+    the pace."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "valu_busy.json")) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return {}
+    out = {}
+    for k, v in d.items():
+        ins = v.get("insts_per_64_env_steps", {})
+        out[k] = {"valu_busy_frac": v.get("VALUBusy", 0.0) / 100.0,
+                  "valu_insts_per_lane_step": ins.get("valu", 0.0),  # wave instructions per 64 env-steps
+                  "fp64_share_of_valu": v.get("fp64_share_of_valu"),
+                  "source": "profiles/valu_busy.json (rocprofv3 --pmc VALUBusy + SQ_INSTS_VALU*, 2^20 envs)"}
+    return out
+
+
 def burn_in(env, steps: int, seed: int, first_step: int) -> int:
     """Untimed fused rollouts until `steps` env-steps have passed; returns the next step index."""
     k = first_step
@@ -599,14 +619,21 @@ def main():
                          "traffic_rule": "2 x FETCH_SIZE + WRITE_SIZE per launch, profiles/pmc_traffic.json"},
             "episodes": episodes,
         }
+        valu = load_valu()
         if rollout is not None:
+            if "rollout_kernel" in valu:  # VALU-issue roofline of the rollout (VALU, not HBM, bound)
+                rollout["valu_roofline"] = valu["rollout_kernel"]
             line["rollout"] = rollout
         if replay is not None:
             line["replay"] = replay
         if qnet is not None:
             line["qnet_policy"] = qnet
         if hdqn is not None:
+            if "hdqn_rollout" in valu:
+                hdqn["valu"] = valu["hdqn_rollout"]
             line["hdqn_policy"] = hdqn
+        if qnet is not None and "qnet_rollout" in valu:
+            qnet[0]["valu"] = valu["qnet_rollout"]
         if size2 is not None:
             line["size_2p22"] = size2
         if world == 1 and not args.no_cpu_baseline:
