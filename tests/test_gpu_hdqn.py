@@ -223,3 +223,93 @@ def test_fused_hdqn_rollout(coracle, n):
                             reward=rows["r_int"][t][None])
     assert ring.memory_counter == c == 2 * n * T
     np.testing.assert_array_equal(ring.memory.cpu().numpy(), mem)
+
+
+def _philox_words(gidx, seed, step):
+    """[len(gidx), 4] uint32 Philox words for arbitrary global env indices (NumPy restatement)."""
+    import merge_numpy as mn
+
+    g = np.asarray(gidx, dtype=np.uint64)
+    z = np.zeros_like(g)
+    m = np.uint64(0xFFFFFFFF)
+    u = mn.philox4x32_10(g & m, g >> np.uint64(32), z + np.uint64(step & 0xFFFFFFFF), z + np.uint64(step >> 32), seed)
+    return np.stack([w.astype(np.uint32) for w in u], axis=1)
+
+
+def test_fused_hdqn_rollout_full_size(coracle):
+    """hdqn.py's acting loop at the BASELINE batch, 2^20 envs x 16 steps in one launch (the
+    kernel's 512-env blocks and the [T, N] goal outputs at full size). Whole batch: actions and
+    goals in range, intrinsic rewards 0/1, no NaN, the step bookkeeping. 2,048 sampled global env
+    indices: every action, next goal and fresh goal is its draws' epsilon-greedy choice (bf16
+    reference argmax, near-ties excused), every transition equals the C oracle's and the state
+    ends bit for bit equal. Reference: scripts/hdqn.py:280-323."""
+    import torch
+
+    from merging_gym import MergeVecEnv
+    from merging_gym.policy import NUM_GOALS, QNet, greedy_threshold
+
+    n, T, seed, k0, burn, dev = 1 << 20, 16, 17, 900, 240, "cuda:0"
+    rng = np.random.default_rng(5)
+    meta_sd, lower_sd = _net(rng, 10, NUM_GOALS), _net(rng, 11, 5)
+    meta, lower = QNet.from_state_dict(meta_sd, device=dev), QNet.from_state_dict(lower_sd, device=dev)
+    env = MergeVecEnv(n, device=dev)
+    for k in range(burn):
+        env.step_random(seed + 1, step_idx=k)
+    idx_np = np.sort(np.random.default_rng(3).choice(n, 2048, replace=False))
+    idx = torch.from_numpy(idx_np).to(dev)
+    envs = coracle.new_envs(len(idx_np))
+    for name, src in (("pos1", env.p1), ("vel1", env.v1), ("pos2", env.p2), ("vel2", env.v2),
+                      ("r1_acc", env.ret1), ("r2_acc", env.ret2)):
+        envs[name] = src[idx].cpu().numpy()
+    envs["steps"] = env.steps[idx].cpu().numpy()
+    envs["winner"] = env.winner[idx].cpu().numpy()
+    envs["time_stamp"] = np.cumsum(np.full(2700, 0.2))[np.maximum(envs["steps"] - 1, 0)] * (envs["steps"] > 0)
+    obs = env.observe()[idx].cpu().numpy().copy()
+    reset_goal = meta.reset_argmax()
+
+    tr = env.rollout_hdqn(T, meta, lower, seed, first_step=k0)
+    assert int(tr["a1"].min()) >= 0 and int(tr["a1"].max()) <= 4 and bool((tr["a2"] == -1).all())
+    for key in ("goal", "next_goal"):
+        assert float(tr[key].min()) >= 0 and float(tr[key].max()) <= NUM_GOALS - 1
+    assert set(torch.unique(tr["reward"]).tolist()) <= {0.0, 1.0}
+    assert not bool(torch.isnan(tr["obs"]).any()) and not bool(torch.isnan(tr["rew"]).any())
+    assert bool((env.counts[:, 3].to(torch.int64) + env.steps.to(torch.int64) == burn + T).all())
+    assert int(tr["done"].sum()) > 1000
+    sub = {k: tr[k][:, idx].cpu().numpy() for k in ("a1", "done", "obs", "rew", "final_observation", "goal",
+                                                       "next_goal", "reward")}
+    thr = greedy_threshold()
+    fresh = _philox_words(idx_np.astype(np.uint64) ^ np.uint64(1 << 63), seed, k0 - 1)
+    qm = mo.qnet_reference(meta_sd, obs, bf16=True)
+    exp0 = np.where(fresh[:, 0] < thr, qm.argmax(1), _pick(fresh[:, 1], NUM_GOALS))
+    assert ((sub["goal"][0] == exp0) | ((fresh[:, 0] < thr) & _near_tie(qm))).all()
+    for t in range(T):
+        ua = _philox_words(idx_np, seed, k0 + t)
+        ub = _philox_words(idx_np.astype(np.uint64) ^ np.uint64(1 << 63), seed, k0 + t)
+        goal_t = sub["goal"][t].astype(np.int64)
+        q1 = mo.qnet_reference(lower_sd, np.concatenate([goal_t[:, None].astype(np.float32), obs], axis=1), bf16=True)
+        greedy = ua[:, 0] < thr
+        exp_a = np.where(greedy, q1.argmax(1), _pick(ua[:, 1], 5))
+        assert ((sub["a1"][t] == exp_a) | (greedy & _near_tie(q1))).all(), t
+        o_obs, o_rew, o_done, o_coll, _, o_fobs, err = coracle.step(envs, sub["a1"][t].astype(np.int8), None,
+                                                                    autoreset=True, final_obs=True)
+        assert err == 0
+        d = o_done.astype(bool)
+        np.testing.assert_array_equal(sub["done"][t], d, err_msg=str(t))
+        np.testing.assert_allclose(sub["obs"][t], o_obs.astype(np.float32), **OBS_TOL)
+        np.testing.assert_allclose(sub["rew"][t], o_rew.astype(np.float32), **OBS_TOL)
+        np.testing.assert_allclose(sub["final_observation"][t][d], o_fobs[d].astype(np.float32), **OBS_TOL)
+        s2 = np.where(d[:, None], sub["final_observation"][t], sub["obs"][t])
+        q2 = mo.qnet_reference(meta_sd, s2, bf16=True)
+        gg = ua[:, 2] < thr
+        g2 = sub["next_goal"][t].astype(np.int64)
+        assert ((g2 == np.where(gg, q2.argmax(1), _pick(ua[:, 3], NUM_GOALS))) | (gg & _near_tie(q2))).all(), t
+        np.testing.assert_array_equal(sub["reward"][t], (g2 == _status(obs)).astype(np.float32))
+        brk = d | (g2 == _status(s2))
+        gf = ub[:, 0] < thr
+        exp_next = np.where(brk, np.where(gf, np.where(d, reset_goal, q2.argmax(1)), _pick(ub[:, 1], NUM_GOALS)), g2)
+        nxt = sub["goal"][t + 1] if t + 1 < T else env.hdqn_goal[idx].cpu().numpy()
+        assert ((nxt == exp_next) | (brk & gf & ~d & _near_tie(q2))).all(), t
+        obs = sub["obs"][t]
+    for name, src in (("pos1", env.p1), ("vel1", env.v1), ("pos2", env.p2), ("vel2", env.v2),
+                      ("r1_acc", env.ret1), ("r2_acc", env.ret2)):
+        np.testing.assert_array_equal(src[idx].cpu().numpy(), envs[name], err_msg=name)
