@@ -345,7 +345,43 @@ def hdqn_leg(env, args, world, dist, torch):
     elapsed = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / L
     per_s = E * T / (kernel_ms * 1e-3)
+
+    # with hdqn.py's lower-level memory (HDQN.store_transition, :316, every transition): the
+    # store fused into the launch vs the rollout followed by mg_replay_store from its outputs
+    from merging_gym import ReplayRing
+
+    ring = ReplayRing(1 << 24, device=env.device, goal=True)
+    Lr = max(1, L // 2)
+
+    def timed(fn):
+        nonlocal k
+        fn()
+        k += T
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(Lr):
+            fn()
+            k += T
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / Lr
+
+    obs0 = env.observe().clone()
+    fused_ms = timed(lambda: env.rollout_hdqn(T, meta, lower, args.seed, first_step=k, ring=ring))
+
+    def separate():
+        tr = env.rollout_hdqn(T, meta, lower, args.seed, first_step=k)
+        ring.store_rollout(obs0, tr, skip_ego_won=False, goal=tr["goal"], next_goal=tr["next_goal"],
+                           reward=tr["reward"])
+    separate_ms = timed(separate)
+    del ring
+    torch.cuda.empty_cache()
     return {"kernel": "hdqn_rollout_kernel<0>", "opponent": "none", "steps_per_launch": T, "launches": L,
+            "with_goal_ring": {"fused_store_ms_per_launch": fused_ms, "rollout_then_replay_store_ms": separate_ms,
+                               "fused_env_steps_per_s": E * T / (fused_ms * 1e-3),
+                               "separate_env_steps_per_s": E * T / (separate_ms * 1e-3),
+                               "ring_capacity": 1 << 24},
             "dtype": "bf16 (fp32 accumulate)", "value": world * E * T * L / elapsed, "unit": "env-steps/s",
             "ms_per_step": elapsed / (L * T) * 1e3, "kernel_ms_mean": kernel_ms,
             "useful_tflops": HDQN_USEFUL_FLOP * per_s / 1e12, "peak_tflops": MFMA_BF16_PEAK_TFLOPS,

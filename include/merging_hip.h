@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 10
+#define MG_ABI_VERSION 11
 #define MG_OBS_DIM 10   /* merging_env.py:75 observation_shape = (10) */
 #define MG_NUM_ACTIONS 5 /* merging_env.py:101-102 action_dict / Discrete(5) */
 #define MG_ACTION_NONE (-1) /* action2=None: the constant-speed "L0" opponent, merging_env.py:152 */
@@ -307,12 +307,19 @@ typedef struct mg_hdqn_traj {
  * action, explore, goal) and counter ((env_offset + i) ^ 2^63, first_step + t) for a fresh goal
  * (x, y) and the uniform opponent (z); a launch's first fresh goals use step first_step - 1.
  * Greedy when the explore draw < greedy_threshold (np.random.randn() <= EPISILO, :84, :168).
- * traj as mg_rollout_qnet; opponent_mode 0 (None) or 1 (uniform). */
+ * traj as mg_rollout_qnet; opponent_mode 0 (None) or 1 (uniform).
+ * ring_rows (optional, 16-byte aligned [ring_capacity, 24] fp32, with ring_counter: one device
+ * uint64): the launch also appends every transition to hdqn.py's lower-level memory
+ * (HDQN.store_transition, :316, which stores them all) -- row [goal, s, a, r, next_goal, s'] of
+ * (t, i) at slot (counter + t n + i) % ring_capacity, exactly what mg_replay_store with
+ * skip_ego_won = 0 writes from this launch's outputs (only the newest ring_capacity rows when
+ * more are appended), then counter += T n. No scan is needed since every row is kept. */
 int mg_rollout_hdqn(const mg_params* params, const mg_state* state, const mg_traj* traj,
                     const mg_hdqn_traj* htraj, const mg_stats* stats, int8_t* goal, int64_t n,
                     int64_t env_offset, uint64_t seed, uint64_t first_step, int32_t num_steps,
                     const void* meta_net, int32_t num_goals, const void* lower_net, int32_t reset_goal,
-                    uint64_t greedy_threshold, int32_t opponent_mode, uint32_t flags, void* stream);
+                    uint64_t greedy_threshold, int32_t opponent_mode, float* ring_rows,
+                    uint64_t* ring_counter, int64_t ring_capacity, uint32_t flags, void* stream);
 
 /* ---- replay memory (scripts/main.py:91-92, :115-119, :130-135) --------------------------------
  * rows: [capacity, row_floats] fp32 device buffer, row = [s(10), a, r, s'(10)] like

@@ -1647,6 +1647,9 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
   }
 }
 
+// memory_counter += k (the fused goal ring's stores are all kept: no scan)
+__global__ void counter_add_kernel(uint64_t* counter, uint64_t k) { *counter += k; }
+
 // ============================================================================ h-DQN acting loop
 // hdqn.py's inner loop (scripts/hdqn.py:280-323) in one launch: Goal_DQN's meta-net picks the
 // sub-goal on every next state (:303), the lower-level Net acts on the goal state
@@ -1685,9 +1688,15 @@ struct HRollout {
   int32_t num_goals;
   int32_t reset_goal;
   uint32_t flags;
+  // fused goal ring (hdqn.py:316 stores every transition, so slots need no scan): rows
+  // [goal, s, a, r, next_goal, s'] of transition (t, i) at (counter0 + t n + i) % capacity
+  float* ring;  // [capacity, 24] or NULL
+  const uint64_t* ring_counter;
+  int64_t ring_capacity;
 };
 
 constexpr int kHEnvs = 512;              // envs per block: two groups of 256
+constexpr int kRowGoalF = 2 * kObs + 4;  // goal ring row floats (hdqn.py:158)
 constexpr int kHHalf = kHEnvs / 2;
 constexpr uint8_t kHGreedy = 0xFF;       // draw byte: take the greedy choice
 
@@ -1738,7 +1747,7 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
   __shared__ __attribute__((aligned(16))) float tile[kHEnvs * kObs];    // s' (reset obs where done)
   __shared__ __attribute__((aligned(16))) uint32_t side[kHEnvs * 5];    // terminal obs, bf16 pairs
   __shared__ uint8_t b_act[kHEnvs], b_goal[kHEnvs], b_done[kHEnvs], b_st_old[kHEnvs],
-      b_st_new[kHEnvs], b_dg[kHEnvs], b_df[kHEnvs];
+      b_st_new[kHEnvs], b_dg[kHEnvs], b_df[kHEnvs], b_g2[kHEnvs];
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int64_t base = static_cast<int64_t>(blockIdx.x) * kHEnvs;
@@ -1790,6 +1799,7 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
           if (R.H.next_goal) st_out(R.H.next_goal + row, static_cast<float>(goal2));
           if (R.H.reward) st_out(R.H.reward + row, goal2 == b_st_old[j] ? 1.0f : 0.0f);
         }
+        b_g2[j] = static_cast<uint8_t>(goal2);  // for the fused ring row of step t - 1
       } else {
         goal_t = goal_prev >= 0 ? goal_prev : (df == kHGreedy ? gstar : df);
       }
@@ -1813,6 +1823,38 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
   Env e[2];
   StepOut r[2];
   bool live[2];
+  // the fused ring row of each group's last step, completed once the Q-net waves have chosen
+  // its next goal: s, s' (terminal where done), goal, action
+  float ps[2][kObs], ps2[2][kObs];
+  int pgoal[2], pact[2];
+  const bool ring = R.ring != nullptr;
+  const uint64_t c0 = ring ? *R.ring_counter : 0;
+  const int64_t total = static_cast<int64_t>(T) * R.n;
+  auto write_row = [&](int g, int t, const float (&s0)[kObs], const float (&s1)[kObs], int pg,
+                       int pa) __attribute__((always_inline)) {
+    const int j = g * kHHalf + 64 * ew + lane;
+    const int64_t i = base + j;
+    const int64_t k = static_cast<int64_t>(t) * R.n + i;  // transition index within the launch
+    if (!ring || i >= R.n || k < total - R.ring_capacity) return;  // the newest capacity rows only
+    const int goal2 = b_g2[j];
+    const int st_old = b_st_old[j];
+    float* row = R.ring + static_cast<int64_t>((c0 + static_cast<uint64_t>(k)) %
+                                               static_cast<uint64_t>(R.ring_capacity)) * kRowGoalF;
+    f32x4 v[6];
+    float f[kRowGoalF];
+    f[0] = static_cast<float>(pg);
+#pragma unroll
+    for (int q = 0; q < kObs; ++q) f[1 + q] = s0[q];
+    f[11] = static_cast<float>(pa);
+    f[12] = goal2 == st_old ? 1.0f : 0.0f;
+    f[13] = static_cast<float>(goal2);
+#pragma unroll
+    for (int q = 0; q < kObs; ++q) f[14 + q] = s1[q];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) v[q] = f32x4{f[4 * q], f[4 * q + 1], f[4 * q + 2], f[4 * q + 3]};
+#pragma unroll
+    for (int q = 0; q < 6; ++q) st_out(reinterpret_cast<f32x4*>(row) + q, v[q]);
+  };
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
     const int j = g * kHHalf + 64 * ew + lane;
@@ -1858,9 +1900,26 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
       const uint4 ub = philox_env_step(gi ^ (uint64_t{1} << 63), k, R.seed);
       const int a1 = static_cast<uint64_t>(ua.x) < R.greedy_thr ? static_cast<int>(b_act[j]) : action_from_u32(ua.y);
       const int a2 = OPP == 1 ? action_from_u32(ub.z) : MG_ACTION_NONE;
-      auto step = [&](Env& ev, StepOut& rv, bool lv) __attribute__((always_inline)) {
+      if (t > 0) {  // step t - 1's next goal is in LDS now (Q(X, t)); wave-uniform branch per group
+        if (g == 0)
+          write_row(0, t - 1, ps[0], ps2[0], pgoal[0], pact[0]);
+        else
+          write_row(1, t - 1, ps[1], ps2[1], pgoal[1], pact[1]);
+      }
+      auto step = [&](Env& ev, StepOut& rv, bool lv, float (&s0)[kObs], float (&s1)[kObs], int& pg,
+                      int& pa) __attribute__((always_inline)) {
         b_st_old[j] = static_cast<uint8_t>(goal_status(rv.o));  // status of the state acted on
+        if (ring) {
+#pragma unroll
+          for (int q = 0; q < kObs; ++q) s0[q] = static_cast<float>(rv.o[q]);
+          pg = b_goal[j];
+          pa = a1;
+        }
         env_step(R.P, ev, a1, a2, rv);
+        if (ring) {
+#pragma unroll
+          for (int q = 0; q < kObs; ++q) s1[q] = static_cast<float>(rv.o[q]);  // terminal where done
+        }
         const int64_t row = static_cast<int64_t>(t) * R.n + i;
         if (lv) {
           if (R.T.rew) st_out(reinterpret_cast<f32x2*>(R.T.rew) + row, f32x2{static_cast<float>(rv.r1), static_cast<float>(rv.r2)});
@@ -1887,12 +1946,15 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
                        wrem <= 0 ? 0 : (wrem < 64 ? static_cast<int>(wrem) : 64));
       };
       if (g == 0)
-        step(e[0], r[0], live[0]);
+        step(e[0], r[0], live[0], ps[0], ps2[0], pgoal[0], pact[0]);
       else
-        step(e[1], r[1], live[1]);
+        step(e[1], r[1], live[1], ps[1], ps2[1], pgoal[1], pact[1]);
     }
     __syncthreads();
   }
+  // both groups' last rows: Q(A,T) and Q(B,T) chose their next goals in the last two phases
+  write_row(0, T - 1, ps[0], ps2[0], pgoal[0], pact[0]);
+  write_row(1, T - 1, ps[1], ps2[1], pgoal[1], pact[1]);
 #pragma unroll
   for (int g = 0; g < 2; ++g)
     if (live[g]) store_env(R.S, base + g * kHHalf + 64 * ew + lane, e[g]);
@@ -2594,7 +2656,10 @@ int mg_rollout_hdqn(const mg_params* params, const mg_state* state, const mg_tra
                     const mg_hdqn_traj* htraj, const mg_stats* stats, int8_t* goal, int64_t n,
                     int64_t env_offset, uint64_t seed, uint64_t first_step, int32_t num_steps,
                     const void* meta_net, int32_t num_goals, const void* lower_net, int32_t reset_goal,
-                    uint64_t greedy_threshold, int32_t opponent_mode, uint32_t flags, void* stream) {
+                    uint64_t greedy_threshold, int32_t opponent_mode, float* ring_rows,
+                    uint64_t* ring_counter, int64_t ring_capacity, uint32_t flags, void* stream) {
+  if (ring_rows && (!ring_counter || ring_capacity < 1 || (reinterpret_cast<uintptr_t>(ring_rows) & 15)))
+    return fail(hipErrorInvalidValue, "%s", "ring_rows needs ring_counter, capacity >= 1 and 16-byte alignment");
   mg_outputs none{};
   if (int e = check_common(params, state, &none, n)) return e;
   if (!traj) return fail(hipErrorInvalidValue, "%s", "traj is NULL (pass a zeroed mg_traj)");
@@ -2629,12 +2694,18 @@ int mg_rollout_hdqn(const mg_params* params, const mg_state* state, const mg_tra
   R.num_goals = num_goals;
   R.reset_goal = reset_goal;
   R.flags = flags;
+  R.ring = ring_rows;
+  R.ring_counter = ring_counter;
+  R.ring_capacity = ring_capacity;
   const unsigned blocks = static_cast<unsigned>((n + kHEnvs - 1) / kHEnvs);
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (opponent_mode == 0)
     hipLaunchKernelGGL(hdqn_rollout_kernel<0>, dim3(blocks), dim3(512), 0, st, R);
   else
     hipLaunchKernelGGL(hdqn_rollout_kernel<1>, dim3(blocks), dim3(512), 0, st, R);
+  if (ring_rows)  // after every block has read the old counter: the same stream orders it
+    hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(1), 0, st, ring_counter,
+                       static_cast<uint64_t>(num_steps) * static_cast<uint64_t>(n));
   return finish_launch("mg_rollout_hdqn");
 }
 

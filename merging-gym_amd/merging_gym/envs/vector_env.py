@@ -309,7 +309,7 @@ class MergeVecEnv:
 
     def rollout_hdqn(self, num_steps: int, meta, lower, seed: int, opponent: str = "none",
                      episilo: float = 0.7, first_step=None, final_observation: bool = True,
-                     won_mask: bool = False):
+                     won_mask: bool = False, ring=None):
         """`num_steps` steps of hdqn.py's inner loop (scripts/hdqn.py:280-323) in one launch:
         Goal_DQN's meta-net (`meta`, a QNet 10 -> num_goals) picks each env's sub-goal on every
         next state, the lower-level Net (`lower`, a QNet 11 -> 5) acts epsilon-greedily on the
@@ -319,12 +319,17 @@ class MergeVecEnv:
         `self.hdqn_goal` ([N] int8, -1 = none yet). Returns rollout_random's [T, N, ...] dict
         plus "goal", "next_goal" and "reward" ([T, N] fp32: the goal columns and the intrinsic
         reward of HDQN.store_transition's rows, :316 -- ReplayRing(goal=True).store_rollout takes
-        them as they are)."""
+        them as they are). ring: a ReplayRing(goal=True) the same launch appends every
+        transition to (hdqn.py:316 stores them all, so the kernel needs no scan): the rows
+        store_rollout(obs0, traj, skip_ego_won=False, goal=..., next_goal=..., reward=...) would
+        write, without re-reading the trajectory."""
         from ..policy import greedy_threshold
 
         torch, nat = self._torch, self._nat
         T, n = int(num_steps), self.num_envs
         mode = {"none": 0, "uniform": 1}[opponent]
+        if ring is not None and (not ring.goal or ring.device != self.device):
+            raise ValueError("the fused store needs a goal ring (ReplayRing(goal=True)) on this env's device")
         if meta.in_dim != _OBS_DIM or lower.in_dim != _OBS_DIM + 1 or lower.out_dim != nat.NUM_ACTIONS:
             raise ValueError("need hdqn.py's nets: meta-net in_dim 10, lower-level Net in_dim 11 -> 5")
         k0 = self._step_idx if first_step is None else int(first_step)
@@ -341,7 +346,9 @@ class MergeVecEnv:
             self._p_ref, self._s_ref, ctypes.byref(buf["_traj"]), ctypes.byref(hb["_h"]), self._st_ref,
             self.hdqn_goal.data_ptr(), n, self.env_offset, seed & 0xFFFFFFFFFFFFFFFF, k0 & 0xFFFFFFFFFFFFFFFF,
             T, meta.packed.data_ptr(), meta.out_dim, lower.packed.data_ptr(), meta.reset_argmax(),
-            greedy_threshold(episilo), mode, self._flags, self._stream())
+            greedy_threshold(episilo), mode, None if ring is None else ring.memory.data_ptr(),
+            None if ring is None else ring._counter.data_ptr(), 0 if ring is None else ring.capacity,
+            self._flags, self._stream())
         nat.check(rc, "mg_rollout_hdqn")
         self._step_idx = k0 + T
         out = dict(buf["_result"])

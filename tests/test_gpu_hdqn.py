@@ -156,9 +156,13 @@ def test_fused_hdqn_rollout(coracle, n):
     goal_prev = None
     rows = {k: [] for k in ("obs0", "obs", "fobs", "a1", "rew", "done", "goal", "goal2", "r_int")}
     ring = ReplayRing(4 * n * T, device=dev, goal=True)
+    # the same rows appended by the launch itself (fused store); a capacity below one launch's
+    # n T transitions so the ring wraps inside a launch (only the newest capacity rows land)
+    cap_f = n * T // 3 + 7
+    ring_f = ReplayRing(cap_f, device=dev, goal=True)
     for launch in range(2):
         obs_first = obs.copy()
-        tr = env.rollout_hdqn(T, meta, lower, seed, first_step=k0)
+        tr = env.rollout_hdqn(T, meta, lower, seed, first_step=k0, ring=ring_f)
         g = {k: tr[k].cpu().numpy().copy() for k in ("goal", "next_goal", "reward")}
         a1_all, done_all = tr["a1"].cpu().numpy().copy(), tr["done"].cpu().numpy().copy()
         o_all, fo_all, rew_all = (tr[k].cpu().numpy().copy() for k in ("obs", "final_observation", "rew"))
@@ -223,6 +227,15 @@ def test_fused_hdqn_rollout(coracle, n):
                             reward=rows["r_int"][t][None])
     assert ring.memory_counter == c == 2 * n * T
     np.testing.assert_array_equal(ring.memory.cpu().numpy(), mem)
+    mem_f = np.zeros((cap_f, 24), np.float32)
+    c = 0
+    for t in range(len(rows["obs"])):
+        c = mo.replay_store(mem_f, c, rows["obs0"][t], rows["obs"][t][None], rows["a1"][t][None].astype(np.int8),
+                            rows["rew"][t][None], rows["done"][t][None], rows["fobs"][t][None], None,
+                            skip_ego_won=False, goal=rows["goal"][t][None], next_goal=rows["goal2"][t][None],
+                            reward=rows["r_int"][t][None])
+    assert ring_f.memory_counter == c
+    np.testing.assert_array_equal(ring_f.memory.cpu().numpy(), mem_f)
 
 
 def _philox_words(gidx, seed, step):
