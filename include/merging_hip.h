@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 11
+#define MG_ABI_VERSION 12
 #define MG_OBS_DIM 10   /* merging_env.py:75 observation_shape = (10) */
 #define MG_NUM_ACTIONS 5 /* merging_env.py:101-102 action_dict / Discrete(5) */
 #define MG_ACTION_NONE (-1) /* action2=None: the constant-speed "L0" opponent, merging_env.py:152 */
@@ -229,11 +229,13 @@ void mg_params_default(mg_params* p);
 int mg_step(const mg_params* params, const mg_state* state, const int8_t* a1, const int8_t* a2,
             const mg_outputs* out, const mg_stats* stats, int64_t n, uint32_t flags, void* stream);
 
-/* As mg_step, with actions drawn on the device: w = word (step_idx mod 4) of Philox4x32-10
- * (key = seed, counter = (env_offset + env index, step_idx div 4)) -- one call covers four
- * steps of a rollout; a shard of a larger batch passes its first global env index as
- * env_offset and draws the same actions it would draw unsharded. opponent_random != 0: the
- * pair x = floor(25 w / 2^32), a1 = x / 5, a2 = x % 5; else a1 = floor(5 w / 2^32), a2 None.
+/* As mg_step, with actions drawn on the device (ABI 12): w = word ((step_idx div 2) mod 4) of
+ * Philox4x32-10 (key = seed, counter = (env_offset + env index, step_idx div 8)) -- one call
+ * covers eight steps of a rollout, two draws per word; a shard of a larger batch passes its first
+ * global env index as env_offset and draws the same actions it would draw unsharded. A draw of
+ * m outcomes is floor(m w / 2^32); an odd step_idx draws from m w mod 2^32 instead (the first
+ * draw's remainder). opponent_random != 0: m = 25, the pair x = draw, a1 = x / 5, a2 = x % 5;
+ * else m = 5, a1 = draw, a2 None.
  * If a1_out / a2_out are non-NULL the actions used are written there (-1 for None). */
 int mg_step_random(const mg_params* params, const mg_state* state, int8_t* a1_out,
                    int8_t* a2_out, const mg_outputs* out, const mg_stats* stats, int64_t n,

@@ -51,6 +51,9 @@ namespace {
 #ifndef MG_REPLAY_PREFETCH
 #define MG_REPLAY_PREFETCH 1  // replay store: next step's obs row loaded before this step's work
 #endif
+#ifndef MG_COPY_FULL_WAVE
+#define MG_COPY_FULL_WAVE 1  // wave_copy_rows: unrolled path for a full 64-row wave
+#endif
 #ifndef MG_SINCOS_COLD
 #define MG_SINCOS_COLD 1  // the |t| >= 1/16 sincos fallback as an out-of-line call
 #endif
@@ -332,12 +335,14 @@ struct StepOut {
   int bad;  // 1: action1 invalid, 2: action2 invalid (the reference's KeyError)
 };
 
-// The random-policy action stream: step k of global env gi uses word (k mod 4) of
-// u = Philox4x32-10(counter (gi, k div 4), key seed) -- one call covers four steps, so a T-step
-// rollout pays a quarter of the 40 quarter-rate 32-bit multiplies per env-step that one call
-// per step cost (Philox was a third of the rollout kernel's VALU time). With both players
-// random, x = floor(25 w / 2^32) is the action pair, a1 = x div 5, a2 = x mod 5 (25 equally
-// likely pairs up to a 25 / 2^32 bias); with the None opponent a1 = floor(5 w / 2^32).
+// The random-policy action stream: step k of global env gi takes word (k div 2) mod 4 of
+// u = Philox4x32-10(counter (gi, k div 8), key seed) -- one call covers eight steps, two draws per
+// 32-bit word, so a T-step rollout pays an eighth of a call's 40 multiplies per env-step (one call
+// per step had been a third of the rollout kernel's VALU). A draw of m outcomes from word w is
+// floor(m w / 2^32); an odd step draws from w' = m w mod 2^32 instead, the remainder of the first
+// draw (m is odd, so w -> w' is a bijection of the 32-bit words and w' is again uniform; the two
+// draws of one word are independent up to an m^2 / 2^32 bias). With both players random m = 25 and
+// x = draw is the action pair, a1 = x div 5, a2 = x mod 5; with the None opponent m = 5, a1 = draw.
 __device__ __forceinline__ uint4 philox_block(uint64_t gi, uint64_t block, uint64_t seed,
                                               bool opaque_key = false) {
   uint32_t k0 = static_cast<uint32_t>(seed), k1 = static_cast<uint32_t>(seed >> 32);
@@ -350,22 +355,31 @@ __device__ __forceinline__ uint4 philox_block(uint64_t gi, uint64_t block, uint6
                        k0, k1);
 }
 
-__device__ __forceinline__ uint32_t philox_word(const uint4& u, uint64_t step) {
-  // word step & 3 by a 64-bit select and shift on values: no indexed private array, no branch
-  const uint64_t lo = (static_cast<uint64_t>(u.y) << 32) | u.x, hi = (static_cast<uint64_t>(u.w) << 32) | u.z;
-  return static_cast<uint32_t>(((step & 2) ? hi : lo) >> (32 * (step & 1)));
-}
+#ifndef MG_PHILOX_STEPS
+#define MG_PHILOX_STEPS 8  // steps one Philox4x32-10 call feeds; 4 = the ABI-10..11 stream (timing A/B only)
+#endif
+constexpr int kStepsPerPhilox = MG_PHILOX_STEPS;  // 4 words x 2 draws
 
-__device__ __forceinline__ void actions_from_word(uint32_t w, int opp_random, int& a1, int& a2) {
-  const uint32_t x = static_cast<uint32_t>((static_cast<uint64_t>(w) * 25u) >> 32);  // 0..24
-  const int b1 = static_cast<int>((x * 13u) >> 6);                                     // x div 5
-  a1 = opp_random ? b1 : action_from_u32(w);
+__device__ __forceinline__ void actions_from_block(const uint4& u, uint64_t step, int opp_random, int& a1,
+                                                   int& a2) {
+  // word (step div 2) & 3 by a 64-bit select and shift on values: no indexed private array, no branch
+  const uint64_t lo = (static_cast<uint64_t>(u.y) << 32) | u.x, hi = (static_cast<uint64_t>(u.w) << 32) | u.z;
+  const uint32_t m = opp_random ? 25u : static_cast<uint32_t>(MG_NUM_ACTIONS);
+#if MG_PHILOX_STEPS == 4
+  const uint32_t w = static_cast<uint32_t>(((step & 2) ? hi : lo) >> (32 * (step & 1)));
+#else
+  uint32_t w = static_cast<uint32_t>(((step & 4) ? hi : lo) >> (32 * ((step >> 1) & 1)));
+  if (step & 1) w *= m;  // the second draw of the word
+#endif
+  const uint32_t x = static_cast<uint32_t>((static_cast<uint64_t>(w) * m) >> 32);
+  const int b1 = static_cast<int>((x * 13u) >> 6);  // x div 5 for x < 25
+  a1 = opp_random ? b1 : static_cast<int>(x);
   a2 = opp_random ? static_cast<int>(x) - 5 * b1 : MG_ACTION_NONE;
 }
 
 __device__ __forceinline__ void draw_actions(uint64_t gi, uint64_t step, uint64_t seed, int opp_random,
                                              int& a1, int& a2) {
-  actions_from_word(philox_word(philox_block(gi, step >> 2, seed), step), opp_random, a1, a2);
+  actions_from_block(philox_block(gi, step / kStepsPerPhilox, seed), step, opp_random, a1, a2);
 }
 
 // time_stamp += dT; done if time_stamp > 500 (:141-143). The fp64 clock first exceeds 500
@@ -398,11 +412,14 @@ __device__ __forceinline__ void move_car(const mg_params& P, double acc, double&
 __device__ __forceinline__ void score_step(const mg_params& P, Env& e, double x1, double y1,
                                            double x2, double y2, StepOut& r, bool frozen = false);
 
-// MergeEnv.step (merging_env.py:138-195) for one env held in registers.
+// MergeEnv.step (merging_env.py:138-195) for one env held in registers. CHECKED = false: the
+// caller guarantees a1 in 0..4 and a2 in -1..4 (device-drawn actions), so the KeyError path and
+// its zeroed outputs are not compiled in.
+template <bool CHECKED = true>
 __device__ __forceinline__ void env_step(const mg_params& P, Env& e, int a1, int a2, StepOut& r) {
   env_clock(P, e);
-  const bool bad1 = !valid_action(a1);
-  const bool bad2 = !(a2 == MG_ACTION_NONE || valid_action(a2));
+  const bool bad1 = CHECKED && !valid_action(a1);
+  const bool bad2 = CHECKED && !(a2 == MG_ACTION_NONE || valid_action(a2));
   r.bad = (bad1 ? 1 : 0) | (bad2 ? 2 : 0);
   r.acc1 = r.acc2 = 0.0;
   r.v1_int = r.v2_int = false;
@@ -680,6 +697,20 @@ __device__ __forceinline__ void wave_store_obs_n(float* wtile, const StepOut (&r
 // A wave's nrows x 10 fp32 LDS slice to dst: 16-byte stores when dst allows, else 8-byte.
 __device__ __forceinline__ void wave_copy_rows(const float* wtile, float* dst, int nrows) {
   const int lane = threadIdx.x & 63;
+#if MG_COPY_FULL_WAVE
+  // a full wave (64 rows = 160 16-byte pieces) into a 16-byte aligned destination: three fixed
+  // lane passes instead of the strided loop (wave-uniform test)
+  if (dst != nullptr && nrows == 64 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+    f32x4* d4 = reinterpret_cast<f32x4*>(dst);
+    const f32x4* s4 = reinterpret_cast<const f32x4*>(wtile);
+    const f32x4 v0 = s4[lane], v1 = s4[64 + lane];
+    const f32x4 v2 = s4[128 + (lane & 31)];
+    st_out(d4 + lane, v0);
+    st_out(d4 + 64 + lane, v1);
+    if (lane < 32) st_out(d4 + 128 + lane, v2);
+    return;
+  }
+#endif
   if (dst != nullptr && nrows > 0) {
     const int nfl = nrows * kObs;
     if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
@@ -869,6 +900,9 @@ struct Rollout {
 
 // num_steps consecutive mg_step_random steps with the env kept in registers: the state is
 // read once and written once per launch; step t's outputs go to slice t of the trajectory.
+#ifndef MG_ROLLOUT_LEAN
+#define MG_ROLLOUT_LEAN 1  // rollout: unchecked step for device-drawn actions, per-step StepOut
+#endif
 #ifndef MG_ROLLOUT_WAVES_PER_EU
 #define MG_ROLLOUT_WAVES_PER_EU 1  // rollout kernel: minimum waves per SIMD the register budget must allow
 #endif
@@ -903,18 +937,23 @@ __global__ __launch_bounds__(kBlock, MG_ROLLOUT_WAVES_PER_EU) void rollout_kerne
     e = load_env(R.S, i);
     stats_load(R.St, i, sreg);
   }
+#if !MG_ROLLOUT_LEAN
   StepOut r;
+#endif
   bool won = false;
-  uint4 u = make_uint4(0u, 0u, 0u, 0u);  // the Philox block of the current four steps
+  uint4 u = make_uint4(0u, 0u, 0u, 0u);  // the Philox block of the current eight steps
   for (int t = 0; t < R.num_steps; ++t) {
+#if MG_ROLLOUT_LEAN
+    StepOut r;  // per step: no loop-carried copy of the observation (dead lanes store nothing)
+#endif
     const int64_t row = static_cast<int64_t>(t) * R.n + i;
     const uint64_t k = R.first_step + t;
-    if (t == 0 || (k & 3) == 0)  // wave-uniform
-      u = philox_block(static_cast<uint64_t>(R.env_offset + i), k >> 2, R.seed, /*opaque_key=*/true);
+    if (t == 0 || k % kStepsPerPhilox == 0)  // wave-uniform
+      u = philox_block(static_cast<uint64_t>(R.env_offset + i), k / kStepsPerPhilox, R.seed, /*opaque_key=*/true);
     if (live) {
       int a1, a2;
-      actions_from_word(philox_word(u, k), R.opp_random, a1, a2);
-      env_step(P, e, a1, a2, r);  // Philox actions are always valid
+      actions_from_block(u, k, R.opp_random, a1, a2);
+      env_step<!MG_ROLLOUT_LEAN>(P, e, a1, a2, r);  // Philox actions are always valid
       if (R.T.rew)
         st_out(reinterpret_cast<f32x2*>(R.T.rew) + row,
                f32x2{static_cast<float>(r.r1), static_cast<float>(r.r2)});

@@ -219,8 +219,9 @@ class MergeVecEnv:
 
     def step_random(self, seed: int, opponent_random: bool = True, step_idx=None,
                     record_actions: bool = True):
-        """One step with actions drawn on the GPU (word step mod 4 of Philox4x32-10 keyed by seed,
-        counter = (global env index, step index div 4); mg_step_random). The actions used land in
+        """One step with actions drawn on the GPU (word (step div 2) mod 4 of Philox4x32-10 keyed by
+        seed, counter = (global env index, step index div 8), two draws per word; mg_step_random,
+        include/merging_hip.h). The actions used land in
         self.a1_buf / a2_buf (always, when they are views of self.flags)."""
         k = self._step_idx if step_idx is None else int(step_idx)
         rc = self._nat.lib.mg_step_random(

@@ -100,18 +100,22 @@ def philox4x32_10(c0, c1, c2, c3, seed: int):
 
 
 def random_actions(gidx, seed: int, step: int, opponent_random: bool = True):
-    """Word w = step mod 4 of Philox(counter (gi, step div 4)) per global env index; both random:
-    x = floor(25 w / 2^32), a1 = x // 5, a2 = x % 5; opponent None: a1 = floor(5 w / 2^32), a2 = -1
-    (the device stream, mg_step_random)."""
+    """Word w = (step div 2) mod 4 of Philox(counter (gi, step div 8)) per global env index; a draw
+    of m outcomes is floor(m w / 2^32), an odd step drawing from m w mod 2^32 instead. Both random:
+    m = 25, x = draw, a1 = x // 5, a2 = x % 5; opponent None: m = 5, a1 = draw, a2 = -1 (the device
+    stream, mg_step_random)."""
     g = gidx.astype(np.uint64)
     z = np.zeros_like(g)
-    blk = step >> 2
+    blk = step >> 3
     u = philox4x32_10(g & _MASK, g >> _S32, z + np.uint64(blk & 0xFFFFFFFF), z + np.uint64(blk >> 32), seed)
-    w = u[step & 3]
+    m = np.uint64(25 if opponent_random else 5)
+    w = u[(step >> 1) & 3]
+    if step & 1:
+        w = (w * m) & _MASK
+    x = ((w * m) >> _S32).astype(np.int64)
     if opponent_random:
-        x = ((w * np.uint64(25)) >> _S32).astype(np.int64)
         return x // 5, x % 5
-    return ((w * np.uint64(5)) >> _S32).astype(np.int64), np.full(len(g), -1)
+    return x, np.full(len(g), -1)
 
 
 class NumpyMergeBatch:

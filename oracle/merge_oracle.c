@@ -256,22 +256,25 @@ void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t
 }
 
 /* The device's random-policy stream (include/merging_hip.h, mg_step_random): step k of env gi
- * uses word k mod 4 of Philox4x32-10(counter (gi, k div 4)); both players random: the pair
- * x = floor(25 w / 2^32), a1 = x / 5, a2 = x % 5; opponent None: a1 = floor(5 w / 2^32). */
+ * draws from word (k div 2) mod 4 of Philox4x32-10(counter (gi, k div 8)); a draw of m outcomes
+ * is floor(m w / 2^32), and an odd step uses w' = m w mod 2^32 (the first draw's remainder).
+ * Both players random: m = 25, x = draw, a1 = x / 5, a2 = x % 5; opponent None: m = 5, a1 = draw. */
 static void draw_actions(int64_t gi, uint64_t seed, uint64_t step, int opp_random, int* a1, int* a2) {
-  const uint64_t blk = step >> 2;
+  const uint64_t blk = step >> 3;
   const uint32_t c[4] = {(uint32_t)gi, (uint32_t)((uint64_t)gi >> 32), (uint32_t)blk,
                          (uint32_t)(blk >> 32)};
   const uint32_t k[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
   uint32_t u[4];
   oracle_philox4x32_10(c, k, u);
-  const uint64_t w = u[step & 3];
+  const uint32_t m = opp_random ? 25u : 5u;
+  uint32_t w = u[(step >> 1) & 3];
+  if (step & 1) w = w * m; /* mod 2^32 */
+  const int x = (int)(((uint64_t)w * m) >> 32);
   if (opp_random) {
-    const int x = (int)((w * 25u) >> 32);
     *a1 = x / 5;
     *a2 = x % 5;
   } else {
-    *a1 = (int)((w * 5u) >> 32);
+    *a1 = x;
     *a2 = -1;
   }
 }
