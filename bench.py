@@ -377,7 +377,21 @@ def hdqn_leg(env, args, world, dist, torch):
     separate_ms = timed(separate)
     del ring
     torch.cuda.empty_cache()
+    # Strategy_OP "selfplay" (hdqn.py:262-264): the same nets also act for the opponent, on the
+    # swapped state (its lower net every step, its meta-net at each outer-loop iteration)
+    for _ in range(2):
+        env.rollout_hdqn(T, meta, lower, args.seed, opponent="self", first_step=k, final_observation=False)
+        k += T
+    self_ms = timed(lambda: env.rollout_hdqn(T, meta, lower, args.seed, opponent="self", first_step=k,
+                                             final_observation=False))
+    self_per_s = E * T / (self_ms * 1e-3)
+    self_flop = HDQN_USEFUL_FLOP + 2 * (11 * 200 + 200 * 100 + 100 * 5)  # + the opponent's lower net
     return {"kernel": "hdqn_rollout_kernel<0>", "opponent": "none", "steps_per_launch": T, "launches": L,
+            "selfplay": {"kernel": "hdqn_rollout_kernel<2>", "kernel_ms_mean": self_ms,
+                         "env_steps_per_s": self_per_s, "useful_tflops_lower_bound": self_flop * self_per_s / 1e12,
+                         "frac_useful_lower_bound": self_flop * self_per_s / 1e12 / MFMA_BF16_PEAK_TFLOPS,
+                         "note": "useful FLOPs count the opponent's lower net every step, not its meta-net "
+                                 "(run only at outer-loop iterations)"},
             "with_goal_ring": {"fused_store_ms_per_launch": fused_ms, "rollout_then_replay_store_ms": separate_ms,
                                "fused_env_steps_per_s": E * T / (fused_ms * 1e-3),
                                "separate_env_steps_per_s": E * T / (separate_ms * 1e-3),

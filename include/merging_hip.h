@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 12
+#define MG_ABI_VERSION 13
 #define MG_OBS_DIM 10   /* merging_env.py:75 observation_shape = (10) */
 #define MG_NUM_ACTIONS 5 /* merging_env.py:101-102 action_dict / Discrete(5) */
 #define MG_ACTION_NONE (-1) /* action2=None: the constant-speed "L0" opponent, merging_env.py:152 */
@@ -295,6 +295,8 @@ typedef struct mg_hdqn_traj {
   float* next_goal;  /* goal Goal_DQN chose on step t's next state (:303; the terminal one at an
                         episode end), the row's next goal */
   float* reward;     /* 1.0 if next_goal == goal_status(state) else 0.0 (:314) */
+  float* goal_op;    /* (optional, opponent_mode 2) the self-play opponent's goal of step t, the
+                        goal of its goal state [goal_op] + swapped state (:285, :299) */
 } mg_hdqn_traj;
 
 /* num_steps steps of hdqn.py's inner loop in ONE launch (opponent L0 or uniform random): per env
@@ -309,7 +311,17 @@ typedef struct mg_hdqn_traj {
  * action, explore, goal) and counter ((env_offset + i) ^ 2^63, first_step + t) for a fresh goal
  * (x, y) and the uniform opponent (z); a launch's first fresh goals use step first_step - 1.
  * Greedy when the explore draw < greedy_threshold (np.random.randn() <= EPISILO, :84, :168).
- * traj as mg_rollout_qnet; opponent_mode 0 (None) or 1 (uniform).
+ * traj as mg_rollout_qnet; opponent_mode 0 (None, Strategy_OP "L0", :261, :294-296), 1 (uniform)
+ * or 2 (Strategy_OP "selfplay", :262-264: upper_op = upper, lower_op = lower, so the same two
+ * nets): the opponent's goal is chosen by the meta-net on the swapped state
+ * state[5:] + state[:5] at every outer-loop iteration (:285 -- the launch's first step when
+ * goal_op[i] < 0, and the step after a break: the ego's goal reached or the episode ended) and
+ * kept in between; its action is the lower net's epsilon-greedy choice on
+ * [goal_op] + swapped state every step (:299-300). Its draws: counter
+ * ((env_offset + i) ^ 2^62, first_step + t), x explore and y action of step t, z explore and
+ * w goal of a fresh opponent goal at step t + 1 (the launch's first at step first_step - 1).
+ * goal_op [n] int8 (required for mode 2, else ignored) holds each env's opponent goal across
+ * launches like goal.
  * ring_rows (optional, 16-byte aligned [ring_capacity, 24] fp32, with ring_counter: one device
  * uint64): the launch also appends every transition to hdqn.py's lower-level memory
  * (HDQN.store_transition, :316, which stores them all) -- row [goal, s, a, r, next_goal, s'] of
@@ -317,7 +329,7 @@ typedef struct mg_hdqn_traj {
  * skip_ego_won = 0 writes from this launch's outputs (only the newest ring_capacity rows when
  * more are appended), then counter += T n. No scan is needed since every row is kept. */
 int mg_rollout_hdqn(const mg_params* params, const mg_state* state, const mg_traj* traj,
-                    const mg_hdqn_traj* htraj, const mg_stats* stats, int8_t* goal, int64_t n,
+                    const mg_hdqn_traj* htraj, const mg_stats* stats, int8_t* goal, int8_t* goal_op, int64_t n,
                     int64_t env_offset, uint64_t seed, uint64_t first_step, int32_t num_steps,
                     const void* meta_net, int32_t num_goals, const void* lower_net, int32_t reset_goal,
                     uint64_t greedy_threshold, int32_t opponent_mode, float* ring_rows,

@@ -1696,6 +1696,10 @@ __global__ void counter_add_kernel(uint64_t* counter, uint64_t k) { *counter += 
 // the inner loop (:320-322), after which -- and after every episode end (:278-283, the outer
 // loops) -- a fresh goal is chosen. Both nets live in LDS (compact packing, 2 x 60.5 KB).
 //
+// OPP 2 is hdqn.py's Strategy_OP "selfplay" (:262-264, upper_op = upper, lower_op = lower): the
+// same two nets also choose the opponent's goal on the swapped state at every outer-loop
+// iteration (:285) and its action on [goal_op] + swapped state (:299-300), two more forwards per
+// phase on the Q-net waves.
 // Per env-step k (global step index) the Philox4x32-10 streams are
 //   A = Philox(counter (gi, k)):            x ego explore draw, y ego random action,
 //                                           z goal explore draw, w random goal (the goal
@@ -1703,6 +1707,8 @@ __global__ void counter_add_kernel(uint64_t* counter, uint64_t k) { *counter += 
 //   B = Philox(counter (gi ^ 2^63, k)):     x, y the same for a fresh goal (after a goal was
 //                                           reached or the episode ended, :283), z the uniform
 //                                           opponent's action (opponent_mode 1)
+//   C = Philox(counter (gi ^ 2^62, k)):     (OPP 2) x explore, y action of the opponent's
+//                                           step, z explore, w goal of its fresh goal at k + 1
 // and a launch whose env has no goal yet (goal[i] < 0) starts it with B of step first_step - 1.
 // Roles as in qnet_rollout_ws_kernel: waves 0-3 run both nets (meta then lower, one 64-env tile
 // each per phase), waves 4-7 the fp64 env step (one env per lane), on two groups of 256 envs
@@ -1715,7 +1721,8 @@ struct HRollout {
   mg_traj T;
   mg_hdqn_traj H;
   mg_stats St;
-  int8_t* goal;  // [n] in / out
+  int8_t* goal;     // [n] in / out
+  int8_t* goal_op;  // [n] in / out, the self-play opponent's goal (OPP 2)
   const uint8_t* meta;
   const uint8_t* lower;
   uint64_t seed;
@@ -1758,14 +1765,16 @@ __device__ __forceinline__ uint4 philox_env_step(uint64_t gi, uint64_t step, uin
 }
 
 // lower-net input of one env: goal state [goal] + state (hdqn.py:291), features 0..10, zero at
-// 11..12 and the bias inputs 1.0 at 13..15
-__device__ __forceinline__ bf16x8 qnet_input_goal(const float* row, int goal, int h) {
+// 11..12 and the bias inputs 1.0 at 13..15; swap: [goal] + state[5:] + state[:5] (the
+// opponent's goal state, :299)
+__device__ __forceinline__ bf16x8 qnet_input_goal(const float* row, int goal, int h, bool swap = false) {
   float v[kObs];
 #pragma unroll
   for (int k = 0; k < kObs / 2; ++k) {
     const f32x2 t = reinterpret_cast<const f32x2*>(row)[k];
-    v[2 * k] = t[0];
-    v[2 * k + 1] = t[1];
+    const int d = swap ? (2 * k + kObs / 2) % kObs : 2 * k;
+    v[d] = t[0];
+    v[d + 1] = t[1];
   }
   auto pk = [](float a, float b) { return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2)); };
   const u32x4 w = h ? u32x4{pk(v[7], v[8]), pk(v[9], 0.f), 0x3F800000u, 0x3F803F80u}
@@ -1787,6 +1796,8 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
   __shared__ __attribute__((aligned(16))) uint32_t side[kHEnvs * 5];    // terminal obs, bf16 pairs
   __shared__ uint8_t b_act[kHEnvs], b_goal[kHEnvs], b_done[kHEnvs], b_st_old[kHEnvs],
       b_st_new[kHEnvs], b_dg[kHEnvs], b_df[kHEnvs], b_g2[kHEnvs];
+  // OPP 2: the opponent's greedy action, current goal and fresh-goal draw
+  __shared__ uint8_t b_aop[OPP == 2 ? kHEnvs : 1], b_gop[OPP == 2 ? kHEnvs : 1], b_dfo[OPP == 2 ? kHEnvs : 1];
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int64_t base = static_cast<int64_t>(blockIdx.x) * kHEnvs;
@@ -1827,11 +1838,12 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
         gstar = argmax_first(q, R.num_goals);
       }
       const int df = b_df[j];
+      bool brk = false;  // step t - 1 left the inner loop (:322): a new outer iteration starts
       if (t > 0) {  // hdqn.py:303-322 for step t - 1
         const int dg = b_dg[j];
         const int goal2 = dg == kHGreedy ? gstar : dg;
         const bool done = b_done[j] != 0;
-        const bool brk = done || goal2 == b_st_new[j];
+        brk = done || goal2 == b_st_new[j];
         goal_t = done ? (df == kHGreedy ? R.reset_goal : df) : (brk ? (df == kHGreedy ? gstar : df) : goal2);
         if (live) {
           const int64_t row = static_cast<int64_t>(t - 1) * R.n + i;
@@ -1842,16 +1854,41 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
       } else {
         goal_t = goal_prev >= 0 ? goal_prev : (df == kHGreedy ? gstar : df);
       }
+      int gop_t = 0;
+      if constexpr (OPP == 2) {  // upper_op.choose_goal(swapped state) at a new outer iteration (:285)
+        const int gop_prev = static_cast<int8_t>(b_gop[j]);
+        const bool fresh_op = t > 0 ? brk : gop_prev < 0;
+        int gop_star = 0;
+        if (__ballot(live && fresh_op) != 0) {  // on the state acted on at step t (reset obs after an end)
+          float q[8];
+          qnet_mlp_swp(lds_meta, qnet_input(tile + (row0 + r) * kObs, true, h),
+                       qnet_input(tile + (row0 + 32 + r) * kObs, true, h), q);
+          gop_star = argmax_first(q, R.num_goals);
+        }
+        const int dfo = b_dfo[j];
+        gop_t = fresh_op ? (dfo == kHGreedy ? gop_star : dfo) : gop_prev;
+      }
       if (t < T) {
         b_goal[j] = static_cast<uint8_t>(goal_t);
         if (live && R.H.goal) st_out(R.H.goal + static_cast<int64_t>(t) * R.n + i, static_cast<float>(goal_t));
+        if constexpr (OPP == 2) {
+          b_gop[j] = static_cast<uint8_t>(gop_t);
+          if (live && R.H.goal_op) st_out(R.H.goal_op + static_cast<int64_t>(t) * R.n + i, static_cast<float>(gop_t));
+        }
         wave_lds_sync();  // the wave's goals are in LDS before the lanes read their column envs'
         float q[8];
         qnet_mlp_swp(lds_lower, qnet_input_goal(tile + (row0 + r) * kObs, b_goal[row0 + r], h),
                      qnet_input_goal(tile + (row0 + 32 + r) * kObs, b_goal[row0 + 32 + r], h), q);
         b_act[j] = static_cast<uint8_t>(argmax_first(q, MG_NUM_ACTIONS));
+        if constexpr (OPP == 2) {  // lower_op.choose_action([goal_op] + swapped state) (:299-300)
+          float qo[8];
+          qnet_mlp_swp(lds_lower, qnet_input_goal(tile + (row0 + r) * kObs, b_gop[row0 + r], h, true),
+                       qnet_input_goal(tile + (row0 + 32 + r) * kObs, b_gop[row0 + 32 + r], h, true), qo);
+          b_aop[j] = static_cast<uint8_t>(argmax_first(qo, MG_NUM_ACTIONS));
+        }
       } else if (live) {
         R.goal[i] = static_cast<int8_t>(goal_t);  // the next launch's starting goal
+        if constexpr (OPP == 2) R.goal_op[i] = static_cast<int8_t>(gop_t);
       }
       __syncthreads();
     }
@@ -1925,6 +1962,11 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
     const uint4 fb = philox_env_step(gi ^ (uint64_t{1} << 63), R.first_step - 1, R.seed);
     b_df[j] = draw_byte(fb.x, fb.y, R.greedy_thr, R.num_goals);
     b_goal[j] = live[g] ? static_cast<uint8_t>(R.goal[i]) : 0;
+    if constexpr (OPP == 2) {
+      const uint4 fc = philox_env_step(gi ^ (uint64_t{1} << 62), R.first_step - 1, R.seed);
+      b_dfo[j] = draw_byte(fc.z, fc.w, R.greedy_thr, R.num_goals);
+      b_gop[j] = live[g] ? static_cast<uint8_t>(R.goal_op[i]) : 0;
+    }
     b_done[j] = 0;
   }
   __syncthreads();
@@ -1938,7 +1980,12 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
       const uint4 ua = philox_env_step(gi, k, R.seed);
       const uint4 ub = philox_env_step(gi ^ (uint64_t{1} << 63), k, R.seed);
       const int a1 = static_cast<uint64_t>(ua.x) < R.greedy_thr ? static_cast<int>(b_act[j]) : action_from_u32(ua.y);
-      const int a2 = OPP == 1 ? action_from_u32(ub.z) : MG_ACTION_NONE;
+      int a2 = OPP == 1 ? action_from_u32(ub.z) : MG_ACTION_NONE;
+      uint4 uc = make_uint4(0u, 0u, 0u, 0u);
+      if constexpr (OPP == 2) {  // the self-play opponent's epsilon-greedy action (:300)
+        uc = philox_env_step(gi ^ (uint64_t{1} << 62), k, R.seed);
+        a2 = static_cast<uint64_t>(uc.x) < R.greedy_thr ? static_cast<int>(b_aop[j]) : action_from_u32(uc.y);
+      }
       if (t > 0) {  // step t - 1's next goal is in LDS now (Q(X, t)); wave-uniform branch per group
         if (g == 0)
           write_row(0, t - 1, ps[0], ps2[0], pgoal[0], pact[0]);
@@ -1968,6 +2015,7 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
         b_st_new[j] = static_cast<uint8_t>(goal_status(rv.o));
         b_dg[j] = draw_byte(ua.z, ua.w, R.greedy_thr, R.num_goals);
         b_df[j] = draw_byte(ub.x, ub.y, R.greedy_thr, R.num_goals);
+        if constexpr (OPP == 2) b_dfo[j] = draw_byte(uc.z, uc.w, R.greedy_thr, R.num_goals);
         const bool won = lv && ev.winner == 1;
         const int64_t rem = R.n - wbase;
         store_won_mask(R.T.won_mask, won, t, R.n, wbase, rem <= 0 ? 0 : (rem < 64 ? static_cast<int>(rem) : 64));
@@ -2692,7 +2740,7 @@ int mg_rollout_qnet(const mg_params* params, const mg_state* state, const mg_tra
 }
 
 int mg_rollout_hdqn(const mg_params* params, const mg_state* state, const mg_traj* traj,
-                    const mg_hdqn_traj* htraj, const mg_stats* stats, int8_t* goal, int64_t n,
+                    const mg_hdqn_traj* htraj, const mg_stats* stats, int8_t* goal, int8_t* goal_op, int64_t n,
                     int64_t env_offset, uint64_t seed, uint64_t first_step, int32_t num_steps,
                     const void* meta_net, int32_t num_goals, const void* lower_net, int32_t reset_goal,
                     uint64_t greedy_threshold, int32_t opponent_mode, float* ring_rows,
@@ -2707,8 +2755,10 @@ int mg_rollout_hdqn(const mg_params* params, const mg_state* state, const mg_tra
     return fail(hipErrorInvalidValue, "%s", "meta_net / lower_net must be 16-byte aligned packed Q-nets");
   if (num_steps < 0 || num_goals < 1 || num_goals > 8 || reset_goal < 0 || reset_goal >= num_goals)
     return fail(hipErrorInvalidValue, "%s", "need num_steps >= 0, 1 <= num_goals <= 8, 0 <= reset_goal < num_goals");
-  if (opponent_mode < 0 || opponent_mode > 1)
-    return fail(hipErrorInvalidValue, "%s", "opponent_mode must be 0 (None) or 1 (uniform)");
+  if (opponent_mode < 0 || opponent_mode > 2)
+    return fail(hipErrorInvalidValue, "%s", "opponent_mode must be 0 (None), 1 (uniform) or 2 (self-play)");
+  if (opponent_mode == 2 && !goal_op)
+    return fail(hipErrorInvalidValue, "%s", "opponent_mode 2 needs goal_op (an [n] int8 device array)");
   if ((traj->obs && (reinterpret_cast<uintptr_t>(traj->obs) & 15)) ||
       (traj->final_obs && (reinterpret_cast<uintptr_t>(traj->final_obs) & 7)) ||
       (traj->rew && (reinterpret_cast<uintptr_t>(traj->rew) & 7)) ||
@@ -2722,6 +2772,7 @@ int mg_rollout_hdqn(const mg_params* params, const mg_state* state, const mg_tra
   if (htraj) R.H = *htraj;
   if (stats) R.St = *stats;
   R.goal = goal;
+  R.goal_op = goal_op;
   R.meta = static_cast<const uint8_t*>(meta_net);
   R.lower = static_cast<const uint8_t*>(lower_net);
   R.seed = seed;
@@ -2740,8 +2791,10 @@ int mg_rollout_hdqn(const mg_params* params, const mg_state* state, const mg_tra
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (opponent_mode == 0)
     hipLaunchKernelGGL(hdqn_rollout_kernel<0>, dim3(blocks), dim3(512), 0, st, R);
-  else
+  else if (opponent_mode == 1)
     hipLaunchKernelGGL(hdqn_rollout_kernel<1>, dim3(blocks), dim3(512), 0, st, R);
+  else
+    hipLaunchKernelGGL(hdqn_rollout_kernel<2>, dim3(blocks), dim3(512), 0, st, R);
   if (ring_rows)  // after every block has read the old counter: the same stream orders it
     hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(1), 0, st, ring_counter,
                        static_cast<uint64_t>(num_steps) * static_cast<uint64_t>(n));

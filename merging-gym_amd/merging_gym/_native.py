@@ -15,7 +15,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libmerging_hip.so"
 LIB_PATH = os.environ.get("MERGING_HIP_LIB", os.path.join(_HERE, LIB_NAME))
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 OBS_DIM = 10
 NUM_ACTIONS = 5
@@ -64,7 +64,7 @@ class Transitions(_c.Structure):
 
 
 class HdqnTraj(_c.Structure):
-    _fields_ = [(n, _P) for n in ("goal", "next_goal", "reward")]
+    _fields_ = [(n, _P) for n in ("goal", "next_goal", "reward", "goal_op")]
 
 
 class Stats(_c.Structure):
@@ -113,7 +113,7 @@ def _load():
     lib.mg_rollout_qnet.argtypes = [PP, SP, _c.POINTER(Traj), STP, _c.c_int64, _c.c_int64, _c.c_uint64,
                                     _c.c_uint64, _c.c_int32, _P, _c.c_int32, _c.c_uint64, _c.c_int32,
                                     _c.c_uint64, _c.c_uint32, _P]
-    lib.mg_rollout_hdqn.argtypes = [PP, SP, _c.POINTER(Traj), _c.POINTER(HdqnTraj), STP, _P, _c.c_int64,
+    lib.mg_rollout_hdqn.argtypes = [PP, SP, _c.POINTER(Traj), _c.POINTER(HdqnTraj), STP, _P, _P, _c.c_int64,
                                     _c.c_int64, _c.c_uint64, _c.c_uint64, _c.c_int32, _P, _c.c_int32, _P,
                                     _c.c_int32, _c.c_uint64, _c.c_int32, _P, _P, _c.c_int64, _c.c_uint32, _P]
     lib.mg_time_next_launch.argtypes = [_P, _P]

@@ -316,11 +316,15 @@ class MergeVecEnv:
         next state, the lower-level Net (`lower`, a QNet 11 -> 5) acts epsilon-greedily on the
         goal state [goal] + state, goal_status gives the intrinsic reward, and a fresh goal is
         chosen once a goal is reached or an episode ends. opponent: "none" (L0, hdqn.py's default
-        Strategy_OP) or "uniform". Each env's current goal persists across launches in
-        `self.hdqn_goal` ([N] int8, -1 = none yet). Returns rollout_random's [T, N, ...] dict
-        plus "goal", "next_goal" and "reward" ([T, N] fp32: the goal columns and the intrinsic
-        reward of HDQN.store_transition's rows, :316 -- ReplayRing(goal=True).store_rollout takes
-        them as they are). ring: a ReplayRing(goal=True) the same launch appends every
+        Strategy_OP), "uniform", or "self" (Strategy_OP "selfplay", :262-264: the same two nets
+        choose the opponent's goal on the swapped state at every outer-loop iteration, :285, and
+        its action on [goal_op] + swapped state, :299-300). Each env's current goal persists
+        across launches in `self.hdqn_goal` ([N] int8, -1 = none yet), the self-play opponent's
+        in `self.hdqn_goal_op`. Returns rollout_random's [T, N, ...] dict plus "goal",
+        "next_goal" and "reward" ([T, N] fp32: the goal columns and the intrinsic reward of
+        HDQN.store_transition's rows, :316 -- ReplayRing(goal=True).store_rollout takes them as
+        they are), and with opponent "self" "goal_op" ([T, N] fp32, the opponent's goal of each
+        step). ring: a ReplayRing(goal=True) the same launch appends every
         transition to (hdqn.py:316 stores them all, so the kernel needs no scan): the rows
         store_rollout(obs0, traj, skip_ego_won=False, goal=..., next_goal=..., reward=...) would
         write, without re-reading the trajectory."""
@@ -328,7 +332,7 @@ class MergeVecEnv:
 
         torch, nat = self._torch, self._nat
         T, n = int(num_steps), self.num_envs
-        mode = {"none": 0, "uniform": 1}[opponent]
+        mode = {"none": 0, "uniform": 1, "self": 2}[opponent]
         if ring is not None and (not ring.goal or ring.device != self.device):
             raise ValueError("the fused store needs a goal ring (ReplayRing(goal=True)) on this env's device")
         if meta.in_dim != _OBS_DIM or lower.in_dim != _OBS_DIM + 1 or lower.out_dim != nat.NUM_ACTIONS:
@@ -338,14 +342,17 @@ class MergeVecEnv:
         hb = getattr(self, "_hdqn_bufs", None)
         if hb is None or hb["goal"].shape[0] != T:
             hb = {k: torch.empty((T, n), dtype=torch.float32, device=self.device)
-                  for k in ("goal", "next_goal", "reward")}
-            hb["_h"] = nat.HdqnTraj(*(hb[k].data_ptr() for k in ("goal", "next_goal", "reward")))
+                  for k in ("goal", "next_goal", "reward", "goal_op")}
+            hb["_h"] = nat.HdqnTraj(*(hb[k].data_ptr() for k in ("goal", "next_goal", "reward", "goal_op")))
             self._hdqn_bufs = hb
         if getattr(self, "hdqn_goal", None) is None:
             self.hdqn_goal = torch.full((n,), -1, dtype=torch.int8, device=self.device)
+        if mode == 2 and getattr(self, "hdqn_goal_op", None) is None:
+            self.hdqn_goal_op = torch.full((n,), -1, dtype=torch.int8, device=self.device)
+        gop = getattr(self, "hdqn_goal_op", None)
         rc = nat.lib.mg_rollout_hdqn(
             self._p_ref, self._s_ref, ctypes.byref(buf["_traj"]), ctypes.byref(hb["_h"]), self._st_ref,
-            self.hdqn_goal.data_ptr(), n, self.env_offset, seed & 0xFFFFFFFFFFFFFFFF, k0 & 0xFFFFFFFFFFFFFFFF,
+            self.hdqn_goal.data_ptr(), None if gop is None else gop.data_ptr(), n, self.env_offset, seed & 0xFFFFFFFFFFFFFFFF, k0 & 0xFFFFFFFFFFFFFFFF,
             T, meta.packed.data_ptr(), meta.out_dim, lower.packed.data_ptr(), meta.reset_argmax(),
             greedy_threshold(episilo), mode, None if ring is None else ring.memory.data_ptr(),
             None if ring is None else ring._counter.data_ptr(), 0 if ring is None else ring.capacity,
@@ -354,6 +361,8 @@ class MergeVecEnv:
         self._step_idx = k0 + T
         out = dict(buf["_result"])
         out.update(goal=hb["goal"], next_goal=hb["next_goal"], reward=hb["reward"])
+        if mode == 2:
+            out["goal_op"] = hb["goal_op"]
         return out
 
     def observe(self):
@@ -426,6 +435,8 @@ class MergeVecEnv:
             sd["ret_sum"], sd["counts"] = self.ret_sum.clone(), self.counts.clone()
         if getattr(self, "hdqn_goal", None) is not None:
             sd["hdqn_goal"] = self.hdqn_goal.clone()  # rollout_hdqn's current goals
+        if getattr(self, "hdqn_goal_op", None) is not None:
+            sd["hdqn_goal_op"] = self.hdqn_goal_op.clone()  # and the self-play opponent's
         return sd
 
     def load_state_dict(self, sd):
@@ -443,6 +454,8 @@ class MergeVecEnv:
             self.counts.copy_(self._torch.as_tensor(sd["counts"]))
         if "hdqn_goal" in sd:
             self.hdqn_goal = self._torch.as_tensor(sd["hdqn_goal"]).to(self.device, self._torch.int8).clone()
+        if "hdqn_goal_op" in sd:
+            self.hdqn_goal_op = self._torch.as_tensor(sd["hdqn_goal_op"]).to(self.device, self._torch.int8).clone()
 
     def close(self):
         pass

@@ -42,7 +42,7 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_native.Traj) == 9 * 8
     assert ctypes.sizeof(_native.Transitions) == 11 * 8
     assert ctypes.sizeof(_native.Stats) == 8
-    assert ctypes.sizeof(_native.HdqnTraj) == 3 * 8
+    assert ctypes.sizeof(_native.HdqnTraj) == 4 * 8
     assert _native.EPISODE_STATS_BYTES == 32  # mg_episode_stats: 2 f64 + 4 u32
     assert _native.REC64_DTYPE.itemsize == 168
 

@@ -119,14 +119,22 @@ def _pick(u, k):  # floor(k u / 2^32)
     return ((u.astype(np.uint64) * np.uint64(k)) >> np.uint64(32)).astype(np.int64)
 
 
-@pytest.mark.parametrize("n", [2048, 1000])
-def test_fused_hdqn_rollout(coracle, n):
+def _swap(o):
+    """state[5:] + state[:5], the opponent's view (hdqn.py:285, :299)."""
+    return np.concatenate([o[:, 5:], o[:, :5]], axis=1)
+
+
+@pytest.mark.parametrize("n,opponent", [(2048, "none"), (1000, "none"), (2048, "self"), (1000, "self")])
+def test_fused_hdqn_rollout(coracle, n, opponent):
     """mg_rollout_hdqn -- hdqn.py:280-323 in one launch -- against the loop restated on the CPU:
     every transition equals the C oracle's given the kernel's actions; every action, next goal and
     fresh goal is the epsilon-greedy choice its Philox draws make with the bf16-emulated nets'
     argmax (near-ties excused); the intrinsic reward is goal_status's; the goal ring the
     trajectory feeds equals the oracle's replay_store bit for bit. Starts mid-episode, so goals
-    are reached and episodes end inside the launch; a second launch continues the goals."""
+    are reached and episodes end inside the launch; a second launch continues the goals.
+    opponent "self" (Strategy_OP "selfplay", :262-264): the opponent's goal is the meta-net's
+    epsilon-greedy choice on the swapped state at every outer-loop iteration (:285) and kept in
+    between, its action the lower net's on [goal_op] + swapped state (:299-300)."""
     import torch
 
     from merging_gym import MergeVecEnv, ReplayRing
@@ -153,7 +161,9 @@ def test_fused_hdqn_rollout(coracle, n):
     q_reset = mo.qnet_reference(meta_sd, coracle.reset(coracle.new_envs(1)).astype(np.float32), bf16=True)
     assert reset_goal == q_reset.argmax(1)[0] or _near_tie(q_reset)[0]
     fresh_off = -(1 << 63)  # counter (env ^ 2^63, step): the fresh-goal stream
-    goal_prev = None
+    op_off = 1 << 62  # counter (env ^ 2^62, step): the self-play opponent's stream
+    selfplay = opponent == "self"
+    goal_prev = gop_prev = None
     rows = {k: [] for k in ("obs0", "obs", "fobs", "a1", "rew", "done", "goal", "goal2", "r_int")}
     ring = ReplayRing(4 * n * T, device=dev, goal=True)
     # the same rows appended by the launch itself (fused store); a capacity below one launch's
@@ -162,9 +172,10 @@ def test_fused_hdqn_rollout(coracle, n):
     ring_f = ReplayRing(cap_f, device=dev, goal=True)
     for launch in range(2):
         obs_first = obs.copy()
-        tr = env.rollout_hdqn(T, meta, lower, seed, first_step=k0, ring=ring_f)
-        g = {k: tr[k].cpu().numpy().copy() for k in ("goal", "next_goal", "reward")}
+        tr = env.rollout_hdqn(T, meta, lower, seed, opponent=opponent, first_step=k0, ring=ring_f)
+        g = {k: tr[k].cpu().numpy().copy() for k in ("goal", "next_goal", "reward") + (("goal_op",) if selfplay else ())}
         a1_all, done_all = tr["a1"].cpu().numpy().copy(), tr["done"].cpu().numpy().copy()
+        a2_all = tr["a2"].cpu().numpy().copy()
         o_all, fo_all, rew_all = (tr[k].cpu().numpy().copy() for k in ("obs", "final_observation", "rew"))
         ring.store_rollout(torch.from_numpy(obs_first).to(dev), tr, skip_ego_won=False, goal=tr["goal"],
                            next_goal=tr["next_goal"], reward=tr["reward"])
@@ -177,6 +188,17 @@ def test_fused_hdqn_rollout(coracle, n):
         else:
             ok = g["goal"][0] == goal_prev
         assert ok.all(), launch
+        if selfplay:  # the opponent's first goal (:285): carried over, or fresh with step k0 - 1's draw
+            if gop_prev is None:
+                fc = coracle.philox_batch(n, op_off, seed, k0 - 1)
+                qo = mo.qnet_reference(meta_sd, _swap(obs), bf16=True)
+                gf0 = fc[:, 2] < thr
+                ok = (g["goal_op"][0] == np.where(gf0, qo.argmax(1), _pick(fc[:, 3], NUM_GOALS))) | (gf0 & _near_tie(qo))
+            else:
+                ok = g["goal_op"][0] == gop_prev
+            assert ok.all(), launch
+        else:
+            assert (a2_all == -1).all()
         for t in range(T):
             k = k0 + t
             ua = coracle.philox_batch(n, 0, seed, k)
@@ -187,7 +209,16 @@ def test_fused_hdqn_rollout(coracle, n):
             greedy = ua[:, 0] < thr
             exp_a = np.where(greedy, q1.argmax(1), _pick(ua[:, 1], 5))
             assert ((a1_all[t] == exp_a) | (greedy & _near_tie(q1))).all(), (launch, t)
-            o_obs, o_rew, o_done, o_coll, _, o_fobs, err = coracle.step(envs, a1_all[t].astype(np.int8), None,
+            a2 = None
+            if selfplay:  # lower_op.choose_action([goal_op] + swapped state), :299-300
+                uc = coracle.philox_batch(n, op_off, seed, k)
+                xo = np.concatenate([g["goal_op"][t][:, None].astype(np.float32), _swap(obs)], axis=1)
+                qa = mo.qnet_reference(lower_sd, xo, bf16=True)
+                go = uc[:, 0] < thr
+                exp_a2 = np.where(go, qa.argmax(1), _pick(uc[:, 1], 5))
+                assert ((a2_all[t] == exp_a2) | (go & _near_tie(qa))).all(), (launch, t)
+                a2 = a2_all[t].astype(np.int8)
+            o_obs, o_rew, o_done, o_coll, _, o_fobs, err = coracle.step(envs, a1_all[t].astype(np.int8), a2,
                                                                         autoreset=True, final_obs=True)
             assert err == 0
             np.testing.assert_array_equal(done_all[t], o_done.astype(bool), err_msg=str(t))
@@ -209,12 +240,21 @@ def test_fused_hdqn_rollout(coracle, n):
             exp_next = np.where(brk, fresh, g2)
             nxt = g["goal"][t + 1] if t + 1 < T else env.hdqn_goal.cpu().numpy().astype(np.int64)
             assert ((nxt == exp_next) | (brk & gf & ~d & _near_tie(q2))).all(), (launch, t)
+            if selfplay:  # the opponent's goal of the next step: fresh at a new outer iteration (:285)
+                qo = mo.qnet_reference(meta_sd, _swap(o_all[t]), bf16=True)  # the state acted on next (reset obs after an end)
+                go = uc[:, 2] < thr
+                exp_op = np.where(brk, np.where(go, qo.argmax(1), _pick(uc[:, 3], NUM_GOALS)), g["goal_op"][t])
+                nxo = g["goal_op"][t + 1] if t + 1 < T else env.hdqn_goal_op.cpu().numpy().astype(np.int64)
+                assert ((nxo == exp_op) | (brk & go & _near_tie(qo))).all(), (launch, t)
             for key, v in (("obs0", obs), ("obs", o_all[t]), ("fobs", fo_all[t]), ("a1", a1_all[t]),
                            ("rew", rew_all[t]), ("done", d), ("goal", g["goal"][t]), ("goal2", g["next_goal"][t]),
                            ("r_int", g["reward"][t])):
                 rows[key].append(v.copy())
             obs = o_all[t]
         goal_prev = env.hdqn_goal.cpu().numpy().astype(np.int64)
+        if selfplay:
+            gop_prev = env.hdqn_goal_op.cpu().numpy().astype(np.int64)
+            assert (np.stack(a2_all) >= 0).all() and (np.stack(a2_all) <= 4).all()
         k0 += T
     assert np.stack(rows["done"]).any() and (np.stack(rows["r_int"]) == 1).any()
     assert (np.stack(rows["goal"]) != np.stack(rows["goal2"])).any()
