@@ -126,6 +126,18 @@ def test_argument_errors_without_gpu():
     rc = _native.lib.mg_step_random(P, st, fake, None, ctypes.byref(_native.Outputs(flags=fake)), None, 16, 0, 1,
                                     0, 1, 0, None)
     assert rc != 0 and b"a1_out" in _native.lib.mg_last_error()
+    # h-DQN acting loop: the self-play opponent needs its goal array, the fused ring its counter
+    # and 16-byte alignment, opponent modes beyond 2 are refused
+    traj, ht = ctypes.byref(_native.Traj()), ctypes.byref(_native.HdqnTraj())
+
+    def hdqn(goal_op, mode, ring=None, counter=None, cap=0):
+        return _native.lib.mg_rollout_hdqn(P, st, traj, ht, None, fake, goal_op, 16, 0, 1, 0, 4, fake, 3, fake,
+                                          0, 1 << 31, mode, ring, counter, cap, 0, None)
+    assert hdqn(None, 2) != 0 and b"goal_op" in _native.lib.mg_last_error()
+    assert hdqn(fake, 3) != 0 and b"opponent_mode" in _native.lib.mg_last_error()
+    assert hdqn(None, 0, ring=fake) != 0 and b"ring_counter" in _native.lib.mg_last_error()
+    assert hdqn(None, 0, ring=ctypes.c_void_p((1 << 20) + 8), counter=fake, cap=16) != 0
+    assert b"16-byte" in _native.lib.mg_last_error()
     # 65536 write blocks in 1024 scan groups: ticket (8) + bases u64 + offsets u32 + totals u32
     assert _native.lib.mg_replay_scratch_bytes(1 << 20, 16) == 8 + 1024 * 8 + 65536 * 4 + 1024 * 4
     assert _native.lib.mg_replay_scratch_bytes(0, 4) == 0
