@@ -24,6 +24,7 @@ Infinity Cache, N = 1 only), cpu_baseline = the CPU restatements on the host cor
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -537,8 +538,19 @@ def main():
     for k in range(k0, k0 + args.burn_in_launches):
         step(k)
     k0 += args.burn_in_launches
+    # The W warm-up launches run inside a rehearsal of the timed window (synchronize, event
+    # pair, launches, event record, synchronize, elapsed time): the first such window of a
+    # process pays one-time host costs -- 55-65 us before its first launch and a 30-40 us stall
+    # inside, +15 % on a 20-launch window, 0 in the following ones (tools/window_probe2.py,
+    # profiles/r02/window_probe2.json)
+    torch.cuda.synchronize()
+    wev0, wev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    wev0.record()
     for k in range(k0, k0 + args.warmup):
         step(k)
+    wev1.record()
+    torch.cuda.synchronize()
+    wev0.elapsed_time(wev1)
     k0 += args.warmup
     graph = capture_steps(step, k0, args.steps, torch) if args.graph else None
     env.clear_statistics()
@@ -548,6 +560,7 @@ def main():
     # a barrier + synchronize, with one HIP event pair recorded on the stream the kernels run on
     # (torch's current stream). Average launch duration = region / K (launch gaps included).
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    gc.disable()  # no collector pause inside the window
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -564,6 +577,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    gc.enable()
     kernel_ms = ev0.elapsed_time(ev1) / args.steps
     k0 += args.steps
     completed_in_window = int(env.counts[:, 0].sum())

@@ -13,7 +13,7 @@ echo "== smoke" && timeout -k 10 300 python -c "import __graft_entry__ as g; g.s
 && echo "== bench driver-style (graph)" && timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_k20_graph.log 2>&1 && tail -1 $O/bench_k20_graph.log | cut -c1-700 \
 && echo "== bench driver-style (no graph)" && timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --graph 0 --no-cpu-baseline > $O/bench_k20_nograph.log 2>&1 && tail -1 $O/bench_k20_nograph.log | cut -c1-500 \
 && echo "== bench default" && timeout -k 10 300 python bench.py > $O/bench_default.log 2>&1 && tail -1 $O/bench_default.log | cut -c1-300 \
-&& echo "== rocprof stats" && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o $TAG -- python bench.py --steps 300 --warmup 20 --no-cpu-baseline > $O/prof.log 2>&1 && tail -1 $O/prof.log | cut -c1-200 \
+&& echo "== rocprof stats" && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o $TAG -- python bench.py --steps 300 --warmup 20 --no-cpu-baseline --size2-envs 0 > $O/prof.log 2>&1 && tail -1 $O/prof.log | cut -c1-200 \
 && echo "== pmc fetch" && timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o pmc -- python tools/profile_pmc.py > $O/pmc_fetch.log 2>&1 \
 && echo "== pmc write" && timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o pmc -- python tools/profile_pmc.py > $O/pmc_write.log 2>&1 \
 && echo "== all ok"
