@@ -543,6 +543,8 @@ def main():
     # process pays one-time host costs -- 55-65 us before its first launch and a 30-40 us stall
     # inside, +15 % on a 20-launch window, 0 in the following ones (tools/window_probe2.py,
     # profiles/r02/window_probe2.json)
+    if world > 1:
+        dist.barrier()
     torch.cuda.synchronize()
     wev0, wev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     wev0.record()
@@ -550,6 +552,8 @@ def main():
         step(k)
     wev1.record()
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     wev0.elapsed_time(wev1)
     k0 += args.warmup
     graph = capture_steps(step, k0, args.steps, torch) if args.graph else None
