@@ -366,3 +366,48 @@ def test_fused_hdqn_rollout_full_size(coracle):
     for name, src in (("pos1", env.p1), ("vel1", env.v1), ("pos2", env.p2), ("vel2", env.v2),
                       ("r1_acc", env.ret1), ("r2_acc", env.ret2)):
         np.testing.assert_array_equal(src[idx].cpu().numpy(), envs[name], err_msg=name)
+
+
+@pytest.mark.parametrize("opponent", ["none", "self"])
+def test_hdqn_checkpoint_resume_is_bit_exact(opponent):
+    """A checkpoint taken between two h-DQN launches (MergeVecEnv.state_dict: the batch state, the
+    step index keying the draws, the ego's goals and the self-play opponent's goals) resumes the
+    acting loop bit for bit: the next launch from the restored env equals the uninterrupted one
+    in every output, goal and state array."""
+    import io
+
+    import torch
+
+    from merging_gym import MergeVecEnv
+    from merging_gym.policy import NUM_GOALS, QNet
+
+    n, T, seed, dev = 1500, 12, 4, "cuda:0"
+    rng = np.random.default_rng(8)
+    meta = QNet.from_state_dict(_net(rng, 10, NUM_GOALS), device=dev)
+    lower = QNet.from_state_dict(_net(rng, 11, 5), device=dev)
+    env = MergeVecEnv(n, device=dev, final_observation=True)
+    for k in range(180):
+        env.step_random(seed, opponent_random=False, step_idx=k)
+    env.rollout_hdqn(T, meta, lower, seed, opponent=opponent, first_step=180)
+    buf = io.BytesIO()
+    torch.save(env.state_dict(), buf)
+    tr_a = {k: v.clone() for k, v in env.rollout_hdqn(T, meta, lower, seed, opponent=opponent).items()
+            if v is not None}
+    end = env.state_dict()
+    buf.seek(0)
+    env2 = MergeVecEnv(n, device=dev, final_observation=True)
+    env2.load_state_dict(torch.load(buf, weights_only=True))
+    tr_b = env2.rollout_hdqn(T, meta, lower, seed, opponent=opponent)
+    assert set(tr_a) <= set(k for k, v in tr_b.items() if v is not None)
+    done = tr_a["done"]
+    assert bool(done.any())
+    for k, v in tr_a.items():
+        if k == "final_observation":  # written on the rows that ended only (the rest is scratch)
+            v, w = v[done], tr_b[k][done]
+        else:
+            w = tr_b[k]
+        same = torch.equal(v, w)
+        assert same, k
+    for k, v in env2.state_dict().items():
+        assert (torch.equal(v, end[k]) if isinstance(v, torch.Tensor) else v == end[k]), k
+    assert ("hdqn_goal_op" in end) == (opponent == "self")
