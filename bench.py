@@ -258,6 +258,10 @@ def qnet_leg(env, args, world, dist, torch, opponent):
     f = np.load(os.path.join(ROOT, "tests", "golden", "dqn_checkpoints.npz"))
     qnet = QNet.from_state_dict({k.split("/", 1)[1]: f[k] for k in f.files if k.startswith("l1/")},
                                 device=env.device)
+    label = opponent
+    if opponent == "other":  # main.py's default Strategy_OP "L1": another trained DQN (:161-168)
+        opponent = QNet.from_state_dict({k.split("/", 1)[1]: f[k] for k in f.files if k.startswith("l3/")},
+                                        device=env.device)
     T, L, E = args.rollout_steps, args.qnet_launches, env.num_envs
     k = 20_000_000
     for _ in range(max(1, args.leg_warmup)):
@@ -280,7 +284,7 @@ def qnet_leg(env, args, world, dist, torch, opponent):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / L
-    nets = 2 if opponent == "self" else 1
+    nets = 2 if label in ("self", "other") else 1
     per_s = E * T / (kernel_ms * 1e-3)
     # BASELINE config 5: greedy-action agreement with the reference's fp32 Net on the CPU
     # (main.py:30-47, re-declared here with torch) over the envs' current observations
@@ -291,8 +295,9 @@ def qnet_leg(env, args, world, dist, torch, opponent):
     h = torch.relu(x @ w["fc1.weight"].T + w["fc1.bias"])
     h = torch.relu(h @ w["fc2.weight"].T + w["fc2.bias"])
     greedy_cpu = (h @ w["out.weight"].T + w["out.bias"]).argmax(1)
-    return {"kernel": f"qnet_rollout_kernel<{ {'none': 0, 'uniform': 1, 'self': 2}[opponent] }>",
-            "opponent": opponent, "steps_per_launch": T, "launches": L, "dtype": "bf16 (fp32 accumulate)",
+    return {"kernel": f"qnet_rollout_kernel<{ {'none': 0, 'uniform': 1, 'self': 2, 'other': 3}[label] }>",
+            "opponent": label if label != "other" else "other net (main.py Strategy_OP L1; checkpoint l3)",
+            "steps_per_launch": T, "launches": L, "dtype": "bf16 (fp32 accumulate)",
             "value": world * E * T * L / elapsed, "unit": "env-steps/s",
             "ms_per_step": elapsed / (L * T) * 1e3, "kernel_ms_mean": kernel_ms,
             "useful_tflops": nets * QNET_USEFUL_FLOP * per_s / 1e12,
@@ -640,7 +645,7 @@ def main():
 
     qnet = None
     if args.qnet_launches > 0 and args.rollout_steps > 0:
-        qnet = [qnet_leg(env, args, world, dist, torch, opp) for opp in ("none", "self")]
+        qnet = [qnet_leg(env, args, world, dist, torch, opp) for opp in ("none", "self", "other")]
 
     hdqn = None
     if args.qnet_launches > 0 and args.rollout_steps > 0:

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 13
+#define MG_ABI_VERSION 14
 #define MG_OBS_DIM 10   /* merging_env.py:75 observation_shape = (10) */
 #define MG_NUM_ACTIONS 5 /* merging_env.py:101-102 action_dict / Discrete(5) */
 #define MG_ACTION_NONE (-1) /* action2=None: the constant-speed "L0" opponent, merging_env.py:152 */
@@ -276,14 +276,17 @@ int mg_qnet_forward(const void* packed, const float* x, int32_t in_dim, int32_t 
  * gives u = (u0, u1, u2, u3); the ego acts greedily (argmax of Q(obs), lowest index on ties)
  * when u0 < greedy_threshold and takes floor(5 u1 / 2^32) otherwise -- greedy_threshold =
  * round(Phi(0.7) 2^32) reproduces `np.random.randn() <= EPISILO` (main.py:105). The opponent
- * is None (opponent_mode 0), uniform floor(5 u3 / 2^32) (1), or the same net on the swapped
- * observation with u2 / u3 and opp_greedy_threshold (2). Outputs as mg_rollout_random
+ * is None (opponent_mode 0), uniform floor(5 u3 / 2^32) (1), the same net on the swapped
+ * observation with u2 / u3 and opp_greedy_threshold (2, Strategy_OP "selfplay", main.py:165-166),
+ * or another packed net opp_net (same out_dim) on the swapped observation the same way (3,
+ * main.py's default Strategy_OP "L1": a separately trained DQN as the opponent, :161-168, :199;
+ * ABI 14; opp_net is ignored by the other modes). Outputs as mg_rollout_random
  * (traj->obs[t] = observation after step t, the network input of step t + 1). */
 int mg_rollout_qnet(const mg_params* params, const mg_state* state, const mg_traj* traj,
                     const mg_stats* stats, int64_t n, int64_t env_offset, uint64_t seed,
                     uint64_t first_step, int32_t num_steps, const void* net, int32_t out_dim,
                     uint64_t greedy_threshold, int32_t opponent_mode,
-                    uint64_t opp_greedy_threshold, uint32_t flags, void* stream);
+                    uint64_t opp_greedy_threshold, const void* opp_net, uint32_t flags, void* stream);
 
 /* ---- h-DQN acting loop (scripts/hdqn.py:280-323) ----------------------------------------------
  * The per-step outputs of mg_rollout_hdqn besides mg_traj, [T, n] fp32 each (NULL skips one):

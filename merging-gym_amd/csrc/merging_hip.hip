@@ -1014,7 +1014,6 @@ constexpr int kQBlock = MG_QNET_BLOCK;                             // waves shar
 // MG_QNET_WS_ILP envs per phase, so a group is 64 x env waves x ILP envs and a block holds two
 constexpr int kQWsThreads = 64 * (4 + MG_QNET_WS_ENV_WAVES);
 constexpr int kQWsWavesPerSimd = (4 + MG_QNET_WS_ENV_WAVES) / 4;
-constexpr int kQWsEnvs = 2 * 64 * MG_QNET_WS_ENV_WAVES * MG_QNET_WS_ILP;
 static_assert(kQOffW2 % 16 == 0 && kQOffW3 % 16 == 0 && kQNetBytes % 16 == 0,
               "packed Q-net sections must stay 16-byte aligned");
 
@@ -1377,6 +1376,7 @@ struct QRollout {
   mg_traj T;
   mg_stats St;
   const uint8_t* net;
+  const uint8_t* opp_net;   // OPP 3: the opponent's own net (main.py's Strategy_OP "L1")
   uint64_t seed;
   uint64_t first_step;
   uint64_t greedy_thr;      // greedy iff u32 draw < greedy_thr (2^32: always)
@@ -1413,7 +1413,7 @@ __device__ __forceinline__ void qnet_policy_step(const QRollout& R, Env& e, Step
   const int a1 = (static_cast<uint64_t>(u.x) < R.greedy_thr) ? greedy1 : action_from_u32(u.y);
   int a2 = MG_ACTION_NONE;
   if constexpr (OPP == 1) a2 = action_from_u32(u.w);
-  if constexpr (OPP == 2)
+  if constexpr (OPP >= 2)
     a2 = (static_cast<uint64_t>(u.z) < R.opp_greedy_thr) ? greedy2 : action_from_u32(u.w);
   env_step(R.P, e, a1, a2, r);
   if (R.T.rew)
@@ -1444,7 +1444,7 @@ __device__ __forceinline__ void qnet_policy_step_n(const QRollout& R, Env (&e)[N
     a1[j] = (static_cast<uint64_t>(u.x) < R.greedy_thr) ? greedy1[j] : action_from_u32(u.y);
     a2[j] = MG_ACTION_NONE;
     if constexpr (OPP == 1) a2[j] = action_from_u32(u.w);
-    if constexpr (OPP == 2)
+    if constexpr (OPP >= 2)
       a2[j] = (static_cast<uint64_t>(u.z) < R.opp_greedy_thr) ? greedy2[j] : action_from_u32(u.w);
   }
   env_step_lockstep<N>(R.P, e, a1, a2, r);
@@ -1577,24 +1577,35 @@ struct PhaseClock {
 //   Q(A,0) | Q(B,0) + step(A,0) | Q(A,1) + step(B,0) | ... | step(B,T-1)
 // Greedy actions go to the env waves through LDS; the new observations come back through the
 // tile rows. Each env-wave lane holds the two envs (one per group) it steps.
+// OPP 3 (main.py's default Strategy_OP "L1", :161-168: the opponent is another trained DQN)
+// keeps a second packed net in LDS; the two nets and a 1,024-env tile would pass the CU's 160 KB,
+// so that instance runs ILP 1: 512-env blocks, one env per env-wave lane.
+template <int OPP>
+constexpr int qws_ilp() { return OPP == 3 ? 1 : MG_QNET_WS_ILP; }
+template <int OPP>
+constexpr int qws_envs() { return 2 * 64 * MG_QNET_WS_ENV_WAVES * qws_ilp<OPP>(); }
+
 template <int OPP>
 __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws_kernel(const QRollout R) {
-  constexpr int kIlp = MG_QNET_WS_ILP;
-  constexpr int kHalf = kQWsEnvs / 2;   // envs per group
-  constexpr int kTiles = kHalf / 256;   // 64-env tiles each Q-net wave computes per phase
+  constexpr int kIlp = qws_ilp<OPP>();
+  constexpr int kEnvs = qws_envs<OPP>();  // envs per block
+  constexpr int kHalf = kEnvs / 2;        // envs per group
+  constexpr int kTiles = kHalf / 256;     // 64-env tiles each Q-net wave computes per phase
   constexpr int kEnvWaves = MG_QNET_WS_ENV_WAVES;
   static_assert(kTiles >= 1 && kHalf == 64 * kEnvWaves * kIlp && kHalf % 256 == 0,
                 "group = 4 Q-net waves x kTiles x 64 envs = env waves x ILP x 64 envs");
   __shared__ __attribute__((aligned(16))) uint8_t lds_net[kQNetBytes];
-  __shared__ __attribute__((aligned(16))) float tile[kQWsEnvs * kObs];
-  __shared__ uint8_t greedy[2][kQWsEnvs];
+  __shared__ __attribute__((aligned(16))) uint8_t lds_net2[OPP == 3 ? kQNetBytes : 16];
+  __shared__ __attribute__((aligned(16))) float tile[kEnvs * kObs];
+  __shared__ uint8_t greedy[2][kEnvs];
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int64_t base = static_cast<int64_t>(blockIdx.x) * kQWsEnvs;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kEnvs;
   const bool qwave = wave < 4;
   const int ew = wave - 4;
 
   qnet_to_lds(R.net, lds_net);
+  if constexpr (OPP == 3) qnet_to_lds(R.opp_net, lds_net2);
   const int phases = 2 * R.num_steps + 1;
   if (qwave) {
     // Q-net waves: the barrier count matches the env waves' loop below, phase for phase
@@ -1610,8 +1621,8 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
           float q[8];
           qnet_forward_ws(lds_net, tile, row0, false, q);
           greedy[0][row0 + lane] = static_cast<uint8_t>(argmax_first(q, R.out_dim));
-          if constexpr (OPP == 2) {
-            qnet_forward_ws(lds_net, tile, row0, true, q);
+          if constexpr (OPP >= 2) {  // the opponent's view state[5:] + state[:5] (main.py:199)
+            qnet_forward_ws(OPP == 3 ? lds_net2 : lds_net, tile, row0, true, q);
             greedy[1][row0 + lane] = static_cast<uint8_t>(argmax_first(q, R.out_dim));
           }
         }
@@ -1652,7 +1663,7 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
 #pragma unroll
       for (int j = 0; j < kIlp; ++j) {
         greedy1[j] = greedy[0][local0 + 64 * j + lane];
-        greedy2[j] = OPP == 2 ? greedy[1][local0 + 64 * j + lane] : 0;
+        greedy2[j] = OPP >= 2 ? greedy[1][local0 + 64 * j + lane] : 0;
       }
       bool won[kIlp];
       // wave-uniform branch: each group's envs stay in named registers
@@ -2678,7 +2689,7 @@ int mg_rollout_qnet(const mg_params* params, const mg_state* state, const mg_tra
                     const mg_stats* stats, int64_t n, int64_t env_offset, uint64_t seed,
                     uint64_t first_step, int32_t num_steps, const void* net, int32_t out_dim,
                     uint64_t greedy_threshold, int32_t opponent_mode,
-                    uint64_t opp_greedy_threshold, uint32_t flags, void* stream) {
+                    uint64_t opp_greedy_threshold, const void* opp_net, uint32_t flags, void* stream) {
   mg_outputs none{};
   if (int e = check_common(params, state, &none, n)) return e;
   if (!traj) return fail(hipErrorInvalidValue, "%s", "traj is NULL (pass a zeroed mg_traj)");
@@ -2686,8 +2697,15 @@ int mg_rollout_qnet(const mg_params* params, const mg_state* state, const mg_tra
     return fail(hipErrorInvalidValue, "%s", "net must be a 16-byte aligned packed Q-net");
   if (num_steps < 0 || out_dim < 1 || out_dim > 8)
     return fail(hipErrorInvalidValue, "%s", "need num_steps >= 0 and 1 <= out_dim <= 8");
-  if (opponent_mode < 0 || opponent_mode > 2)
-    return fail(hipErrorInvalidValue, "%s", "opponent_mode must be 0 (None), 1 (uniform) or 2 (same net)");
+  if (opponent_mode < 0 || opponent_mode > 3)
+    return fail(hipErrorInvalidValue, "%s",
+                "opponent_mode must be 0 (None), 1 (uniform), 2 (same net) or 3 (opp_net)");
+  if (opponent_mode == 3 && (!opp_net || (reinterpret_cast<uintptr_t>(opp_net) & 15)))
+    return fail(hipErrorInvalidValue, "%s", "opponent_mode 3 needs opp_net, a 16-byte aligned packed Q-net");
+#if !MG_QNET_WS
+  if (opponent_mode == 3)
+    return fail(hipErrorInvalidValue, "%s", "opponent_mode 3 needs the specialised-wave kernel (MG_QNET_WS)");
+#endif
   if ((traj->obs && (reinterpret_cast<uintptr_t>(traj->obs) & 15)) ||
       (traj->final_obs && (reinterpret_cast<uintptr_t>(traj->final_obs) & 7)) ||
       (traj->rew && (reinterpret_cast<uintptr_t>(traj->rew) & 7)) ||
@@ -2700,6 +2718,7 @@ int mg_rollout_qnet(const mg_params* params, const mg_state* state, const mg_tra
   R.T = *traj;
   if (stats) R.St = *stats;
   R.net = static_cast<const uint8_t*>(net);
+  R.opp_net = static_cast<const uint8_t*>(opp_net);
   R.seed = seed;
   R.first_step = first_step;
   R.greedy_thr = greedy_threshold;
@@ -2716,7 +2735,8 @@ int mg_rollout_qnet(const mg_params* params, const mg_state* state, const mg_tra
 #if MG_QNET_WS
 #define MG_QKERNEL qnet_rollout_ws_kernel
   const unsigned threads = kQWsThreads;
-  blocks = static_cast<unsigned>((n + kQWsEnvs - 1) / kQWsEnvs);
+  const int64_t block_envs = opponent_mode == 3 ? qws_envs<3>() : qws_envs<0>();
+  blocks = static_cast<unsigned>((n + block_envs - 1) / block_envs);
 #else
 #define MG_QKERNEL qnet_rollout_kernel
   const unsigned threads = kQBlock;
@@ -2732,8 +2752,12 @@ int mg_rollout_qnet(const mg_params* params, const mg_state* state, const mg_tra
     MG_LAUNCH_Q(0);
   else if (opponent_mode == 1)
     MG_LAUNCH_Q(1);
-  else
+  else if (opponent_mode == 2)
     MG_LAUNCH_Q(2);
+#if MG_QNET_WS
+  else
+    MG_LAUNCH_Q(3);
+#endif
 #undef MG_LAUNCH_Q
 #undef MG_QKERNEL
   return finish_launch("mg_rollout_qnet");

@@ -15,7 +15,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libmerging_hip.so"
 LIB_PATH = os.environ.get("MERGING_HIP_LIB", os.path.join(_HERE, LIB_NAME))
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 OBS_DIM = 10
 NUM_ACTIONS = 5
@@ -112,7 +112,7 @@ def _load():
     lib.mg_qnet_forward.argtypes = [_P, _P, _c.c_int32, _c.c_int32, _P, _c.c_int64, _P]
     lib.mg_rollout_qnet.argtypes = [PP, SP, _c.POINTER(Traj), STP, _c.c_int64, _c.c_int64, _c.c_uint64,
                                     _c.c_uint64, _c.c_int32, _P, _c.c_int32, _c.c_uint64, _c.c_int32,
-                                    _c.c_uint64, _c.c_uint32, _P]
+                                    _c.c_uint64, _P, _c.c_uint32, _P]
     lib.mg_rollout_hdqn.argtypes = [PP, SP, _c.POINTER(Traj), _c.POINTER(HdqnTraj), STP, _P, _P, _c.c_int64,
                                     _c.c_int64, _c.c_uint64, _c.c_uint64, _c.c_int32, _P, _c.c_int32, _P,
                                     _c.c_int32, _c.c_uint64, _c.c_int32, _P, _P, _c.c_int64, _c.c_uint32, _P]

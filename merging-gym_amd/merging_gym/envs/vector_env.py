@@ -289,13 +289,21 @@ class MergeVecEnv:
                      final_observation: bool = True, won_mask: bool = True):
         """`num_steps` steps with the reference's epsilon-greedy DQN policy (main.py:99-112)
         computed on the device (bf16 MFMA) and fused with the env step, one launch.
-        opponent: "none" (L0), "uniform", or "self" (the same net on the swapped observation,
-        main.py:199). Returns the same [T, N, ...] dict as rollout_random."""
+        opponent: "none" (L0), "uniform", "self" (the same net on the swapped observation,
+        main.py:199, Strategy_OP "selfplay"), or another QNet with the same out_dim (main.py's
+        default Strategy_OP "L1", :161-168: a separately trained DQN acting epsilon-greedily on
+        the swapped observation). Returns the same [T, N, ...] dict as rollout_random."""
         from ..policy import greedy_threshold
 
         torch, nat = self._torch, self._nat
         T, n = int(num_steps), self.num_envs
-        mode = {"none": 0, "uniform": 1, "self": 2}[opponent]
+        opp_net = None
+        if isinstance(opponent, str):
+            mode = {"none": 0, "uniform": 1, "self": 2}[opponent]
+        else:  # a QNet: the opponent's own DQN
+            mode, opp_net = 3, opponent
+            if opp_net.in_dim != _OBS_DIM or opp_net.out_dim != qnet.out_dim:
+                raise ValueError("the opponent's net needs in_dim 10 and the ego net's out_dim")
         if qnet.in_dim != _OBS_DIM:
             raise ValueError("the fused rollout feeds the 10-value observation: the net needs in_dim 10")
         k0 = self._step_idx if first_step is None else int(first_step)
@@ -303,7 +311,8 @@ class MergeVecEnv:
         rc = nat.lib.mg_rollout_qnet(
             self._p_ref, self._s_ref, ctypes.byref(buf["_traj"]), self._st_ref, n, self.env_offset,
             seed & 0xFFFFFFFFFFFFFFFF, k0 & 0xFFFFFFFFFFFFFFFF, T, qnet.packed.data_ptr(), qnet.out_dim,
-            greedy_threshold(episilo), mode, greedy_threshold(opp_episilo), self._flags, self._stream())
+            greedy_threshold(episilo), mode, greedy_threshold(opp_episilo),
+            None if opp_net is None else opp_net.packed.data_ptr(), self._flags, self._stream())
         nat.check(rc, "mg_rollout_qnet")
         self._step_idx = k0 + T
         return buf["_result"]

@@ -39,8 +39,11 @@ int main() {
   mg_traj tj{};
   tj.flags = reinterpret_cast<uint8_t*>(static_cast<char*>(fake) + 2);
   bad += expect_error(mg_rollout_random(&p, &sf, &tj, nullptr, 16, 0, 1, 0, 4, 1, 0, nullptr), "misaligned flags");
-  bad += expect_error(mg_rollout_qnet(&p, &sf, &tj, nullptr, 16, 0, 1, 0, 4, fake, 9, 0, 0, 0, 0, nullptr),
+  bad += expect_error(mg_rollout_qnet(&p, &sf, &tj, nullptr, 16, 0, 1, 0, 4, fake, 9, 0, 0, 0, nullptr, 0, nullptr),
                       "out_dim 9");
+  mg_traj tq{};
+  bad += expect_error(mg_rollout_qnet(&p, &sf, &tq, nullptr, 16, 0, 1, 0, 4, fake, 5, 0, 3, 0, nullptr, 0, nullptr),
+                      "opponent net missing");
   bad += expect_error(mg_qnet_pack(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 10, 5, fake, nullptr),
                       "NULL weights");
   bad += expect_error(mg_qnet_forward(fake, static_cast<float*>(fake), 17, 0, static_cast<float*>(fake), 4, nullptr), "in_dim 17");

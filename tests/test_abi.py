@@ -156,8 +156,15 @@ def test_empty_batches_are_no_ops_without_gpu():
     assert lib.mg_step_random(P, ctypes.byref(st), None, None, out, None, 0, 0, 1, 0, 1, 0, None) == 0
     assert lib.mg_rollout_random(P, ctypes.byref(st), traj, None, 0, 0, 1, 0, 16, 1, 0, None) == 0
     assert lib.mg_rollout_random(P, ctypes.byref(st), traj, None, 64, 0, 1, 0, 0, 1, 0, None) == 0
-    assert lib.mg_rollout_qnet(P, ctypes.byref(st), traj, None, 0, 0, 1, 0, 16, fake, 5, 0, 0, 0, 0,
+    assert lib.mg_rollout_qnet(P, ctypes.byref(st), traj, None, 0, 0, 1, 0, 16, fake, 5, 0, 0, 0, None, 0,
                                None) == 0
+    # main.py's Strategy_OP "L1" opponent (its own net): opp_net required and 16-byte aligned
+    assert lib.mg_rollout_qnet(P, ctypes.byref(st), traj, None, 16, 0, 1, 0, 4, fake, 5, 0, 3, 0, None, 0,
+                               None) != 0 and b"opp_net" in lib.mg_last_error()
+    assert lib.mg_rollout_qnet(P, ctypes.byref(st), traj, None, 16, 0, 1, 0, 4, fake, 5, 0, 3, 0,
+                               ctypes.c_void_p((1 << 20) + 8), 0, None) != 0
+    assert lib.mg_rollout_qnet(P, ctypes.byref(st), traj, None, 16, 0, 1, 0, 4, fake, 5, 0, 4, 0, fake, 0,
+                               None) != 0 and b"opponent_mode" in lib.mg_last_error()
     assert lib.mg_reset(P, ctypes.byref(st), None, out, 0, None) == 0
     assert lib.mg_observe(P, ctypes.byref(st), out, 0, None) == 0
     assert lib.mg_qnet_forward(fake, fake, 10, 0, fake, 0, None) == 0

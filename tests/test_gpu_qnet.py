@@ -111,11 +111,13 @@ def test_qnet_forward_hdqn_nets(torch, coracle, in_dim, out_dim):
 
 
 @pytest.mark.parametrize("opponent,n", [("none", 4096), ("uniform", 4096), ("self", 4096),
-                                        ("none", 1000), ("self", 577)])
+                                        ("none", 1000), ("self", 577), ("other", 4096), ("other", 577)])
 def test_rollout_qnet_policy_and_transitions(torch, coracle, nets, opponent, n):
     """Every action is the epsilon-greedy choice (Philox draws exact, greedy = argmax of the
     bf16 reference except near-ties) and every transition equals the CPU oracle's. The odd
-    sizes leave partial waves / a partial block and unaligned trajectory rows."""
+    sizes leave partial waves / a partial block and unaligned trajectory rows. "other" is
+    main.py's default Strategy_OP "L1" (:161-168): the opponent is another shipped checkpoint
+    (l3) acting on the swapped observation, the kernel instance with both nets in LDS."""
     from merging_gym import MergeVecEnv
     from merging_gym.policy import QNet, greedy_threshold
 
@@ -132,7 +134,9 @@ def test_rollout_qnet_policy_and_transitions(torch, coracle, nets, opponent, n):
     envs["winner"] = env.winner.cpu().numpy()
     envs["time_stamp"] = np.cumsum(np.full(2700, 0.2))[np.maximum(envs["steps"] - 1, 0)] * (envs["steps"] > 0)
     obs_in = env.observe().cpu().numpy().copy()
-    traj = env.rollout_qnet(T, qnet, seed, opponent=opponent, first_step=k0)
+    opp_key = "l3" if opponent == "other" else "l1"
+    opp = QNet.from_state_dict(nets["l3"], device="cuda:0") if opponent == "other" else opponent
+    traj = env.rollout_qnet(T, qnet, seed, opponent=opp, first_step=k0)
     traj = {k: (v.cpu().numpy() if v is not None else None) for k, v in traj.items()}
     thr = greedy_threshold(0.7)
     for t in range(T):
@@ -149,7 +153,7 @@ def test_rollout_qnet_policy_and_transitions(torch, coracle, nets, opponent, n):
             if opponent == "uniform":
                 assert (traj["a2"][t] == rnd2).all()
             else:
-                q2 = mo.qnet_reference(nets["l1"], obs_in, bf16=True, swap=True)
+                q2 = mo.qnet_reference(nets[opp_key], obs_in, bf16=True, swap=True)
                 g2 = u[:, 2].astype(np.uint64) < thr
                 ok2 = (traj["a2"][t] == np.where(g2, q2.argmax(1), rnd2)) | (g2 & _near_tie(q2))
                 assert ok2.all(), t
@@ -227,7 +231,7 @@ def test_greedy_threshold_is_phi_of_episilo():
     assert greedy_threshold(50.0) == 2**32 and greedy_threshold(-50.0) == 0
 
 
-@pytest.mark.parametrize("opponent", ["none", "self"])
+@pytest.mark.parametrize("opponent", ["none", "self", "other"])
 def test_rollout_qnet_full_size(torch, coracle, nets, opponent):
     """BASELINE config 5 at its own size: 2^20 envs x 16 steps in one launch (the kernel's
     1,024-env blocks, both pipelined groups and the [T, N, .] trajectory indexing at full size).
@@ -255,7 +259,9 @@ def test_rollout_qnet_full_size(torch, coracle, nets, opponent):
     obs_in = env.observe()[idx].cpu().numpy().copy()
     ret_sum0, counts0 = env.ret_sum[idx].cpu().numpy(), env.counts[idx].cpu().numpy().astype(np.uint32)
 
-    traj = env.rollout_qnet(T, qnet, seed, opponent=opponent, first_step=k0)
+    opp_key = "l3" if opponent == "other" else "l1"
+    opp = QNet.from_state_dict(nets["l3"], device="cuda:0") if opponent == "other" else opponent
+    traj = env.rollout_qnet(T, qnet, seed, opponent=opp, first_step=k0)
     # whole batch
     a1, a2 = traj["a1"], traj["a2"]
     assert int(a1.min()) >= 0 and int(a1.max()) <= 4
@@ -281,8 +287,8 @@ def test_rollout_qnet_full_size(torch, coracle, nets, opponent):
         ok1 = (sub["a1"][t] == exp1) | (greedy & _near_tie(q))
         assert ok1.all(), (t, idx_np[~ok1][:5])
         rnd2 = (u[:, 3].astype(np.uint64) * 5) >> 32
-        if opponent == "self":
-            q2 = mo.qnet_reference(nets["l1"], obs_in, bf16=True, swap=True)
+        if opponent in ("self", "other"):
+            q2 = mo.qnet_reference(nets[opp_key], obs_in, bf16=True, swap=True)
             g2 = u[:, 2].astype(np.uint64) < thr
             ok2 = (sub["a2"][t] == np.where(g2, q2.argmax(1), rnd2)) | (g2 & _near_tie(q2))
             assert ok2.all(), t

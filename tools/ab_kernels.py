@@ -40,7 +40,7 @@ def bind(path):
     lib.mg_qnet_pack.argtypes = [P] * 6 + [ctypes.c_int32, ctypes.c_int32, P, P]
     lib.mg_rollout_qnet.argtypes = [PP, SP, ctypes.POINTER(nat.Traj), STP, ctypes.c_int64, ctypes.c_int64,
                                     ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int32, P, ctypes.c_int32,
-                                    ctypes.c_uint64, ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint32, P]
+                                    ctypes.c_uint64, ctypes.c_int32, ctypes.c_uint64, P, ctypes.c_uint32, P]
     return lib
 
 
@@ -105,7 +105,7 @@ class Bed:
         thr = 3255688812  # round(Phi(0.7) * 2^32)
         rc = self.lib.mg_rollout_qnet(ctypes.byref(self.params), ctypes.byref(self.state), ctypes.byref(self.traj),
                                       ctypes.byref(self.stats), self.n, 0, 5, self.k, self.T, self.net.data_ptr(), 5,
-                                      thr, opp, thr, 1, torch.cuda.current_stream().cuda_stream)
+                                      thr, opp, thr, None, 1, torch.cuda.current_stream().cuda_stream)
         assert rc == 0
         self.k += self.T
 
