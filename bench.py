@@ -636,6 +636,13 @@ def main():
                     completed_in_timed_window_rank0=completed_in_window,
                     counted_since="start of the timed window (statistics cleared after the warm-up)")
 
+    # the step kernel past the Infinity Cache first, while device memory is unfragmented: allocated
+    # after the Q-net and h-DQN legs (gigabytes of trajectory buffers and rings, some freed) the
+    # same 2^22-env batch measured 2.2x slower, with no clock effect (tools/throttle_probe.py)
+    size2 = None
+    if world == 1 and args.size2_envs > 0 and args.size2_envs != E:
+        size2 = size2_leg(args, torch)
+
     rollout = None
     if args.rollout_steps > 0:
         rollout = rollout_leg(env, args, world, dist, torch)
@@ -650,10 +657,6 @@ def main():
     hdqn = None
     if args.qnet_launches > 0 and args.rollout_steps > 0:
         hdqn = hdqn_leg(env, args, world, dist, torch)
-
-    size2 = None
-    if world == 1 and args.size2_envs > 0 and args.size2_envs != E:
-        size2 = size2_leg(args, torch)
 
     total_env_steps = world * E * args.steps
     value = total_env_steps / elapsed
