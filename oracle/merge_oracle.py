@@ -366,7 +366,7 @@ def step_with_won(coracle, envs, a1, a2=None):
 
 
 def replay_store(memory, counter, obs_first, obs, a1, rew, done=None, final_obs=None, won=None,
-                 skip_ego_won=True, goal=None, next_goal=None, reward=None):
+                 skip_ego_won=True, goal=None, next_goal=None, reward=None, meta_goal=None):
     """DQN.store_transition (scripts/main.py:115-119) applied to T steps of n envs in (t, i)
     order -- the order of stepping envs 0..n-1 each step and storing in turn -- with main.py:209's
     `if env.winner is not 1` filter. Row = np.hstack((s, [a, r], s')) with s the observation
@@ -377,7 +377,13 @@ def replay_store(memory, counter, obs_first, obs, a1, rew, done=None, final_obs=
 
     goal / next_goal [T, n]: hdqn.py's lower-level rows (HDQN.store_transition :180-184 on
     goal_state = [goal] + state, :291 and :304): [goal, s, a, r, next_goal, s'], 24 floats.
-    reward [T, n] replaces the ego's env reward as r (hdqn.py:314's intrinsic reward)."""
+    reward [T, n] replaces the ego's env reward as r (hdqn.py:314's intrinsic reward).
+
+    meta_goal [T, n]: Goal_DQN's memory instead (Goal_DQN.store_transition, hdqn.py:97-101, called
+    at :325 once the inner loop broke, with state = next_state after :320 and goal the :303
+    choice): rows [s', meta_goal, reward, s'] (22 floats) for the transitions whose `won` bit is
+    clear -- here the mask marks the steps that did NOT end an inner loop -- and reward the
+    extrinsic reward summed since that loop began (:286, :313)."""
     a1 = np.asarray(a1)
     T, n = a1.shape
     cap = memory.shape[0]
@@ -388,12 +394,14 @@ def replay_store(memory, counter, obs_first, obs, a1, rew, done=None, final_obs=
         d = np.asarray(done, bool).reshape(T, n)
         nxt[d] = np.asarray(final_obs, np.float32).reshape(T, n, -1)[d]
     keep = np.ones((T, n), bool)
-    if skip_ego_won and won is not None:
+    if (skip_ego_won or meta_goal is not None) and won is not None:
         keep = ~np.asarray(won, bool).reshape(T, n)
     r = (np.asarray(rew, np.float32).reshape(T, n, 2)[..., :1] if reward is None
          else np.asarray(reward, np.float32).reshape(T, n, 1))
     a = a1[..., None].astype(np.float32)
-    if goal is None:
+    if meta_goal is not None:  # Goal_DQN rows: [s', goal, extrinsic reward, s'] (:325)
+        cols = [nxt, np.asarray(meta_goal, np.float32).reshape(T, n, 1), r, nxt]
+    elif goal is None:
         cols = [prev, a, r, nxt]
     else:  # hdqn.py:180-184 on goal_state = [goal] + state (:291, :304)
         g = np.asarray(goal, np.float32).reshape(T, n, 1)

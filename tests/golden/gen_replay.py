@@ -61,11 +61,16 @@ def run_hdqn(hdqn_mod, env, steps, opp_random, seed):
     next_goal_state (:304), intrinsic reward 1.0 if goal == goal_status(state) (:314, the
     reference's own goal_status), lower.store_transition (:316), state = next_state (:320), and a
     fresh goal at :283 after the :322 break or an episode end. Goals and actions come from a
-    seeded numpy generator instead of the meta-controller / choose_action."""
+    seeded numpy generator instead of the meta-controller / choose_action. Goal_DQN's own memory
+    rides along: extrinsic_reward += reward each step (:286, :313) and, after each :322 break or
+    episode end, upper.store_transition(state, goal, extrinsic_reward, next_state) (:325, with
+    state = next_state already and goal the :303 choice) into its (200, 22) memory (:75)."""
     import torch
 
     rng = np.random.default_rng(seed)
     lower = hdqn_mod.HDQN()
+    upper = hdqn_mod.Goal_DQN()
+    extrinsic = 0
     a1s = rng.integers(0, 5, steps).astype(np.int8)
     a2s = rng.integers(0, 5, steps).astype(np.int8) if opp_random else np.full(steps, -1, np.int8)
     goal_s = np.zeros(steps, np.float32)
@@ -79,6 +84,7 @@ def run_hdqn(hdqn_mod, env, steps, opp_random, seed):
             goal_state = torch.unsqueeze(torch.FloatTensor([goal] + state), dim=0)  # :291
             a2 = None if a2s[k] < 0 else int(a2s[k])
             next_state, rewards, done, info = env.step(int(a1s[k]), a2)
+            extrinsic += rewards[0]  # :311-313
             new_goal = int(rng.integers(0, 3))  # :303 upper.choose_goal(next_state)
             next_goal_state = torch.unsqueeze(torch.FloatTensor([new_goal] + next_state), dim=0)  # :304
             r_int = 1.0 if new_goal == hdqn_mod.goal_status(state) else 0.0  # :314
@@ -86,6 +92,9 @@ def run_hdqn(hdqn_mod, env, steps, opp_random, seed):
             goal_s[k], goal_s2[k], intrinsic[k], done_f[k] = goal, new_goal, r_int, bool(done)
             state = next_state  # :320
             goal = new_goal
+            if done or goal == hdqn_mod.goal_status(state):  # :322 break -> :325, then :286
+                upper.store_transition(state, goal, extrinsic, next_state)
+                extrinsic = 0
             if done:  # episode over: reset, then :283 picks a goal
                 state = env.reset()
                 goal = int(rng.integers(0, 3))
@@ -93,7 +102,9 @@ def run_hdqn(hdqn_mod, env, steps, opp_random, seed):
                 goal = int(rng.integers(0, 3))
     return {"a1": a1s, "a2": a2s, "done": done_f, "goal": goal_s, "next_goal": goal_s2,
             "intrinsic": intrinsic, "memory": np.asarray(lower.memory, np.float64),
-            "counter": np.int64(lower.memory_counter), "capacity": np.int64(lower.memory.shape[0])}
+            "counter": np.int64(lower.memory_counter), "capacity": np.int64(lower.memory.shape[0]),
+            "meta_memory": np.asarray(upper.memory, np.float64), "meta_counter": np.int64(upper.memory_counter),
+            "meta_capacity": np.int64(upper.memory.shape[0])}
 
 
 def main():

@@ -129,3 +129,53 @@ def test_goal_status_matches_reference_intrinsic_rewards(coracle, replay_golden,
     scalar = np.array([goal_status([float(x) for x in row]) for row in prev])
     np.testing.assert_array_equal(batch, scalar)
     np.testing.assert_array_equal((g["next_goal"] == batch).astype(np.float32), g["intrinsic"])
+
+
+def meta_rows_inputs(rew1, done, next_goal, status_next):
+    """Goal_DQN's memory inputs of one env's run (hdqn.py:286, :311-313, :322, :325): the
+    no-break mask (a step that did not end the inner loop stores nothing) and the extrinsic
+    reward summed in fp64 since the inner loop began, as stored at a break."""
+    brk = np.asarray(done, bool) | (np.asarray(next_goal) == np.asarray(status_next))
+    ext = np.zeros(len(brk))
+    acc = 0.0
+    for k in range(len(brk)):
+        acc += float(rew1[k])
+        ext[k] = acc
+        if brk[k]:
+            acc = 0.0
+    return ~brk, ext
+
+
+@pytest.mark.parametrize("tag", ["HL0", "HRR"])
+def test_oracle_meta_store_reproduces_goal_dqn_memory(coracle, replay_golden, tag):
+    """Goal_DQN's memory (Goal_DQN.store_transition :97-101 at :325 after each inner-loop break or
+    episode end; rows [state, goal, extrinsic_reward, next_state] with state = next_state and the
+    :303 goal): the reference's own run (gen_replay.run_hdqn) equals the oracle's meta rows fed by
+    the oracle's own steps (fp64 rewards summed as the reference sums them) bit for bit."""
+    g = {k[len(tag) + 1:]: replay_golden[k] for k in replay_golden.files if k.startswith(tag + "_")}
+    T = len(g["a1"])
+    envs = coracle.new_envs(1)
+    obs0 = coracle.reset(envs).astype(np.float32)
+    obs = np.empty((T, 1, 10), np.float32)
+    fobs = np.full((T, 1, 10), np.nan, np.float32)
+    rew = np.empty((T, 1, 2), np.float32)
+    done = np.empty((T, 1), bool)
+    rew1 = np.empty(T)
+    nxt64 = np.empty((T, 10))
+    for t in range(T):
+        o, r, d, _, _, fo, err = coracle.step(envs, g["a1"][t:t + 1], None if g["a2"][t] < 0 else g["a2"][t:t + 1],
+                                              autoreset=True, final_obs=True)
+        assert err == 0
+        obs[t], rew[t], done[t] = o.astype(np.float32), r.astype(np.float32), bool(d[0])
+        fobs[t] = fo.astype(np.float32)
+        rew1[t] = r[0, 0]
+        nxt64[t] = fo[0] if d[0] else o[0]
+    np.testing.assert_array_equal(done[:, 0], g["done"])
+    status = np.where(nxt64[:, 0] < -0.5 * nxt64[:, 9], 0, np.where(nxt64[:, 0] < 0.5 * nxt64[:, 9], 1, 2))
+    nobrk, ext = meta_rows_inputs(rew1, done[:, 0], g["next_goal"], status)
+    cap = int(g["meta_capacity"])
+    mem = np.zeros((cap, 22), np.float32)
+    counter = mo.replay_store(mem, 0, obs0, obs, g["a1"][:, None], rew, done, fobs, nobrk[:, None],
+                              reward=ext[:, None], meta_goal=g["next_goal"][:, None])
+    assert counter == int(g["meta_counter"]) > cap  # the ring wrapped
+    np.testing.assert_array_equal(mem, g["meta_memory"].astype(np.float32))
