@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 14
+#define MG_ABI_VERSION 15
 #define MG_OBS_DIM 10   /* merging_env.py:75 observation_shape = (10) */
 #define MG_NUM_ACTIONS 5 /* merging_env.py:101-102 action_dict / Discrete(5) */
 #define MG_ACTION_NONE (-1) /* action2=None: the constant-speed "L0" opponent, merging_env.py:152 */
@@ -193,6 +193,13 @@ typedef struct mg_transitions {
   const float* reward;      /* [T, n] r of the row, or NULL (r = rew[t, i, 0]) */
   const uint8_t* flags;     /* [T, n, 4] interleaved (a1, a2, done, coll) of mg_traj.flags, or NULL:
                                then a1 = flags[4 row], done = flags[4 row + 2] */
+  const float* meta_goal;   /* (ABI 15) [T, n] or NULL: Goal_DQN's memory instead (hdqn.py:97-101,
+                               stored at :325 once an inner loop broke): row [s', meta_goal, reward,
+                               s'] with s' the next state (terminal where done) for the transitions
+                               whose won_mask bit is CLEAR -- the mask then marks the steps that did
+                               not end an inner loop (mg_hdqn_traj.no_break) and is required, as is
+                               reward (the extrinsic reward, mg_hdqn_traj.ext_reward); 22-float rows,
+                               goal NULL, skip_ego_won ignored */
 } mg_transitions;
 
 /* Completed-episode statistics of one env, updated only when it finishes (MG_AUTORESET):
@@ -300,6 +307,12 @@ typedef struct mg_hdqn_traj {
   float* reward;     /* 1.0 if next_goal == goal_status(state) else 0.0 (:314) */
   float* goal_op;    /* (optional, opponent_mode 2) the self-play opponent's goal of step t, the
                         goal of its goal state [goal_op] + swapped state (:285, :299) */
+  float* ext_reward; /* (optional, ABI 15) extrinsic reward summed since the inner loop began,
+                        through step t (:286, :311-313): Goal_DQN's row reward at a break;
+                        needs ext_acc */
+  uint64_t* no_break; /* (optional, ABI 15) [T, ceil(n/64)] bit i of word t ceil(n/64) + i/64 set
+                        where step t did not end the inner loop (:322): the rows Goal_DQN does not
+                        store (mg_transitions.meta_goal) */
 } mg_hdqn_traj;
 
 /* num_steps steps of hdqn.py's inner loop in ONE launch (opponent L0 or uniform random): per env
@@ -324,7 +337,8 @@ typedef struct mg_hdqn_traj {
  * ((env_offset + i) ^ 2^62, first_step + t), x explore and y action of step t, z explore and
  * w goal of a fresh opponent goal at step t + 1 (the launch's first at step first_step - 1).
  * goal_op [n] int8 (required for mode 2, else ignored) holds each env's opponent goal across
- * launches like goal.
+ * launches like goal. ext_acc [n] double (required with htraj->ext_reward or no_break, ABI 15)
+ * holds each env's extrinsic reward since its inner loop began, across launches (0 at a break).
  * ring_rows (optional, 16-byte aligned [ring_capacity, 24] fp32, with ring_counter: one device
  * uint64): the launch also appends every transition to hdqn.py's lower-level memory
  * (HDQN.store_transition, :316, which stores them all) -- row [goal, s, a, r, next_goal, s'] of
@@ -332,7 +346,8 @@ typedef struct mg_hdqn_traj {
  * skip_ego_won = 0 writes from this launch's outputs (only the newest ring_capacity rows when
  * more are appended), then counter += T n. No scan is needed since every row is kept. */
 int mg_rollout_hdqn(const mg_params* params, const mg_state* state, const mg_traj* traj,
-                    const mg_hdqn_traj* htraj, const mg_stats* stats, int8_t* goal, int8_t* goal_op, int64_t n,
+                    const mg_hdqn_traj* htraj, const mg_stats* stats, int8_t* goal, int8_t* goal_op,
+                    double* ext_acc, int64_t n,
                     int64_t env_offset, uint64_t seed, uint64_t first_step, int32_t num_steps,
                     const void* meta_net, int32_t num_goals, const void* lower_net, int32_t reset_goal,
                     uint64_t greedy_threshold, int32_t opponent_mode, float* ring_rows,

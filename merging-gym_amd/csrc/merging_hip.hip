@@ -1734,6 +1734,7 @@ struct HRollout {
   mg_stats St;
   int8_t* goal;     // [n] in / out
   int8_t* goal_op;  // [n] in / out, the self-play opponent's goal (OPP 2)
+  double* ext_acc;  // [n] in / out, extrinsic reward since the inner loop began (Goal_DQN rows)
   const uint8_t* meta;
   const uint8_t* lower;
   uint64_t seed;
@@ -1914,6 +1915,24 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
   // its next goal: s, s' (terminal where done), goal, action
   float ps[2][kObs], ps2[2][kObs];
   int pgoal[2], pact[2];
+  // Goal_DQN's memory (hdqn.py:286, :311-313, :322, :325): the extrinsic reward since each env's
+  // inner loop began, and at each step whether that loop ended (known once Q(X, t + 1) has chosen
+  // the step's next goal, so it is emitted together with the ring row of the step)
+  const bool outer = R.H.ext_reward != nullptr || R.H.no_break != nullptr;
+  double acc[2] = {0.0, 0.0};
+  auto finish_outer = [&](int g, int t, double& ac) __attribute__((always_inline)) {
+    const int j = g * kHHalf + 64 * ew + lane;
+    const int64_t i = base + j;
+    const int64_t wbase = base + g * kHHalf + 64 * ew;
+    const bool lv = i < R.n;
+    const bool brk = b_done[j] != 0 || b_g2[j] == b_st_new[j];
+    if (R.H.ext_reward && lv) st_out(R.H.ext_reward + static_cast<int64_t>(t) * R.n + i, static_cast<float>(ac));
+    if (R.H.no_break) {
+      const uint64_t m = __ballot(lv && !brk);
+      if (lane == 0 && wbase < R.n) st_out(R.H.no_break + static_cast<int64_t>(t) * ((R.n + 63) >> 6) + (wbase >> 6), m);
+    }
+    if (brk) ac = 0.0;  // :286 extrinsic_reward = 0 for the next outer iteration
+  };
   const bool ring = R.ring != nullptr;
   const uint64_t c0 = ring ? *R.ring_counter : 0;
   const int64_t total = static_cast<int64_t>(T) * R.n;
@@ -1973,6 +1992,7 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
     const uint4 fb = philox_env_step(gi ^ (uint64_t{1} << 63), R.first_step - 1, R.seed);
     b_df[j] = draw_byte(fb.x, fb.y, R.greedy_thr, R.num_goals);
     b_goal[j] = live[g] ? static_cast<uint8_t>(R.goal[i]) : 0;
+    if (outer && live[g]) acc[g] = R.ext_acc[i];
     if constexpr (OPP == 2) {
       const uint4 fc = philox_env_step(gi ^ (uint64_t{1} << 62), R.first_step - 1, R.seed);
       b_dfo[j] = draw_byte(fc.z, fc.w, R.greedy_thr, R.num_goals);
@@ -2002,9 +2022,15 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
           write_row(0, t - 1, ps[0], ps2[0], pgoal[0], pact[0]);
         else
           write_row(1, t - 1, ps[1], ps2[1], pgoal[1], pact[1]);
+        if (outer) {
+          if (g == 0)
+            finish_outer(0, t - 1, acc[0]);
+          else
+            finish_outer(1, t - 1, acc[1]);
+        }
       }
       auto step = [&](Env& ev, StepOut& rv, bool lv, float (&s0)[kObs], float (&s1)[kObs], int& pg,
-                      int& pa) __attribute__((always_inline)) {
+                      int& pa, double& ac) __attribute__((always_inline)) {
         b_st_old[j] = static_cast<uint8_t>(goal_status(rv.o));  // status of the state acted on
         if (ring) {
 #pragma unroll
@@ -2013,6 +2039,7 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
           pa = a1;
         }
         env_step(R.P, ev, a1, a2, rv);
+        ac += rv.r1;  // :311-313 extrinsic_reward += reward
         if (ring) {
 #pragma unroll
           for (int q = 0; q < kObs; ++q) s1[q] = static_cast<float>(rv.o[q]);  // terminal where done
@@ -2044,15 +2071,22 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
                        wrem <= 0 ? 0 : (wrem < 64 ? static_cast<int>(wrem) : 64));
       };
       if (g == 0)
-        step(e[0], r[0], live[0], ps[0], ps2[0], pgoal[0], pact[0]);
+        step(e[0], r[0], live[0], ps[0], ps2[0], pgoal[0], pact[0], acc[0]);
       else
-        step(e[1], r[1], live[1], ps[1], ps2[1], pgoal[1], pact[1]);
+        step(e[1], r[1], live[1], ps[1], ps2[1], pgoal[1], pact[1], acc[1]);
     }
     __syncthreads();
   }
   // both groups' last rows: Q(A,T) and Q(B,T) chose their next goals in the last two phases
   write_row(0, T - 1, ps[0], ps2[0], pgoal[0], pact[0]);
   write_row(1, T - 1, ps[1], ps2[1], pgoal[1], pact[1]);
+  if (outer) {
+    finish_outer(0, T - 1, acc[0]);
+    finish_outer(1, T - 1, acc[1]);
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+      if (live[g]) R.ext_acc[base + g * kHHalf + 64 * ew + lane] = acc[g];
+  }
 #pragma unroll
   for (int g = 0; g < 2; ++g)
     if (live[g]) store_env(R.S, base + g * kHHalf + 64 * ew + lane, e[g]);
@@ -2263,10 +2297,15 @@ __device__ __forceinline__ void load_row10(const float* src, float (&v)[kObs]) {
   }
 }
 
-template <bool GOAL>
+// KIND 0: main.py's DQN rows [s, a, r, s']; 1: hdqn.py's lower-level goal rows
+// [goal, s, a, r, next_goal, s']; 2: Goal_DQN's rows [s', meta_goal, r, s'] (hdqn.py:97-101 at
+// :325, where state is already next_state).
+template <int KIND>
 __global__ __launch_bounds__(kRBlock) void replay_write_kernel(const ReplayIn R, const ReplayScratch S,
                                                                const uint64_t* counter, float* rows,
                                                                int64_t cap) {
+  constexpr bool GOAL = KIND == 1;
+  constexpr bool META = KIND == 2;
   constexpr int kRow = GOAL ? kRowGoal : 2 * kObs + 2;  // floats per row
   constexpr int kS = GOAL ? 1 : 0;                      // column of s[0]
   constexpr int kS2 = kS + kObs + 2 + kS;               // column of s'[0]
@@ -2313,10 +2352,13 @@ __global__ __launch_bounds__(kRBlock) void replay_write_kernel(const ReplayIn R,
           for (int k = 0; k < kObs; ++k) s2[k] = o[k];
 #pragma unroll
         for (int k = 0; k < kObs; ++k) {
-          d[kS + k] = s[k];
+          d[kS + k] = META ? s2[k] : s[k];
           d[kS2 + k] = s2[k];
         }
-        d[kS + kObs] = static_cast<float>(R.X.flags ? static_cast<int8_t>(R.X.flags[4 * row]) : R.X.a1[row]);
+        if constexpr (META)
+          d[kS + kObs] = R.X.meta_goal[row];
+        else
+          d[kS + kObs] = static_cast<float>(R.X.flags ? static_cast<int8_t>(R.X.flags[4 * row]) : R.X.a1[row]);
         d[kS + kObs + 1] = R.X.reward ? R.X.reward[row] : R.X.rew[2 * row];
         if constexpr (GOAL) {
           d[0] = R.X.goal[row];
@@ -2764,8 +2806,9 @@ int mg_rollout_qnet(const mg_params* params, const mg_state* state, const mg_tra
 }
 
 int mg_rollout_hdqn(const mg_params* params, const mg_state* state, const mg_traj* traj,
-                    const mg_hdqn_traj* htraj, const mg_stats* stats, int8_t* goal, int8_t* goal_op, int64_t n,
-                    int64_t env_offset, uint64_t seed, uint64_t first_step, int32_t num_steps,
+                    const mg_hdqn_traj* htraj, const mg_stats* stats, int8_t* goal, int8_t* goal_op,
+                    double* ext_acc, int64_t n, int64_t env_offset, uint64_t seed, uint64_t first_step,
+                    int32_t num_steps,
                     const void* meta_net, int32_t num_goals, const void* lower_net, int32_t reset_goal,
                     uint64_t greedy_threshold, int32_t opponent_mode, float* ring_rows,
                     uint64_t* ring_counter, int64_t ring_capacity, uint32_t flags, void* stream) {
@@ -2783,6 +2826,10 @@ int mg_rollout_hdqn(const mg_params* params, const mg_state* state, const mg_tra
     return fail(hipErrorInvalidValue, "%s", "opponent_mode must be 0 (None), 1 (uniform) or 2 (self-play)");
   if (opponent_mode == 2 && !goal_op)
     return fail(hipErrorInvalidValue, "%s", "opponent_mode 2 needs goal_op (an [n] int8 device array)");
+  if (htraj && (htraj->ext_reward || htraj->no_break) && !ext_acc)
+    return fail(hipErrorInvalidValue, "%s", "ext_reward / no_break need ext_acc (an [n] double device array)");
+  if (htraj && htraj->no_break && (reinterpret_cast<uintptr_t>(htraj->no_break) & 7))
+    return fail(hipErrorInvalidValue, "%s", "no_break must be 8-byte aligned");
   if ((traj->obs && (reinterpret_cast<uintptr_t>(traj->obs) & 15)) ||
       (traj->final_obs && (reinterpret_cast<uintptr_t>(traj->final_obs) & 7)) ||
       (traj->rew && (reinterpret_cast<uintptr_t>(traj->rew) & 7)) ||
@@ -2797,6 +2844,7 @@ int mg_rollout_hdqn(const mg_params* params, const mg_state* state, const mg_tra
   if (stats) R.St = *stats;
   R.goal = goal;
   R.goal_op = goal_op;
+  R.ext_acc = ext_acc;
   R.meta = static_cast<const uint8_t*>(meta_net);
   R.lower = static_cast<const uint8_t*>(lower_net);
   R.seed = seed;
@@ -2840,6 +2888,9 @@ int mg_replay_store(float* rows, uint64_t* counter, int64_t capacity, int32_t ro
   if (row_floats != (tr->goal ? kRowGoal : kRow) || (tr->goal != nullptr) != (tr->next_goal != nullptr))
     return fail(hipErrorInvalidValue, "%s",
                 "mg_replay_store: row_floats must be 22, or 24 with both goal and next_goal set");
+  if (tr->meta_goal && (tr->goal || !tr->reward || !tr->won_mask))
+    return fail(hipErrorInvalidValue, "%s",
+                "mg_replay_store: meta_goal (Goal_DQN rows) needs reward and won_mask (no_break) and no goal");
   if (n < 0 || num_steps < 0) return fail(hipErrorInvalidValue, "%s", "mg_replay_store: n < 0 or num_steps < 0");
   if (n == 0 || num_steps == 0) return 0;
   if (!tr->obs_first || !tr->obs || !(tr->a1 || tr->flags) || !tr->rew)
@@ -2866,17 +2917,20 @@ int mg_replay_store(float* rows, uint64_t* counter, int64_t capacity, int32_t ro
   R.nbx = nbx;
   R.nb = nb;
   R.T = num_steps;
-  R.skip_won = skip_ego_won;
+  R.skip_won = tr->meta_goal ? 1 : skip_ego_won;  // Goal_DQN rows: keep the steps that broke
   const ReplayScratch S = replay_scratch(scratch, nb);
   hipStream_t st = static_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(replay_scan_kernel, dim3(static_cast<unsigned>(replay_groups(nb))), dim3(64), 0, st,
                      R, S);
   hipLaunchKernelGGL(replay_group_scan_kernel, dim3(1), dim3(64), 0, st, S, replay_groups(nb), counter);
   if (tr->goal)
-    hipLaunchKernelGGL(replay_write_kernel<true>, dim3(static_cast<unsigned>(nbx), chunks), dim3(kRBlock), 0,
+    hipLaunchKernelGGL(replay_write_kernel<1>, dim3(static_cast<unsigned>(nbx), chunks), dim3(kRBlock), 0,
+                       st, R, S, counter, rows, capacity);
+  else if (tr->meta_goal)
+    hipLaunchKernelGGL(replay_write_kernel<2>, dim3(static_cast<unsigned>(nbx), chunks), dim3(kRBlock), 0,
                        st, R, S, counter, rows, capacity);
   else
-    hipLaunchKernelGGL(replay_write_kernel<false>, dim3(static_cast<unsigned>(nbx), chunks), dim3(kRBlock), 0,
+    hipLaunchKernelGGL(replay_write_kernel<0>, dim3(static_cast<unsigned>(nbx), chunks), dim3(kRBlock), 0,
                        st, R, S, counter, rows, capacity);
   return finish_launch("mg_replay_store");
 }

@@ -15,7 +15,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libmerging_hip.so"
 LIB_PATH = os.environ.get("MERGING_HIP_LIB", os.path.join(_HERE, LIB_NAME))
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 OBS_DIM = 10
 NUM_ACTIONS = 5
@@ -60,11 +60,11 @@ class Traj(_c.Structure):
 
 class Transitions(_c.Structure):
     _fields_ = [(n, _P) for n in ("obs_first", "obs", "final_obs", "a1", "rew", "done", "won_mask", "goal",
-                                  "next_goal", "reward", "flags")]
+                                  "next_goal", "reward", "flags", "meta_goal")]
 
 
 class HdqnTraj(_c.Structure):
-    _fields_ = [(n, _P) for n in ("goal", "next_goal", "reward", "goal_op")]
+    _fields_ = [(n, _P) for n in ("goal", "next_goal", "reward", "goal_op", "ext_reward", "no_break")]
 
 
 class Stats(_c.Structure):
@@ -113,7 +113,7 @@ def _load():
     lib.mg_rollout_qnet.argtypes = [PP, SP, _c.POINTER(Traj), STP, _c.c_int64, _c.c_int64, _c.c_uint64,
                                     _c.c_uint64, _c.c_int32, _P, _c.c_int32, _c.c_uint64, _c.c_int32,
                                     _c.c_uint64, _P, _c.c_uint32, _P]
-    lib.mg_rollout_hdqn.argtypes = [PP, SP, _c.POINTER(Traj), _c.POINTER(HdqnTraj), STP, _P, _P, _c.c_int64,
+    lib.mg_rollout_hdqn.argtypes = [PP, SP, _c.POINTER(Traj), _c.POINTER(HdqnTraj), STP, _P, _P, _P, _c.c_int64,
                                     _c.c_int64, _c.c_uint64, _c.c_uint64, _c.c_int32, _P, _c.c_int32, _P,
                                     _c.c_int32, _c.c_uint64, _c.c_int32, _P, _P, _c.c_int64, _c.c_uint32, _P]
     lib.mg_time_next_launch.argtypes = [_P, _P]

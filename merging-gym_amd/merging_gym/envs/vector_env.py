@@ -319,7 +319,7 @@ class MergeVecEnv:
 
     def rollout_hdqn(self, num_steps: int, meta, lower, seed: int, opponent: str = "none",
                      episilo: float = 0.7, first_step=None, final_observation: bool = True,
-                     won_mask: bool = False, ring=None):
+                     won_mask: bool = False, ring=None, goal_memory: bool = False):
         """`num_steps` steps of hdqn.py's inner loop (scripts/hdqn.py:280-323) in one launch:
         Goal_DQN's meta-net (`meta`, a QNet 10 -> num_goals) picks each env's sub-goal on every
         next state, the lower-level Net (`lower`, a QNet 11 -> 5) acts epsilon-greedily on the
@@ -336,7 +336,11 @@ class MergeVecEnv:
         step). ring: a ReplayRing(goal=True) the same launch appends every
         transition to (hdqn.py:316 stores them all, so the kernel needs no scan): the rows
         store_rollout(obs0, traj, skip_ego_won=False, goal=..., next_goal=..., reward=...) would
-        write, without re-reading the trajectory."""
+        write, without re-reading the trajectory. goal_memory: also return "ext_reward" ([T, N]
+        fp32, the extrinsic reward summed since each env's inner loop began, :286, :311-313) and
+        "no_break" ([T, ceil(N/64)] int64 bits: the step did not end the inner loop, :322), from
+        which ReplayRing.store_meta appends Goal_DQN's rows (:325); the running sums persist in
+        `self.hdqn_ext` ([N] f64, checkpointed)."""
         from ..policy import greedy_threshold
 
         torch, nat = self._torch, self._nat
@@ -351,17 +355,24 @@ class MergeVecEnv:
         hb = getattr(self, "_hdqn_bufs", None)
         if hb is None or hb["goal"].shape[0] != T:
             hb = {k: torch.empty((T, n), dtype=torch.float32, device=self.device)
-                  for k in ("goal", "next_goal", "reward", "goal_op")}
+                  for k in ("goal", "next_goal", "reward", "goal_op", "ext_reward")}
+            hb["no_break"] = torch.empty((T, (n + 63) // 64), dtype=torch.int64, device=self.device)
             hb["_h"] = nat.HdqnTraj(*(hb[k].data_ptr() for k in ("goal", "next_goal", "reward", "goal_op")))
+            hb["_hm"] = nat.HdqnTraj(*(hb[k].data_ptr() for k in ("goal", "next_goal", "reward", "goal_op",
+                                                                   "ext_reward", "no_break")))
             self._hdqn_bufs = hb
+        if goal_memory and getattr(self, "hdqn_ext", None) is None:
+            self.hdqn_ext = torch.zeros(n, dtype=torch.float64, device=self.device)
         if getattr(self, "hdqn_goal", None) is None:
             self.hdqn_goal = torch.full((n,), -1, dtype=torch.int8, device=self.device)
         if mode == 2 and getattr(self, "hdqn_goal_op", None) is None:
             self.hdqn_goal_op = torch.full((n,), -1, dtype=torch.int8, device=self.device)
         gop = getattr(self, "hdqn_goal_op", None)
+        ext = getattr(self, "hdqn_ext", None) if goal_memory else None
         rc = nat.lib.mg_rollout_hdqn(
-            self._p_ref, self._s_ref, ctypes.byref(buf["_traj"]), ctypes.byref(hb["_h"]), self._st_ref,
-            self.hdqn_goal.data_ptr(), None if gop is None else gop.data_ptr(), n, self.env_offset, seed & 0xFFFFFFFFFFFFFFFF, k0 & 0xFFFFFFFFFFFFFFFF,
+            self._p_ref, self._s_ref, ctypes.byref(buf["_traj"]), ctypes.byref(hb["_hm" if goal_memory else "_h"]),
+            self._st_ref, self.hdqn_goal.data_ptr(), None if gop is None else gop.data_ptr(),
+            None if ext is None else ext.data_ptr(), n, self.env_offset, seed & 0xFFFFFFFFFFFFFFFF, k0 & 0xFFFFFFFFFFFFFFFF,
             T, meta.packed.data_ptr(), meta.out_dim, lower.packed.data_ptr(), meta.reset_argmax(),
             greedy_threshold(episilo), mode, None if ring is None else ring.memory.data_ptr(),
             None if ring is None else ring._counter.data_ptr(), 0 if ring is None else ring.capacity,
@@ -372,6 +383,8 @@ class MergeVecEnv:
         out.update(goal=hb["goal"], next_goal=hb["next_goal"], reward=hb["reward"])
         if mode == 2:
             out["goal_op"] = hb["goal_op"]
+        if goal_memory:
+            out.update(ext_reward=hb["ext_reward"], no_break=hb["no_break"])
         return out
 
     def observe(self):
@@ -446,6 +459,8 @@ class MergeVecEnv:
             sd["hdqn_goal"] = self.hdqn_goal.clone()  # rollout_hdqn's current goals
         if getattr(self, "hdqn_goal_op", None) is not None:
             sd["hdqn_goal_op"] = self.hdqn_goal_op.clone()  # and the self-play opponent's
+        if getattr(self, "hdqn_ext", None) is not None:
+            sd["hdqn_ext"] = self.hdqn_ext.clone()  # extrinsic reward of the running inner loops
         return sd
 
     def load_state_dict(self, sd):
@@ -465,6 +480,8 @@ class MergeVecEnv:
             self.hdqn_goal = self._torch.as_tensor(sd["hdqn_goal"]).to(self.device, self._torch.int8).clone()
         if "hdqn_goal_op" in sd:
             self.hdqn_goal_op = self._torch.as_tensor(sd["hdqn_goal_op"]).to(self.device, self._torch.int8).clone()
+        if "hdqn_ext" in sd:
+            self.hdqn_ext = self._torch.as_tensor(sd["hdqn_ext"]).to(self.device, self._torch.float64).clone()
 
     def close(self):
         pass

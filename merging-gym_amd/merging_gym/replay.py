@@ -80,22 +80,29 @@ class ReplayRing:
         return int(self._counter.item())
 
     def store(self, obs_first, obs, a1, rew, done=None, final_obs=None, won_mask=None,
-              skip_ego_won: bool = True, goal=None, next_goal=None, reward=None, flags=None):
+              skip_ego_won: bool = True, goal=None, next_goal=None, reward=None, flags=None, meta_goal=None):
         """Append T steps of N envs ([T, N, ...] tensors; obs_first [N, 10] = observation
         before step 0). skip_ego_won drops the transitions whose won bit is set (main.py:209;
         hdqn.py:316 stores all: pass False). A goal ring needs goal / next_goal [T, N] (the goal
         columns of s and s'); reward [T, N] replaces the ego's env reward rew[..., 0] as the r
         column (hdqn.py:314's intrinsic reward). flags: a rollout's interleaved [T, N, 4] buffer
         (a1, a2, done, collision), read in place of a1 / done. Stream-ordered; nothing is
-        synchronised."""
+        synchronised. meta_goal [T, N]: Goal_DQN's memory instead (hdqn.py:97-101 at :325, a plain
+        22-float ring): rows [s', meta_goal, reward, s'] for the steps whose won_mask bit is clear,
+        the mask then being the rollout's no_break and reward its ext_reward (store_meta)."""
         torch = self._torch
         if self.goal != (goal is not None) or (goal is None) != (next_goal is None):
             raise ValueError("a goal ring takes goal and next_goal; a plain ring takes neither")
+        if meta_goal is not None:
+            if self.goal or reward is None or won_mask is None:
+                raise ValueError("Goal_DQN rows need a plain ring, reward (ext_reward) and won_mask (no_break)")
+            skip_ego_won = True
         a1 = torch.as_tensor(a1, device=self.device)
         if a1.dim() == 1:  # one step
             goal = None if goal is None else torch.as_tensor(goal, device=self.device)[None]
             next_goal = None if next_goal is None else torch.as_tensor(next_goal, device=self.device)[None]
             reward = None if reward is None else torch.as_tensor(reward, device=self.device)[None]
+            meta_goal = None if meta_goal is None else torch.as_tensor(meta_goal, device=self.device)[None]
             a1 = a1[None]
             obs = torch.as_tensor(obs, device=self.device)[None]
             rew = torch.as_tensor(rew, device=self.device)[None]
@@ -122,6 +129,8 @@ class ReplayRing:
             goal, next_goal = self._f32(goal, (T, n)), self._f32(next_goal, (T, n))
         if reward is not None:
             reward = self._f32(reward, (T, n))
+        if meta_goal is not None:
+            meta_goal = self._f32(meta_goal, (T, n))
         if done is not None:
             done = torch.as_tensor(done, device=self.device)
             if done.dtype == torch.bool:
@@ -139,13 +148,14 @@ class ReplayRing:
         ptr = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
         tr = _native.Transitions(ptr(obs_first), ptr(obs), ptr(final_obs), ptr(a1), ptr(rew),
                                  ptr(done), ptr(won_mask) if skip_ego_won else None, ptr(goal),
-                                 ptr(next_goal), ptr(reward), ptr(flags))
+                                 ptr(next_goal), ptr(reward), ptr(flags), ptr(meta_goal))
         scratch = self._scratch_for(n, T)
         rc = _native.lib.mg_replay_store(
             self.memory.data_ptr(), self._counter.data_ptr(), self.capacity, self.row, ctypes.byref(tr), n,
             T, 1 if skip_ego_won else 0, scratch.data_ptr(), scratch.numel() * 8, self._stream())
         _native.check(rc, "mg_replay_store")
-        self._keepalive = (obs_first, obs, a1, rew, done, final_obs, won_mask, goal, next_goal, reward, flags)
+        self._keepalive = (obs_first, obs, a1, rew, done, final_obs, won_mask, goal, next_goal, reward, flags,
+                           meta_goal)
 
     def store_rollout(self, obs_first, traj, skip_ego_won: bool = True, goal=None, next_goal=None,
                       reward=None):
@@ -158,6 +168,18 @@ class ReplayRing:
         self.store(obs_first, traj["obs"], traj["a1"], traj["rew"], traj["done"],
                    traj["final_observation"], traj.get("won_mask"), skip_ego_won, goal, next_goal, reward,
                    traj.get("flags"))
+
+    def store_meta(self, traj):
+        """Append Goal_DQN's rows of an h-DQN rollout (MergeVecEnv.rollout_hdqn(...,
+        goal_memory=True)): upper.store_transition(state, goal, extrinsic_reward, next_state) at
+        every inner-loop break or episode end (hdqn.py:325; state is already next_state and goal
+        the :303 choice), in (t, i) order, into a plain ring (GOAL_MEMORY_CAPACITY = 200, :22,
+        :75)."""
+        if traj.get("final_observation") is None or traj.get("no_break") is None:
+            raise ValueError("roll out with final_observation=True and goal_memory=True")
+        self.store(traj["obs"][0], traj["obs"], traj["a1"], traj["rew"], traj["done"], traj["final_observation"],
+                   traj["no_break"], True, None, None, traj["ext_reward"], traj.get("flags"),
+                   meta_goal=traj["next_goal"])
 
     def store_transition(self, state, action, reward, next_state):
         """The reference's single-transition call (main.py:115-119; hdqn.py:180-184 for a goal

@@ -40,9 +40,9 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_native.State) == 7 * 8
     assert ctypes.sizeof(_native.Outputs) == 10 * 8
     assert ctypes.sizeof(_native.Traj) == 9 * 8
-    assert ctypes.sizeof(_native.Transitions) == 11 * 8
+    assert ctypes.sizeof(_native.Transitions) == 12 * 8
     assert ctypes.sizeof(_native.Stats) == 8
-    assert ctypes.sizeof(_native.HdqnTraj) == 4 * 8
+    assert ctypes.sizeof(_native.HdqnTraj) == 6 * 8
     assert _native.EPISODE_STATS_BYTES == 32  # mg_episode_stats: 2 f64 + 4 u32
     assert _native.REC64_DTYPE.itemsize == 168
 
@@ -131,13 +131,22 @@ def test_argument_errors_without_gpu():
     traj, ht = ctypes.byref(_native.Traj()), ctypes.byref(_native.HdqnTraj())
 
     def hdqn(goal_op, mode, ring=None, counter=None, cap=0):
-        return _native.lib.mg_rollout_hdqn(P, st, traj, ht, None, fake, goal_op, 16, 0, 1, 0, 4, fake, 3, fake,
+        return _native.lib.mg_rollout_hdqn(P, st, traj, ht, None, fake, goal_op, None, 16, 0, 1, 0, 4, fake, 3, fake,
                                           0, 1 << 31, mode, ring, counter, cap, 0, None)
     assert hdqn(None, 2) != 0 and b"goal_op" in _native.lib.mg_last_error()
     assert hdqn(fake, 3) != 0 and b"opponent_mode" in _native.lib.mg_last_error()
     assert hdqn(None, 0, ring=fake) != 0 and b"ring_counter" in _native.lib.mg_last_error()
     assert hdqn(None, 0, ring=ctypes.c_void_p((1 << 20) + 8), counter=fake, cap=16) != 0
     assert b"16-byte" in _native.lib.mg_last_error()
+    # Goal_DQN's outputs (ext_reward / no_break) need the running sums, ext_acc
+    htm = _native.HdqnTraj(None, None, None, None, fake, None)
+    rc = _native.lib.mg_rollout_hdqn(P, st, traj, ctypes.byref(htm), None, fake, None, None, 16, 0, 1, 0, 4, fake,
+                                     3, fake, 0, 1 << 31, 0, None, None, 0, 0, None)
+    assert rc != 0 and b"ext_acc" in _native.lib.mg_last_error()
+    # Goal_DQN rows in the replay store need reward and the no-break mask
+    trm = _native.Transitions(fake, fake, None, fake, fake, None, None, None, None, None, None, fake)
+    rc = _native.lib.mg_replay_store(fake, fake, 16, 22, ctypes.byref(trm), 4, 1, 0, fake, 1 << 20, None)
+    assert rc != 0 and b"meta_goal" in _native.lib.mg_last_error()
     # 65536 write blocks in 1024 scan groups: ticket (8) + bases u64 + offsets u32 + totals u32
     assert _native.lib.mg_replay_scratch_bytes(1 << 20, 16) == 8 + 1024 * 8 + 65536 * 4 + 1024 * 4
     assert _native.lib.mg_replay_scratch_bytes(0, 4) == 0

@@ -170,9 +170,17 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
     # n T transitions so the ring wraps inside a launch (only the newest capacity rows land)
     cap_f = n * T // 3 + 7
     ring_f = ReplayRing(cap_f, device=dev, goal=True)
+    # Goal_DQN's memory (hdqn.py:325) from the same launches: a 200-row plain ring (:22, :75)
+    ring_m = ReplayRing(200, device=dev)
+    mem_m = np.zeros((200, 22), np.float32)
+    c_m = 0
+    acc = np.zeros(n)  # extrinsic reward since each inner loop began (:286, :311-313), fp64
     for launch in range(2):
         obs_first = obs.copy()
-        tr = env.rollout_hdqn(T, meta, lower, seed, opponent=opponent, first_step=k0, ring=ring_f)
+        tr = env.rollout_hdqn(T, meta, lower, seed, opponent=opponent, first_step=k0, ring=ring_f, goal_memory=True)
+        ring_m.store_meta(tr)
+        ext_all = tr["ext_reward"].cpu().numpy().copy()
+        nb_all = tr["no_break"].cpu().numpy().copy()
         g = {k: tr[k].cpu().numpy().copy() for k in ("goal", "next_goal", "reward") + (("goal_op",) if selfplay else ())}
         a1_all, done_all = tr["a1"].cpu().numpy().copy(), tr["done"].cpu().numpy().copy()
         a2_all = tr["a2"].cpu().numpy().copy()
@@ -235,6 +243,15 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
             np.testing.assert_array_equal(g["reward"][t], (g2 == _status(obs)).astype(np.float32))
             # the goal of the next step: kept, or fresh once reached / after an episode end
             brk = d | (g2 == _status(s2))
+            # Goal_DQN's row inputs: extrinsic reward through step t, and the no-break bits
+            acc += o_rew[:, 0]
+            np.testing.assert_array_equal(ext_all[t], acc.astype(np.float32), err_msg=str((launch, t)))
+            bits = np.unpackbits(nb_all[t].view(np.uint8), bitorder="little")[:n].astype(bool)
+            np.testing.assert_array_equal(bits, ~brk, err_msg=str((launch, t)))
+            c_m = mo.replay_store(mem_m, c_m, obs, o_all[t][None], a1_all[t][None].astype(np.int8),
+                                  rew_all[t][None], d[None], fo_all[t][None], ~brk[None],
+                                  reward=acc.astype(np.float32)[None], meta_goal=g["next_goal"][t][None])
+            acc[brk] = 0.0
             gf = ub[:, 0] < thr
             fresh = np.where(gf, np.where(d, reset_goal, q2.argmax(1)), _pick(ub[:, 1], NUM_GOALS))
             exp_next = np.where(brk, fresh, g2)
@@ -276,6 +293,9 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
                             reward=rows["r_int"][t][None])
     assert ring_f.memory_counter == c
     np.testing.assert_array_equal(ring_f.memory.cpu().numpy(), mem_f)
+    assert ring_m.memory_counter == c_m > 200  # Goal_DQN's ring wrapped
+    np.testing.assert_array_equal(ring_m.memory.cpu().numpy(), mem_m)
+    np.testing.assert_array_equal(env.hdqn_ext.cpu().numpy(), acc)
 
 
 def _philox_words(gidx, seed, step):

@@ -252,3 +252,72 @@ def test_mixed_size_stores_share_scratch(torch):
         c = mo.replay_store(mem, c, obs0, obs, a1, rew, done, fobs, _unpack(words, n))
         assert ring.memory_counter == c, (n, T)
         np.testing.assert_array_equal(ring.memory.cpu().numpy(), mem, err_msg=str((n, T)))
+
+
+def test_goal_dqn_ring_reference_run(torch):
+    """Goal_DQN's memory (Goal_DQN.store_transition :97-101 at hdqn.py:325): the reference run's
+    actions and goals (tests/golden/replay_golden.npz, HL0 / HRR, gen_replay.run_hdqn) through
+    MergeVecEnv(1); at every inner-loop break or episode end the row [s', goal, extrinsic_reward,
+    s'] (extrinsic reward summed in fp64 from the env's rewards since the loop began, :286,
+    :311-313) goes through the device store's Goal_DQN mode. The ring equals the reference's
+    [200, 22] memory and counter (obs to fp32 tolerance, the rest exact)."""
+    from merging_gym import MergeVecEnv, ReplayRing
+
+    g = np.load(os.path.join(ROOT, "tests", "golden", "replay_golden.npz"))
+    for tag in ("HL0", "HRR"):
+        a1, a2, goal2 = g[f"{tag}_a1"], g[f"{tag}_a2"], g[f"{tag}_next_goal"]
+        dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+        env = MergeVecEnv(1, device="cuda:0")
+        ring = ReplayRing(int(g[f"{tag}_meta_capacity"]), device="cuda:0")
+        prev = env.reset().clone()
+        a1_d, a2_d = dev(a1.astype(np.int8)), dev(a2.astype(np.int8))
+        acc = 0.0
+        for k in range(len(a1)):
+            obs, rew, done, info = env.step(a1_d[k:k + 1], a2_d[k:k + 1])
+            acc += float(rew[0, 0])  # the fp32 reward the batched API returns, summed in fp64
+            s2 = info["final_observation"] if bool(done[0]) else obs
+            st = s2.cpu().numpy()[0].astype(np.float64)
+            status = 0 if st[0] < -0.5 * st[9] else (1 if st[0] < 0.5 * st[9] else 2)
+            brk = bool(done[0]) or int(goal2[k]) == status
+            nb = torch.tensor([0 if brk else 1], dtype=torch.int64, device="cuda:0")  # one step's mask word
+            ring.store(prev, obs, a1_d[k:k + 1], rew, done, info["final_observation"], nb, True, None, None,
+                       torch.tensor([acc], dtype=torch.float32, device="cuda:0"),
+                       meta_goal=torch.tensor([float(goal2[k])], device="cuda:0"))
+            if brk:
+                acc = 0.0
+            prev = obs.clone()
+        assert ring.memory_counter == int(g[f"{tag}_meta_counter"])
+        np.testing.assert_allclose(ring.memory.cpu().numpy(), g[f"{tag}_meta_memory"].astype(np.float32), **OBS_TOL)
+
+
+@pytest.mark.parametrize("cap", [7, 200])
+def test_goal_dqn_rows_match_oracle(torch, cap):
+    """Goal_DQN rows [s', meta_goal, r, s'] (22 floats) kept where the no-break bit is clear, over
+    stores of several shapes on random inputs: bit-exact with the oracle's replay_store."""
+    from merging_gym import ReplayRing
+
+    rng = np.random.default_rng(cap + 1)
+    ring = ReplayRing(cap, device="cuda:0")
+    mem = np.zeros((cap, 22), np.float32)
+    c = 0
+    dev = lambda a: torch.from_numpy(a).cuda()  # noqa: E731
+    for n, T in ((3000, 7), (5, 1), (257, 33)):
+        obs0 = rng.standard_normal((n, 10)).astype(np.float32)
+        obs = rng.standard_normal((T, n, 10)).astype(np.float32)
+        fobs = rng.standard_normal((T, n, 10)).astype(np.float32)
+        a1 = rng.integers(0, 5, (T, n)).astype(np.int8)
+        rew = rng.standard_normal((T, n, 2)).astype(np.float32)
+        done = (rng.random((T, n)) < 0.1).astype(np.uint8)
+        goal2 = rng.integers(0, 3, (T, n)).astype(np.float32)
+        ext = rng.standard_normal((T, n)).astype(np.float32)
+        nobrk = rng.random((T, n)) < 0.8
+        words = np.zeros((T, (n + 63) // 64), np.uint64)
+        for t in range(T):
+            bits = np.zeros(words.shape[1] * 64, np.uint8)
+            bits[:n] = nobrk[t]
+            words[t] = np.packbits(bits, bitorder="little").view(np.uint64)
+        ring.store(dev(obs0), dev(obs), dev(a1), dev(rew), dev(done), dev(fobs), dev(words.view(np.int64)), True,
+                   reward=dev(ext), meta_goal=dev(goal2))
+        c = mo.replay_store(mem, c, obs0, obs, a1, rew, done, fobs, nobrk, reward=ext, meta_goal=goal2)
+        assert ring.memory_counter == c, (n, T)
+        np.testing.assert_array_equal(ring.memory.cpu().numpy(), mem, err_msg=str((n, T)))
