@@ -54,6 +54,9 @@ namespace {
 #ifndef MG_COPY_FULL_WAVE
 #define MG_COPY_FULL_WAVE 1  // wave_copy_rows: unrolled path for a full 64-row wave
 #endif
+#ifndef MG_HDQN_OUTER
+#define MG_HDQN_OUTER 1  // h-DQN kernel: Goal_DQN's row inputs (0: compiled out, timing A/B only)
+#endif
 #ifndef MG_SINCOS_COLD
 #define MG_SINCOS_COLD 1  // the |t| >= 1/16 sincos fallback as an out-of-line call
 #endif
@@ -1918,7 +1921,7 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
   // Goal_DQN's memory (hdqn.py:286, :311-313, :322, :325): the extrinsic reward since each env's
   // inner loop began, and at each step whether that loop ended (known once Q(X, t + 1) has chosen
   // the step's next goal, so it is emitted together with the ring row of the step)
-  const bool outer = R.H.ext_reward != nullptr || R.H.no_break != nullptr;
+  const bool outer = MG_HDQN_OUTER && (R.H.ext_reward != nullptr || R.H.no_break != nullptr);
   double acc[2] = {0.0, 0.0};
   auto finish_outer = [&](int g, int t, double& ac) __attribute__((always_inline)) {
     const int j = g * kHHalf + 64 * ew + lane;
