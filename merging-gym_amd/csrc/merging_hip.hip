@@ -54,9 +54,6 @@ namespace {
 #ifndef MG_COPY_FULL_WAVE
 #define MG_COPY_FULL_WAVE 1  // wave_copy_rows: unrolled path for a full 64-row wave
 #endif
-#ifndef MG_HDQN_OUTER
-#define MG_HDQN_OUTER 1  // h-DQN kernel: Goal_DQN's row inputs (0: compiled out, timing A/B only)
-#endif
 #ifndef MG_SINCOS_COLD
 #define MG_SINCOS_COLD 1  // the |t| >= 1/16 sincos fallback as an out-of-line call
 #endif
@@ -358,22 +355,15 @@ __device__ __forceinline__ uint4 philox_block(uint64_t gi, uint64_t block, uint6
                        k0, k1);
 }
 
-#ifndef MG_PHILOX_STEPS
-#define MG_PHILOX_STEPS 8  // steps one Philox4x32-10 call feeds; 4 = the ABI-10..11 stream (timing A/B only)
-#endif
-constexpr int kStepsPerPhilox = MG_PHILOX_STEPS;  // 4 words x 2 draws
+constexpr int kStepsPerPhilox = 8;  // steps one Philox4x32-10 call feeds: 4 words x 2 draws
 
 __device__ __forceinline__ void actions_from_block(const uint4& u, uint64_t step, int opp_random, int& a1,
                                                    int& a2) {
   // word (step div 2) & 3 by a 64-bit select and shift on values: no indexed private array, no branch
   const uint64_t lo = (static_cast<uint64_t>(u.y) << 32) | u.x, hi = (static_cast<uint64_t>(u.w) << 32) | u.z;
   const uint32_t m = opp_random ? 25u : static_cast<uint32_t>(MG_NUM_ACTIONS);
-#if MG_PHILOX_STEPS == 4
-  const uint32_t w = static_cast<uint32_t>(((step & 2) ? hi : lo) >> (32 * (step & 1)));
-#else
   uint32_t w = static_cast<uint32_t>(((step & 4) ? hi : lo) >> (32 * ((step >> 1) & 1)));
   if (step & 1) w *= m;  // the second draw of the word
-#endif
   const uint32_t x = static_cast<uint32_t>((static_cast<uint64_t>(w) * m) >> 32);
   const int b1 = static_cast<int>((x * 13u) >> 6);  // x div 5 for x < 25
   a1 = opp_random ? b1 : static_cast<int>(x);
@@ -1921,7 +1911,7 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
   // Goal_DQN's memory (hdqn.py:286, :311-313, :322, :325): the extrinsic reward since each env's
   // inner loop began, and at each step whether that loop ended (known once Q(X, t + 1) has chosen
   // the step's next goal, so it is emitted together with the ring row of the step)
-  const bool outer = MG_HDQN_OUTER && (R.H.ext_reward != nullptr || R.H.no_break != nullptr);
+  const bool outer = R.H.ext_reward != nullptr || R.H.no_break != nullptr;
   double acc[2] = {0.0, 0.0};
   auto finish_outer = [&](int g, int t, double& ac) __attribute__((always_inline)) {
     const int j = g * kHHalf + 64 * ew + lane;
