@@ -33,6 +33,20 @@ def _near_tie(q, tol=1e-2):
     return (s[:, -1] - s[:, -2]) <= tol * np.maximum(1.0, np.abs(s[:, -1]))
 
 
+def _assert_choices(got, exp, greedy, q, what):
+    """got == exp wherever not (greedy and a near-tie); on failure name the envs, their Q rows and
+    top-2 gaps, so a summation-order tie can be told from a wrong forward."""
+    ok = (got == exp) | (greedy & _near_tie(q))
+    if not ok.all():
+        bad = np.flatnonzero(~ok)
+        s = np.sort(q[bad], axis=1)
+        gap = (s[:, -1] - s[:, -2]) / np.maximum(1.0, np.abs(s[:, -1]))
+        raise AssertionError(f"{what}: {bad.size} of {ok.size} differ; envs {bad[:8].tolist()}, got "
+                             f"{np.asarray(got)[bad[:8]].tolist()}, expected {np.asarray(exp)[bad[:8]].tolist()}, "
+                             f"greedy {np.asarray(greedy)[bad[:8]].tolist()}, top-2 gap {gap[:8].tolist()}, "
+                             f"q {q[bad[:3]].tolist()}")
+
+
 def test_batched_hdqn_inner_loop(coracle):
     import torch
 
@@ -216,7 +230,7 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
             q1 = mo.qnet_reference(lower_sd, x, bf16=True)
             greedy = ua[:, 0] < thr
             exp_a = np.where(greedy, q1.argmax(1), _pick(ua[:, 1], 5))
-            assert ((a1_all[t] == exp_a) | (greedy & _near_tie(q1))).all(), (launch, t)
+            _assert_choices(a1_all[t], exp_a, greedy, q1, f"ego action, launch {launch} step {t}")
             a2 = None
             if selfplay:  # lower_op.choose_action([goal_op] + swapped state), :299-300
                 uc = coracle.philox_batch(n, op_off, seed, k)
@@ -224,7 +238,7 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
                 qa = mo.qnet_reference(lower_sd, xo, bf16=True)
                 go = uc[:, 0] < thr
                 exp_a2 = np.where(go, qa.argmax(1), _pick(uc[:, 1], 5))
-                assert ((a2_all[t] == exp_a2) | (go & _near_tie(qa))).all(), (launch, t)
+                _assert_choices(a2_all[t], exp_a2, go, qa, f"opponent action, launch {launch} step {t}")
                 a2 = a2_all[t].astype(np.int8)
             o_obs, o_rew, o_done, o_coll, _, o_fobs, err = coracle.step(envs, a1_all[t].astype(np.int8), a2,
                                                                         autoreset=True, final_obs=True)

@@ -17,7 +17,10 @@ d = json.loads(open(sys.argv[3]).read().strip().splitlines()[-1])
 q = d["qnet_policy"]
 print(f"{sys.argv[1]:>14} r{sys.argv[2]}  step {d['roofline']['kernel_ms_mean']*1e3:6.2f} us  rollout "
       f"{d['rollout']['kernel_ms_mean']*1e3/16:6.2f} us/step  qnet ego {q[0]['kernel_ms_mean']*1e3/16:6.2f} "
-      f"self {q[1]['kernel_ms_mean']*1e3/16:6.2f} us/step  frac {q[0]['frac_useful']:.3f} / {q[1]['frac_useful']:.3f}")
+      f"self {q[1]['kernel_ms_mean']*1e3/16:6.2f} us/step  frac {q[0]['frac_useful']:.3f} / {q[1]['frac_useful']:.3f}"
+      + (f"  other-net {q[2]['kernel_ms_mean']*1e3/16:6.2f}" if len(q) > 2 else "")
+      + (f"  hdqn {d['hdqn_policy']['kernel_ms_mean']*1e3/16:6.2f} self {d['hdqn_policy']['selfplay']['kernel_ms_mean']*1e3/16:6.2f}"
+         if "hdqn_policy" in d else ""))
 EOF
   done
 done

@@ -39,10 +39,16 @@ __global__ __launch_bounds__(64) void k(float* out, unsigned long long* cyc, int
     for (int it = 0; it < iters; ++it) { STEP8("v_mfma_f32_16x16x32_bf16", a, b) }
     t1 = __builtin_amdgcn_s_memtime();
     s = c0[l & 3] + c1[1] + c2[2] + c3[3] + c4[0] + c5[1] + c6[2] + c7[3];
-  } else {
+  } else if constexpr (MODE == 2) {
     ACC8(f32x4);
     t0 = __builtin_amdgcn_s_memtime();
     for (int it = 0; it < iters; ++it) { STEP8("v_mfma_f32_16x16x16_bf16", a4, b4) }
+    t1 = __builtin_amdgcn_s_memtime();
+    s = c0[l & 3] + c1[1] + c2[2] + c3[3] + c4[0] + c5[1] + c6[2] + c7[3];
+  } else {  // 16 independent 4x4x4 blocks: the Q-net's layer-2 tail candidate
+    ACC8(f32x4);
+    t0 = __builtin_amdgcn_s_memtime();
+    for (int it = 0; it < iters; ++it) { STEP8("v_mfma_f32_4x4x4_16b_bf16", a4, b4) }
     t1 = __builtin_amdgcn_s_memtime();
     s = c0[l & 3] + c1[1] + c2[2] + c3[3] + c4[0] + c5[1] + c6[2] + c7[3];
   }
@@ -56,13 +62,14 @@ int main() {
   (void)hipMalloc(&out, blocks * 64 * 4);
   (void)hipMalloc(&cyc, blocks * 8);
   static unsigned long long h[blocks];
-  const char* names[3] = {"32x32x16_bf16", "16x16x32_bf16", "16x16x16bf16_1k"};
+  const char* names[4] = {"32x32x16_bf16", "16x16x32_bf16", "16x16x16bf16_1k", "4x4x4_16b_bf16"};
   double ref = 0;
-  for (int mode = 0; mode < 3; ++mode) {
+  for (int mode = 0; mode < 4; ++mode) {
     for (int rep = 0; rep < 2; ++rep) {
       if (mode == 0) hipLaunchKernelGGL(k<0>, dim3(blocks), dim3(64), 0, 0, out, cyc, iters);
       if (mode == 1) hipLaunchKernelGGL(k<1>, dim3(blocks), dim3(64), 0, 0, out, cyc, iters);
       if (mode == 2) hipLaunchKernelGGL(k<2>, dim3(blocks), dim3(64), 0, 0, out, cyc, iters);
+      if (mode == 3) hipLaunchKernelGGL(k<3>, dim3(blocks), dim3(64), 0, 0, out, cyc, iters);
       (void)hipDeviceSynchronize();
     }
     (void)hipMemcpy(h, cyc, sizeof(h), hipMemcpyDeviceToHost);
