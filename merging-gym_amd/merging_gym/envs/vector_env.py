@@ -45,7 +45,11 @@ class MergeVecEnv:
 
     def __init__(self, num_envs: int, device=None, autoreset: bool = True, env_offset: int = 0,
                  final_observation: bool = True, episode_stats: bool = True,
-                 done_mask: bool = False, won_mask: bool = False):
+                 done_mask: bool = False, won_mask: bool = False, strict_actions: bool = False):
+        """strict_actions: step() raises KeyError for an action outside action_dict the way the
+        reference's step does (merging_env.py:101, :134-136), at the cost of one stream
+        synchronisation per step; by default the kernel only flags it on the device and
+        check_actions() raises later (the stream stays asynchronous)."""
         import torch
 
         from .. import _native
@@ -102,6 +106,7 @@ class MergeVecEnv:
         self.won_mask = (torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
                          if won_mask else None)
         self.error = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.strict_actions = bool(strict_actions)
         # one 32-byte mg_episode_stats record per env; ret_sum [N,2] f64 and counts [N,4] i32
         # (episodes, collisions, ego-first arrivals, steps) are strided views of it
         self._ep_stats = torch.zeros((n, 4), dtype=torch.float64, device=dev) if episode_stats else None
@@ -215,6 +220,8 @@ class MergeVecEnv:
             self._p_ref, self._s_ref, a1.data_ptr(), None if a2 is None else a2.data_ptr(),
             self._o_ref, self._st_ref, self.num_envs, self._flags, self._stream())
         self._nat.check(rc, "mg_step")
+        if self.strict_actions:
+            self.check_actions()
         return self._outputs()
 
     def step_random(self, seed: int, opponent_random: bool = True, step_idx=None,

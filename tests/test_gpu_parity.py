@@ -291,6 +291,21 @@ def test_invalid_actions_flag_error(torch):
     env.check_actions()
 
 
+def test_strict_actions_raise_at_step(torch):
+    """strict_actions: step() itself raises KeyError like the reference's action_dict lookup
+    (merging_env.py:101, :134-136); the flag is cleared, so the next valid step goes through."""
+    from merging_gym import MergeVecEnv
+
+    env = MergeVecEnv(64, device="cuda:0", autoreset=False, strict_actions=True)
+    a1 = torch.full((64,), 2, dtype=torch.int8, device="cuda:0")
+    a2 = a1.clone()
+    a2[7] = 5
+    with pytest.raises(KeyError):
+        env.step(a1, a2)
+    env.step(a1, None)
+    assert int(env.steps[0]) == 2
+
+
 def test_native_errors_are_raised(torch):
     from merging_gym import _native
 
