@@ -391,6 +391,17 @@ def hdqn_leg(env, args, world, dist, torch):
     self_ms = timed(lambda: env.rollout_hdqn(T, meta, lower, args.seed, opponent="self", first_step=k,
                                              final_observation=False))
     self_per_s = E * T / (self_ms * 1e-3)
+    # any other Strategy_OP (hdqn.py:265-268): the opponent's own Goal_DQN + HDQN from another
+    # checkpoint; four nets exceed one CU's LDS, so the kernel reads the opponent's from L2
+    meta_op, lower_op = net(10, NUM_GOALS), net(11, 5)
+    env.hdqn_goal_op = None  # fresh opponent goals for the other nets
+    for _ in range(2):
+        env.rollout_hdqn(T, meta, lower, args.seed, opponent=(meta_op, lower_op), first_step=k,
+                         final_observation=False)
+        k += T
+    other_ms = timed(lambda: env.rollout_hdqn(T, meta, lower, args.seed, opponent=(meta_op, lower_op),
+                                              first_step=k, final_observation=False))
+    other_per_s = E * T / (other_ms * 1e-3)
     self_flop = HDQN_USEFUL_FLOP + 2 * (11 * 200 + 200 * 100 + 100 * 5)  # + the opponent's lower net
     return {"kernel": "hdqn_rollout_kernel<0>", "opponent": "none", "steps_per_launch": T, "launches": L,
             "selfplay": {"kernel": "hdqn_rollout_kernel<2>", "kernel_ms_mean": self_ms,
@@ -398,6 +409,10 @@ def hdqn_leg(env, args, world, dist, torch):
                          "frac_useful_lower_bound": self_flop * self_per_s / 1e12 / MFMA_BF16_PEAK_TFLOPS,
                          "note": "useful FLOPs count the opponent's lower net every step, not its meta-net "
                                  "(run only at outer-loop iterations)"},
+            "other_checkpoint": {"kernel": "hdqn_rollout_kernel<3>", "kernel_ms_mean": other_ms,
+                                 "env_steps_per_s": other_per_s,
+                                 "frac_useful_lower_bound": self_flop * other_per_s / 1e12 / MFMA_BF16_PEAK_TFLOPS,
+                                 "note": "opponent nets read from global memory (L2), not LDS"},
             "with_goal_ring": {"fused_store_ms_per_launch": fused_ms, "rollout_then_replay_store_ms": separate_ms,
                                "fused_env_steps_per_s": E * T / (fused_ms * 1e-3),
                                "separate_env_steps_per_s": E * T / (separate_ms * 1e-3),

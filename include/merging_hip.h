@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 15
+#define MG_ABI_VERSION 16
 #define MG_OBS_DIM 10   /* merging_env.py:75 observation_shape = (10) */
 #define MG_NUM_ACTIONS 5 /* merging_env.py:101-102 action_dict / Discrete(5) */
 #define MG_ACTION_NONE (-1) /* action2=None: the constant-speed "L0" opponent, merging_env.py:152 */
@@ -305,7 +305,7 @@ typedef struct mg_hdqn_traj {
   float* next_goal;  /* goal Goal_DQN chose on step t's next state (:303; the terminal one at an
                         episode end), the row's next goal */
   float* reward;     /* 1.0 if next_goal == goal_status(state) else 0.0 (:314) */
-  float* goal_op;    /* (optional, opponent_mode 2) the self-play opponent's goal of step t, the
+  float* goal_op;    /* (optional, opponent_mode 2 / 3) the opponent's goal of step t, the
                         goal of its goal state [goal_op] + swapped state (:285, :299) */
   float* ext_reward; /* (optional, ABI 15) extrinsic reward summed since the inner loop began,
                         through step t (:286, :311-313): Goal_DQN's row reward at a break;
@@ -327,16 +327,20 @@ typedef struct mg_hdqn_traj {
  * action, explore, goal) and counter ((env_offset + i) ^ 2^63, first_step + t) for a fresh goal
  * (x, y) and the uniform opponent (z); a launch's first fresh goals use step first_step - 1.
  * Greedy when the explore draw < greedy_threshold (np.random.randn() <= EPISILO, :84, :168).
- * traj as mg_rollout_qnet; opponent_mode 0 (None, Strategy_OP "L0", :261, :294-296), 1 (uniform)
- * or 2 (Strategy_OP "selfplay", :262-264: upper_op = upper, lower_op = lower, so the same two
- * nets): the opponent's goal is chosen by the meta-net on the swapped state
+ * traj as mg_rollout_qnet; opponent_mode 0 (None, Strategy_OP "L0", :261, :294-296), 1 (uniform),
+ * 2 (Strategy_OP "selfplay", :262-264: upper_op = upper, lower_op = lower, so the same two
+ * nets) or 3 (any other Strategy_OP, :265-268: upper_op / lower_op loaded from another h-DQN
+ * checkpoint -- opp_meta_net / opp_lower_net, packed like meta_net / lower_net, 16-byte aligned,
+ * ignored by the other modes; ABI 16. Four nets exceed one CU's LDS, so the opponent's two are
+ * read from global memory, where they stay L2-resident): the opponent's goal is chosen by its
+ * meta-net on the swapped state
  * state[5:] + state[:5] at every outer-loop iteration (:285 -- the launch's first step when
  * goal_op[i] < 0, and the step after a break: the ego's goal reached or the episode ended) and
- * kept in between; its action is the lower net's epsilon-greedy choice on
+ * kept in between; its action is its lower net's epsilon-greedy choice on
  * [goal_op] + swapped state every step (:299-300). Its draws: counter
  * ((env_offset + i) ^ 2^62, first_step + t), x explore and y action of step t, z explore and
  * w goal of a fresh opponent goal at step t + 1 (the launch's first at step first_step - 1).
- * goal_op [n] int8 (required for mode 2, else ignored) holds each env's opponent goal across
+ * goal_op [n] int8 (required for modes 2 and 3, else ignored) holds each env's opponent goal across
  * launches like goal. ext_acc [n] double (required with htraj->ext_reward or no_break, ABI 15)
  * holds each env's extrinsic reward since its inner loop began, across launches (0 at a break).
  * ring_rows (optional, 16-byte aligned [ring_capacity, 24] fp32, with ring_counter: one device
@@ -350,7 +354,8 @@ int mg_rollout_hdqn(const mg_params* params, const mg_state* state, const mg_tra
                     double* ext_acc, int64_t n,
                     int64_t env_offset, uint64_t seed, uint64_t first_step, int32_t num_steps,
                     const void* meta_net, int32_t num_goals, const void* lower_net, int32_t reset_goal,
-                    uint64_t greedy_threshold, int32_t opponent_mode, float* ring_rows,
+                    uint64_t greedy_threshold, int32_t opponent_mode, const void* opp_meta_net,
+                    const void* opp_lower_net, float* ring_rows,
                     uint64_t* ring_counter, int64_t ring_capacity, uint32_t flags, void* stream);
 
 /* ---- replay memory (scripts/main.py:91-92, :115-119, :130-135) --------------------------------

@@ -1730,6 +1730,8 @@ struct HRollout {
   double* ext_acc;  // [n] in / out, extrinsic reward since the inner loop began (Goal_DQN rows)
   const uint8_t* meta;
   const uint8_t* lower;
+  const uint8_t* meta_op;   // OPP 3: the opponent's own packed nets (read from global memory / L2)
+  const uint8_t* lower_op;
   uint64_t seed;
   uint64_t first_step;
   uint64_t greedy_thr;
@@ -1777,9 +1779,12 @@ __device__ __forceinline__ bf16x8 qnet_input_goal(const float* row, int goal, in
 #pragma unroll
   for (int k = 0; k < kObs / 2; ++k) {
     const f32x2 t = reinterpret_cast<const f32x2*>(row)[k];
-    const int d = swap ? (2 * k + kObs / 2) % kObs : 2 * k;
-    v[d] = t[0];
-    v[d + 1] = t[1];
+    // swapped view state[5:] + state[:5]: pair (4, 5) straddles the halves, so each element
+    // takes its own destination (element 5 -> v[0], element 4 -> v[9])
+    const int d0 = swap ? (2 * k + kObs / 2) % kObs : 2 * k;
+    const int d1 = swap ? (2 * k + 1 + kObs / 2) % kObs : 2 * k + 1;
+    v[d0] = t[0];
+    v[d1] = t[1];
   }
   auto pk = [](float a, float b) { return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2)); };
   const u32x4 w = h ? u32x4{pk(v[7], v[8]), pk(v[9], 0.f), 0x3F800000u, 0x3F803F80u}
@@ -1801,8 +1806,9 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
   __shared__ __attribute__((aligned(16))) uint32_t side[kHEnvs * 5];    // terminal obs, bf16 pairs
   __shared__ uint8_t b_act[kHEnvs], b_goal[kHEnvs], b_done[kHEnvs], b_st_old[kHEnvs],
       b_st_new[kHEnvs], b_dg[kHEnvs], b_df[kHEnvs], b_g2[kHEnvs];
-  // OPP 2: the opponent's greedy action, current goal and fresh-goal draw
-  __shared__ uint8_t b_aop[OPP == 2 ? kHEnvs : 1], b_gop[OPP == 2 ? kHEnvs : 1], b_dfo[OPP == 2 ? kHEnvs : 1];
+  // OPP 2 / 3: the opponent's greedy action, current goal and fresh-goal draw
+  constexpr bool kOpNets = OPP >= 2;  // the opponent acts through h-DQN nets
+  __shared__ uint8_t b_aop[kOpNets ? kHEnvs : 1], b_gop[kOpNets ? kHEnvs : 1], b_dfo[kOpNets ? kHEnvs : 1];
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int64_t base = static_cast<int64_t>(blockIdx.x) * kHEnvs;
@@ -1860,14 +1866,18 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
         goal_t = goal_prev >= 0 ? goal_prev : (df == kHGreedy ? gstar : df);
       }
       int gop_t = 0;
-      if constexpr (OPP == 2) {  // upper_op.choose_goal(swapped state) at a new outer iteration (:285)
+      if constexpr (kOpNets) {  // upper_op.choose_goal(swapped state) at a new outer iteration (:285)
         const int gop_prev = static_cast<int8_t>(b_gop[j]);
         const bool fresh_op = t > 0 ? brk : gop_prev < 0;
         int gop_star = 0;
         if (__ballot(live && fresh_op) != 0) {  // on the state acted on at step t (reset obs after an end)
           float q[8];
-          qnet_mlp_swp(lds_meta, qnet_input(tile + (row0 + r) * kObs, true, h),
-                       qnet_input(tile + (row0 + 32 + r) * kObs, true, h), q);
+          const bf16x8 x0 = qnet_input(tile + (row0 + r) * kObs, true, h);
+          const bf16x8 x1 = qnet_input(tile + (row0 + 32 + r) * kObs, true, h);
+          if constexpr (OPP == 3)
+            qnet_mlp_swp(R.meta_op, x0, x1, q);  // the opponent's own Goal_DQN (:267)
+          else
+            qnet_mlp_swp(lds_meta, x0, x1, q);
           gop_star = argmax_first(q, R.num_goals);
         }
         const int dfo = b_dfo[j];
@@ -1876,7 +1886,7 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
       if (t < T) {
         b_goal[j] = static_cast<uint8_t>(goal_t);
         if (live && R.H.goal) st_out(R.H.goal + static_cast<int64_t>(t) * R.n + i, static_cast<float>(goal_t));
-        if constexpr (OPP == 2) {
+        if constexpr (kOpNets) {
           b_gop[j] = static_cast<uint8_t>(gop_t);
           if (live && R.H.goal_op) st_out(R.H.goal_op + static_cast<int64_t>(t) * R.n + i, static_cast<float>(gop_t));
         }
@@ -1885,15 +1895,19 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
         qnet_mlp_swp(lds_lower, qnet_input_goal(tile + (row0 + r) * kObs, b_goal[row0 + r], h),
                      qnet_input_goal(tile + (row0 + 32 + r) * kObs, b_goal[row0 + 32 + r], h), q);
         b_act[j] = static_cast<uint8_t>(argmax_first(q, MG_NUM_ACTIONS));
-        if constexpr (OPP == 2) {  // lower_op.choose_action([goal_op] + swapped state) (:299-300)
+        if constexpr (kOpNets) {  // lower_op.choose_action([goal_op] + swapped state) (:299-300)
           float qo[8];
-          qnet_mlp_swp(lds_lower, qnet_input_goal(tile + (row0 + r) * kObs, b_gop[row0 + r], h, true),
-                       qnet_input_goal(tile + (row0 + 32 + r) * kObs, b_gop[row0 + 32 + r], h, true), qo);
+          const bf16x8 x0 = qnet_input_goal(tile + (row0 + r) * kObs, b_gop[row0 + r], h, true);
+          const bf16x8 x1 = qnet_input_goal(tile + (row0 + 32 + r) * kObs, b_gop[row0 + 32 + r], h, true);
+          if constexpr (OPP == 3)
+            qnet_mlp_swp(R.lower_op, x0, x1, qo);  // the opponent's own HDQN (:268)
+          else
+            qnet_mlp_swp(lds_lower, x0, x1, qo);
           b_aop[j] = static_cast<uint8_t>(argmax_first(qo, MG_NUM_ACTIONS));
         }
       } else if (live) {
         R.goal[i] = static_cast<int8_t>(goal_t);  // the next launch's starting goal
-        if constexpr (OPP == 2) R.goal_op[i] = static_cast<int8_t>(gop_t);
+        if constexpr (kOpNets) R.goal_op[i] = static_cast<int8_t>(gop_t);
       }
       __syncthreads();
     }
@@ -1986,7 +2000,7 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
     b_df[j] = draw_byte(fb.x, fb.y, R.greedy_thr, R.num_goals);
     b_goal[j] = live[g] ? static_cast<uint8_t>(R.goal[i]) : 0;
     if (outer && live[g]) acc[g] = R.ext_acc[i];
-    if constexpr (OPP == 2) {
+    if constexpr (kOpNets) {
       const uint4 fc = philox_env_step(gi ^ (uint64_t{1} << 62), R.first_step - 1, R.seed);
       b_dfo[j] = draw_byte(fc.z, fc.w, R.greedy_thr, R.num_goals);
       b_gop[j] = live[g] ? static_cast<uint8_t>(R.goal_op[i]) : 0;
@@ -2006,7 +2020,7 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
       const int a1 = static_cast<uint64_t>(ua.x) < R.greedy_thr ? static_cast<int>(b_act[j]) : action_from_u32(ua.y);
       int a2 = OPP == 1 ? action_from_u32(ub.z) : MG_ACTION_NONE;
       uint4 uc = make_uint4(0u, 0u, 0u, 0u);
-      if constexpr (OPP == 2) {  // the self-play opponent's epsilon-greedy action (:300)
+      if constexpr (kOpNets) {  // the self-play opponent's epsilon-greedy action (:300)
         uc = philox_env_step(gi ^ (uint64_t{1} << 62), k, R.seed);
         a2 = static_cast<uint64_t>(uc.x) < R.greedy_thr ? static_cast<int>(b_aop[j]) : action_from_u32(uc.y);
       }
@@ -2046,7 +2060,7 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
         b_st_new[j] = static_cast<uint8_t>(goal_status(rv.o));
         b_dg[j] = draw_byte(ua.z, ua.w, R.greedy_thr, R.num_goals);
         b_df[j] = draw_byte(ub.x, ub.y, R.greedy_thr, R.num_goals);
-        if constexpr (OPP == 2) b_dfo[j] = draw_byte(uc.z, uc.w, R.greedy_thr, R.num_goals);
+        if constexpr (kOpNets) b_dfo[j] = draw_byte(uc.z, uc.w, R.greedy_thr, R.num_goals);
         const bool won = lv && ev.winner == 1;
         const int64_t rem = R.n - wbase;
         store_won_mask(R.T.won_mask, won, t, R.n, wbase, rem <= 0 ? 0 : (rem < 64 ? static_cast<int>(rem) : 64));
@@ -2803,7 +2817,8 @@ int mg_rollout_hdqn(const mg_params* params, const mg_state* state, const mg_tra
                     double* ext_acc, int64_t n, int64_t env_offset, uint64_t seed, uint64_t first_step,
                     int32_t num_steps,
                     const void* meta_net, int32_t num_goals, const void* lower_net, int32_t reset_goal,
-                    uint64_t greedy_threshold, int32_t opponent_mode, float* ring_rows,
+                    uint64_t greedy_threshold, int32_t opponent_mode, const void* opp_meta_net,
+                    const void* opp_lower_net, float* ring_rows,
                     uint64_t* ring_counter, int64_t ring_capacity, uint32_t flags, void* stream) {
   if (ring_rows && (!ring_counter || ring_capacity < 1 || (reinterpret_cast<uintptr_t>(ring_rows) & 15)))
     return fail(hipErrorInvalidValue, "%s", "ring_rows needs ring_counter, capacity >= 1 and 16-byte alignment");
@@ -2815,10 +2830,15 @@ int mg_rollout_hdqn(const mg_params* params, const mg_state* state, const mg_tra
     return fail(hipErrorInvalidValue, "%s", "meta_net / lower_net must be 16-byte aligned packed Q-nets");
   if (num_steps < 0 || num_goals < 1 || num_goals > 8 || reset_goal < 0 || reset_goal >= num_goals)
     return fail(hipErrorInvalidValue, "%s", "need num_steps >= 0, 1 <= num_goals <= 8, 0 <= reset_goal < num_goals");
-  if (opponent_mode < 0 || opponent_mode > 2)
-    return fail(hipErrorInvalidValue, "%s", "opponent_mode must be 0 (None), 1 (uniform) or 2 (self-play)");
-  if (opponent_mode == 2 && !goal_op)
-    return fail(hipErrorInvalidValue, "%s", "opponent_mode 2 needs goal_op (an [n] int8 device array)");
+  if (opponent_mode < 0 || opponent_mode > 3)
+    return fail(hipErrorInvalidValue, "%s",
+                "opponent_mode must be 0 (None), 1 (uniform), 2 (self-play) or 3 (other h-DQN)");
+  if (opponent_mode >= 2 && !goal_op)
+    return fail(hipErrorInvalidValue, "%s", "opponent_mode 2 / 3 needs goal_op (an [n] int8 device array)");
+  if (opponent_mode == 3 &&
+      (!opp_meta_net || !opp_lower_net ||
+       ((reinterpret_cast<uintptr_t>(opp_meta_net) | reinterpret_cast<uintptr_t>(opp_lower_net)) & 15)))
+    return fail(hipErrorInvalidValue, "%s", "opponent_mode 3 needs 16-byte aligned opp_meta_net / opp_lower_net");
   if (htraj && (htraj->ext_reward || htraj->no_break) && !ext_acc)
     return fail(hipErrorInvalidValue, "%s", "ext_reward / no_break need ext_acc (an [n] double device array)");
   if (htraj && htraj->no_break && (reinterpret_cast<uintptr_t>(htraj->no_break) & 7))
@@ -2840,6 +2860,8 @@ int mg_rollout_hdqn(const mg_params* params, const mg_state* state, const mg_tra
   R.ext_acc = ext_acc;
   R.meta = static_cast<const uint8_t*>(meta_net);
   R.lower = static_cast<const uint8_t*>(lower_net);
+  R.meta_op = static_cast<const uint8_t*>(opp_meta_net);
+  R.lower_op = static_cast<const uint8_t*>(opp_lower_net);
   R.seed = seed;
   R.first_step = first_step;
   R.greedy_thr = greedy_threshold;
@@ -2858,8 +2880,10 @@ int mg_rollout_hdqn(const mg_params* params, const mg_state* state, const mg_tra
     hipLaunchKernelGGL(hdqn_rollout_kernel<0>, dim3(blocks), dim3(512), 0, st, R);
   else if (opponent_mode == 1)
     hipLaunchKernelGGL(hdqn_rollout_kernel<1>, dim3(blocks), dim3(512), 0, st, R);
-  else
+  else if (opponent_mode == 2)
     hipLaunchKernelGGL(hdqn_rollout_kernel<2>, dim3(blocks), dim3(512), 0, st, R);
+  else
+    hipLaunchKernelGGL(hdqn_rollout_kernel<3>, dim3(blocks), dim3(512), 0, st, R);
   if (ring_rows)  // after every block has read the old counter: the same stream orders it
     hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(1), 0, st, ring_counter,
                        static_cast<uint64_t>(num_steps) * static_cast<uint64_t>(n));

@@ -15,7 +15,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libmerging_hip.so"
 LIB_PATH = os.environ.get("MERGING_HIP_LIB", os.path.join(_HERE, LIB_NAME))
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 OBS_DIM = 10
 NUM_ACTIONS = 5
@@ -115,7 +115,8 @@ def _load():
                                     _c.c_uint64, _P, _c.c_uint32, _P]
     lib.mg_rollout_hdqn.argtypes = [PP, SP, _c.POINTER(Traj), _c.POINTER(HdqnTraj), STP, _P, _P, _P, _c.c_int64,
                                     _c.c_int64, _c.c_uint64, _c.c_uint64, _c.c_int32, _P, _c.c_int32, _P,
-                                    _c.c_int32, _c.c_uint64, _c.c_int32, _P, _P, _c.c_int64, _c.c_uint32, _P]
+                                    _c.c_int32, _c.c_uint64, _c.c_int32, _P, _P, _P, _P, _c.c_int64, _c.c_uint32,
+                                    _P]
     lib.mg_time_next_launch.argtypes = [_P, _P]
     lib.mg_replay_scratch_bytes.argtypes = [_c.c_int64, _c.c_int32]
     lib.mg_replay_scratch_bytes.restype = _c.c_size_t

@@ -324,7 +324,7 @@ class MergeVecEnv:
         self._step_idx = k0 + T
         return buf["_result"]
 
-    def rollout_hdqn(self, num_steps: int, meta, lower, seed: int, opponent: str = "none",
+    def rollout_hdqn(self, num_steps: int, meta, lower, seed: int, opponent="none",
                      episilo: float = 0.7, first_step=None, final_observation: bool = True,
                      won_mask: bool = False, ring=None, goal_memory: bool = False):
         """`num_steps` steps of hdqn.py's inner loop (scripts/hdqn.py:280-323) in one launch:
@@ -334,12 +334,14 @@ class MergeVecEnv:
         chosen once a goal is reached or an episode ends. opponent: "none" (L0, hdqn.py's default
         Strategy_OP), "uniform", or "self" (Strategy_OP "selfplay", :262-264: the same two nets
         choose the opponent's goal on the swapped state at every outer-loop iteration, :285, and
-        its action on [goal_op] + swapped state, :299-300). Each env's current goal persists
-        across launches in `self.hdqn_goal` ([N] int8, -1 = none yet), the self-play opponent's
-        in `self.hdqn_goal_op`. Returns rollout_random's [T, N, ...] dict plus "goal",
+        its action on [goal_op] + swapped state, :299-300), or a (meta_op, lower_op) pair of
+        QNets from another h-DQN checkpoint (any other Strategy_OP, :265-268: Goal_DQN and HDQN
+        loaded from load_path_op, acting the same way). Each env's current goal persists across
+        launches in `self.hdqn_goal` ([N] int8, -1 = none yet), the opponent's in
+        `self.hdqn_goal_op`. Returns rollout_random's [T, N, ...] dict plus "goal",
         "next_goal" and "reward" ([T, N] fp32: the goal columns and the intrinsic reward of
         HDQN.store_transition's rows, :316 -- ReplayRing(goal=True).store_rollout takes them as
-        they are), and with opponent "self" "goal_op" ([T, N] fp32, the opponent's goal of each
+        they are), and with an h-DQN opponent "goal_op" ([T, N] fp32, the opponent's goal of each
         step). ring: a ReplayRing(goal=True) the same launch appends every
         transition to (hdqn.py:316 stores them all, so the kernel needs no scan): the rows
         store_rollout(obs0, traj, skip_ego_won=False, goal=..., next_goal=..., reward=...) would
@@ -352,7 +354,15 @@ class MergeVecEnv:
 
         torch, nat = self._torch, self._nat
         T, n = int(num_steps), self.num_envs
-        mode = {"none": 0, "uniform": 1, "self": 2}[opponent]
+        opp_meta = opp_lower = None
+        if isinstance(opponent, (tuple, list)):
+            opp_meta, opp_lower = opponent
+            if (opp_meta.in_dim != _OBS_DIM or opp_meta.out_dim != meta.out_dim or opp_lower.in_dim != _OBS_DIM + 1
+                    or opp_lower.out_dim != nat.NUM_ACTIONS):
+                raise ValueError("the opponent's nets must be shaped like meta and lower (10 -> goals, 11 -> 5)")
+            mode = 3
+        else:
+            mode = {"none": 0, "uniform": 1, "self": 2}[opponent]
         if ring is not None and (not ring.goal or ring.device != self.device):
             raise ValueError("the fused store needs a goal ring (ReplayRing(goal=True)) on this env's device")
         if meta.in_dim != _OBS_DIM or lower.in_dim != _OBS_DIM + 1 or lower.out_dim != nat.NUM_ACTIONS:
@@ -372,7 +382,7 @@ class MergeVecEnv:
             self.hdqn_ext = torch.zeros(n, dtype=torch.float64, device=self.device)
         if getattr(self, "hdqn_goal", None) is None:
             self.hdqn_goal = torch.full((n,), -1, dtype=torch.int8, device=self.device)
-        if mode == 2 and getattr(self, "hdqn_goal_op", None) is None:
+        if mode >= 2 and getattr(self, "hdqn_goal_op", None) is None:
             self.hdqn_goal_op = torch.full((n,), -1, dtype=torch.int8, device=self.device)
         gop = getattr(self, "hdqn_goal_op", None)
         ext = getattr(self, "hdqn_ext", None) if goal_memory else None
@@ -381,14 +391,15 @@ class MergeVecEnv:
             self._st_ref, self.hdqn_goal.data_ptr(), None if gop is None else gop.data_ptr(),
             None if ext is None else ext.data_ptr(), n, self.env_offset, seed & 0xFFFFFFFFFFFFFFFF, k0 & 0xFFFFFFFFFFFFFFFF,
             T, meta.packed.data_ptr(), meta.out_dim, lower.packed.data_ptr(), meta.reset_argmax(),
-            greedy_threshold(episilo), mode, None if ring is None else ring.memory.data_ptr(),
+            greedy_threshold(episilo), mode, None if opp_meta is None else opp_meta.packed.data_ptr(),
+            None if opp_lower is None else opp_lower.packed.data_ptr(), None if ring is None else ring.memory.data_ptr(),
             None if ring is None else ring._counter.data_ptr(), 0 if ring is None else ring.capacity,
             self._flags, self._stream())
         nat.check(rc, "mg_rollout_hdqn")
         self._step_idx = k0 + T
         out = dict(buf["_result"])
         out.update(goal=hb["goal"], next_goal=hb["next_goal"], reward=hb["reward"])
-        if mode == 2:
+        if mode >= 2:
             out["goal_op"] = hb["goal_op"]
         if goal_memory:
             out.update(ext_reward=hb["ext_reward"], no_break=hb["no_break"])

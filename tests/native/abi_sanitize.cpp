@@ -62,18 +62,21 @@ int main() {
   mg_hdqn_traj ht{};
   int8_t* g8 = static_cast<int8_t*>(fake);
   bad += expect_error(mg_rollout_hdqn(&p, &sf, &tj0, &ht, nullptr, g8, nullptr, nullptr, 16, 0, 1, 0, 4, fake, 3, fake, 0,
-                                      1ull << 31, 2, nullptr, nullptr, 0, 0, nullptr), "self-play without goal_op");
+                                      1ull << 31, 2, nullptr, nullptr, nullptr, nullptr, 0, 0, nullptr), "self-play without goal_op");
   bad += expect_error(mg_rollout_hdqn(&p, &sf, &tj0, &ht, nullptr, g8, g8, nullptr, 16, 0, 1, 0, 4, fake, 3, fake, 0,
-                                      1ull << 31, 3, nullptr, nullptr, 0, 0, nullptr), "opponent_mode 3");
+                                      1ull << 31, 3, nullptr, nullptr, nullptr, nullptr, 0, 0, nullptr),
+                      "opponent_mode 3 without its nets");
+  bad += expect_error(mg_rollout_hdqn(&p, &sf, &tj0, &ht, nullptr, g8, g8, nullptr, 16, 0, 1, 0, 4, fake, 3, fake, 0,
+                                      1ull << 31, 4, fake, fake, nullptr, nullptr, 0, 0, nullptr), "opponent_mode 4");
   bad += expect_error(mg_rollout_hdqn(&p, &sf, &tj0, &ht, nullptr, g8, nullptr, nullptr, 16, 0, 1, 0, 4, fake, 3, fake, 0,
-                                      1ull << 31, 0, static_cast<float*>(fake), nullptr, 16, 0, nullptr),
+                                      1ull << 31, 0, nullptr, nullptr, static_cast<float*>(fake), nullptr, 16, 0, nullptr),
                       "ring without counter");
   if (mg_rollout_hdqn(&p, &sf, &tj0, &ht, nullptr, g8, nullptr, nullptr, 0, 0, 1, 0, 4, fake, 3, fake, 0, 1ull << 31, 0,
-                      nullptr, nullptr, 0, 0, nullptr) != 0) bad += 1;  // empty batch
+                      nullptr, nullptr, nullptr, nullptr, 0, 0, nullptr) != 0) bad += 1;  // empty batch
   mg_hdqn_traj htm{};
   htm.no_break = static_cast<uint64_t*>(fake);
   bad += expect_error(mg_rollout_hdqn(&p, &sf, &tj0, &htm, nullptr, g8, nullptr, nullptr, 16, 0, 1, 0, 4, fake, 3,
-                                      fake, 0, 1ull << 31, 0, nullptr, nullptr, 0, 0, nullptr),
+                                      fake, 0, 1ull << 31, 0, nullptr, nullptr, nullptr, nullptr, 0, 0, nullptr),
                       "Goal_DQN outputs without ext_acc");
   if (mg_replay_scratch_bytes(1 << 20, 16) != 8 + 1024 * 8 + 65536 * 4 + 1024 * 4) bad += 1;
   if (mg_qnet_packed_bytes() % 16 != 0) bad += 1;

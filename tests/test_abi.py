@@ -126,22 +126,27 @@ def test_argument_errors_without_gpu():
     rc = _native.lib.mg_step_random(P, st, fake, None, ctypes.byref(_native.Outputs(flags=fake)), None, 16, 0, 1,
                                     0, 1, 0, None)
     assert rc != 0 and b"a1_out" in _native.lib.mg_last_error()
-    # h-DQN acting loop: the self-play opponent needs its goal array, the fused ring its counter
-    # and 16-byte alignment, opponent modes beyond 2 are refused
+    # h-DQN acting loop: the self-play / other-checkpoint opponent needs its goal array (mode 3
+    # also both of its nets, 16-byte aligned), the fused ring its counter and 16-byte alignment,
+    # opponent modes beyond 3 are refused
     traj, ht = ctypes.byref(_native.Traj()), ctypes.byref(_native.HdqnTraj())
 
-    def hdqn(goal_op, mode, ring=None, counter=None, cap=0):
+    def hdqn(goal_op, mode, ring=None, counter=None, cap=0, opp=(None, None)):
         return _native.lib.mg_rollout_hdqn(P, st, traj, ht, None, fake, goal_op, None, 16, 0, 1, 0, 4, fake, 3, fake,
-                                          0, 1 << 31, mode, ring, counter, cap, 0, None)
+                                          0, 1 << 31, mode, opp[0], opp[1], ring, counter, cap, 0, None)
     assert hdqn(None, 2) != 0 and b"goal_op" in _native.lib.mg_last_error()
-    assert hdqn(fake, 3) != 0 and b"opponent_mode" in _native.lib.mg_last_error()
+    assert hdqn(None, 3, opp=(fake, fake)) != 0 and b"goal_op" in _native.lib.mg_last_error()
+    assert hdqn(fake, 3) != 0 and b"opp_meta_net" in _native.lib.mg_last_error()
+    assert hdqn(fake, 3, opp=(fake, ctypes.c_void_p((1 << 20) + 8))) != 0
+    assert b"opp_meta_net" in _native.lib.mg_last_error()
+    assert hdqn(fake, 4) != 0 and b"opponent_mode" in _native.lib.mg_last_error()
     assert hdqn(None, 0, ring=fake) != 0 and b"ring_counter" in _native.lib.mg_last_error()
     assert hdqn(None, 0, ring=ctypes.c_void_p((1 << 20) + 8), counter=fake, cap=16) != 0
     assert b"16-byte" in _native.lib.mg_last_error()
     # Goal_DQN's outputs (ext_reward / no_break) need the running sums, ext_acc
     htm = _native.HdqnTraj(None, None, None, None, fake, None)
     rc = _native.lib.mg_rollout_hdqn(P, st, traj, ctypes.byref(htm), None, fake, None, None, 16, 0, 1, 0, 4, fake,
-                                     3, fake, 0, 1 << 31, 0, None, None, 0, 0, None)
+                                     3, fake, 0, 1 << 31, 0, None, None, None, None, 0, 0, None)
     assert rc != 0 and b"ext_acc" in _native.lib.mg_last_error()
     # Goal_DQN rows in the replay store need reward and the no-break mask
     trm = _native.Transitions(fake, fake, None, fake, fake, None, None, None, None, None, None, fake)

@@ -28,6 +28,22 @@ def _net(rng, in_dim, out_dim):
     return sd
 
 
+def _selector_net(c=10.0):
+    """A lower-level Net (11 -> 5) whose greedy choice reads one input: Q0 = relu(x[1]),
+    Q1 = c, Q2..4 = 0, so argmax = 0 iff x[1] > c. x[1] is state[0] on the ego's goal state and
+    state[5] on the opponent's swapped one (hdqn.py:291, :299) -- the feature a swap that drops
+    an element would lose. (Seeded uniform nets, hdqn.py:41-47, pick nearly the same action for
+    every env and would not notice.)"""
+    sd = {"fc1.weight": np.zeros((200, 11), np.float32), "fc1.bias": np.zeros(200, np.float32),
+          "fc2.weight": np.zeros((100, 200), np.float32), "fc2.bias": np.zeros(100, np.float32),
+          "out.weight": np.zeros((5, 100), np.float32), "out.bias": np.zeros(5, np.float32)}
+    sd["fc1.weight"][0, 1] = 1.0
+    sd["fc2.weight"][0, 0] = 1.0
+    sd["out.weight"][0, 0] = 1.0
+    sd["out.bias"][1] = c
+    return sd
+
+
 def _near_tie(q, tol=1e-2):
     s = np.sort(q, axis=1)
     return (s[:, -1] - s[:, -2]) <= tol * np.maximum(1.0, np.abs(s[:, -1]))
@@ -138,7 +154,9 @@ def _swap(o):
     return np.concatenate([o[:, 5:], o[:, :5]], axis=1)
 
 
-@pytest.mark.parametrize("n,opponent", [(2048, "none"), (1000, "none"), (2048, "self"), (1000, "self")])
+@pytest.mark.parametrize("n,opponent", [(2048, "none"), (1000, "none"), (2048, "self"), (1000, "self"),
+                                        (2048, "other"), (1000, "other"), (1000, "self-selector"),
+                                        (1000, "other-selector")])
 def test_fused_hdqn_rollout(coracle, n, opponent):
     """mg_rollout_hdqn -- hdqn.py:280-323 in one launch -- against the loop restated on the CPU:
     every transition equals the C oracle's given the kernel's actions; every action, next goal and
@@ -148,7 +166,9 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
     are reached and episodes end inside the launch; a second launch continues the goals.
     opponent "self" (Strategy_OP "selfplay", :262-264): the opponent's goal is the meta-net's
     epsilon-greedy choice on the swapped state at every outer-loop iteration (:285) and kept in
-    between, its action the lower net's on [goal_op] + swapped state (:299-300)."""
+    between, its action the lower net's on [goal_op] + swapped state (:299-300). opponent
+    "other" (any other Strategy_OP, :265-268): the same, with a second pair of nets standing in
+    for the checkpoint load_path_op holds (the kernel reads them from global memory)."""
     import torch
 
     from merging_gym import MergeVecEnv, ReplayRing
@@ -157,7 +177,15 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
     T, seed, dev = 24, 9, "cuda:0"
     rng = np.random.default_rng(21)
     meta_sd, lower_sd = _net(rng, 10, NUM_GOALS), _net(rng, 11, 5)
+    if opponent == "self-selector":  # both players act through the one-feature net
+        lower_sd = _selector_net()
     meta, lower = QNet.from_state_dict(meta_sd, device=dev), QNet.from_state_dict(lower_sd, device=dev)
+    op_meta_sd, op_lower_sd = meta_sd, lower_sd  # self-play: upper_op = upper, lower_op = lower
+    opp_arg = "self" if opponent == "self-selector" else opponent
+    if opponent in ("other", "other-selector"):
+        op_meta_sd = _net(rng, 10, NUM_GOALS)
+        op_lower_sd = _net(rng, 11, 5) if opponent == "other" else _selector_net()
+        opp_arg = (QNet.from_state_dict(op_meta_sd, device=dev), QNet.from_state_dict(op_lower_sd, device=dev))
     thr = greedy_threshold()
     env = MergeVecEnv(n, device=dev, final_observation=True)
     k0 = 190
@@ -176,7 +204,7 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
     assert reset_goal == q_reset.argmax(1)[0] or _near_tie(q_reset)[0]
     fresh_off = -(1 << 63)  # counter (env ^ 2^63, step): the fresh-goal stream
     op_off = 1 << 62  # counter (env ^ 2^62, step): the self-play opponent's stream
-    selfplay = opponent == "self"
+    selfplay = opponent != "none"  # the opponent acts through h-DQN nets
     goal_prev = gop_prev = None
     rows = {k: [] for k in ("obs0", "obs", "fobs", "a1", "rew", "done", "goal", "goal2", "r_int")}
     ring = ReplayRing(4 * n * T, device=dev, goal=True)
@@ -191,7 +219,7 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
     acc = np.zeros(n)  # extrinsic reward since each inner loop began (:286, :311-313), fp64
     for launch in range(2):
         obs_first = obs.copy()
-        tr = env.rollout_hdqn(T, meta, lower, seed, opponent=opponent, first_step=k0, ring=ring_f, goal_memory=True)
+        tr = env.rollout_hdqn(T, meta, lower, seed, opponent=opp_arg, first_step=k0, ring=ring_f, goal_memory=True)
         ring_m.store_meta(tr)
         ext_all = tr["ext_reward"].cpu().numpy().copy()
         nb_all = tr["no_break"].cpu().numpy().copy()
@@ -213,7 +241,7 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
         if selfplay:  # the opponent's first goal (:285): carried over, or fresh with step k0 - 1's draw
             if gop_prev is None:
                 fc = coracle.philox_batch(n, op_off, seed, k0 - 1)
-                qo = mo.qnet_reference(meta_sd, _swap(obs), bf16=True)
+                qo = mo.qnet_reference(op_meta_sd, _swap(obs), bf16=True)
                 gf0 = fc[:, 2] < thr
                 ok = (g["goal_op"][0] == np.where(gf0, qo.argmax(1), _pick(fc[:, 3], NUM_GOALS))) | (gf0 & _near_tie(qo))
             else:
@@ -235,7 +263,7 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
             if selfplay:  # lower_op.choose_action([goal_op] + swapped state), :299-300
                 uc = coracle.philox_batch(n, op_off, seed, k)
                 xo = np.concatenate([g["goal_op"][t][:, None].astype(np.float32), _swap(obs)], axis=1)
-                qa = mo.qnet_reference(lower_sd, xo, bf16=True)
+                qa = mo.qnet_reference(op_lower_sd, xo, bf16=True)
                 go = uc[:, 0] < thr
                 exp_a2 = np.where(go, qa.argmax(1), _pick(uc[:, 1], 5))
                 _assert_choices(a2_all[t], exp_a2, go, qa, f"opponent action, launch {launch} step {t}")
@@ -272,7 +300,7 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
             nxt = g["goal"][t + 1] if t + 1 < T else env.hdqn_goal.cpu().numpy().astype(np.int64)
             assert ((nxt == exp_next) | (brk & gf & ~d & _near_tie(q2))).all(), (launch, t)
             if selfplay:  # the opponent's goal of the next step: fresh at a new outer iteration (:285)
-                qo = mo.qnet_reference(meta_sd, _swap(o_all[t]), bf16=True)  # the state acted on next (reset obs after an end)
+                qo = mo.qnet_reference(op_meta_sd, _swap(o_all[t]), bf16=True)  # the state acted on next (reset obs after an end)
                 go = uc[:, 2] < thr
                 exp_op = np.where(brk, np.where(go, qo.argmax(1), _pick(uc[:, 3], NUM_GOALS)), g["goal_op"][t])
                 nxo = g["goal_op"][t + 1] if t + 1 < T else env.hdqn_goal_op.cpu().numpy().astype(np.int64)
@@ -402,7 +430,7 @@ def test_fused_hdqn_rollout_full_size(coracle):
         np.testing.assert_array_equal(src[idx].cpu().numpy(), envs[name], err_msg=name)
 
 
-@pytest.mark.parametrize("opponent", ["none", "self"])
+@pytest.mark.parametrize("opponent", ["none", "self", "other"])
 def test_hdqn_checkpoint_resume_is_bit_exact(opponent):
     """A checkpoint taken between two h-DQN launches (MergeVecEnv.state_dict: the batch state, the
     step index keying the draws, the ego's goals and the self-play opponent's goals) resumes the
@@ -419,6 +447,9 @@ def test_hdqn_checkpoint_resume_is_bit_exact(opponent):
     rng = np.random.default_rng(8)
     meta = QNet.from_state_dict(_net(rng, 10, NUM_GOALS), device=dev)
     lower = QNet.from_state_dict(_net(rng, 11, 5), device=dev)
+    if opponent == "other":  # another h-DQN checkpoint's nets (hdqn.py:265-268)
+        opponent = (QNet.from_state_dict(_net(rng, 10, NUM_GOALS), device=dev),
+                    QNet.from_state_dict(_net(rng, 11, 5), device=dev))
     env = MergeVecEnv(n, device=dev, final_observation=True)
     for k in range(180):
         env.step_random(seed, opponent_random=False, step_idx=k)
@@ -444,4 +475,34 @@ def test_hdqn_checkpoint_resume_is_bit_exact(opponent):
         assert same, k
     for k, v in env2.state_dict().items():
         assert (torch.equal(v, end[k]) if isinstance(v, torch.Tensor) else v == end[k]), k
-    assert ("hdqn_goal_op" in end) == (opponent == "self")
+    assert ("hdqn_goal_op" in end) == (opponent != "none")
+
+
+def test_other_checkpoint_opponent_with_own_nets_equals_selfplay():
+    """An opponent checkpoint holding the ego's own nets (hdqn.py:265-268 with load_path_op =
+    load_path) is self-play (:262-264): opponent mode 3, which reads the opponent's nets from
+    global memory, must give mode 2's outputs bit for bit."""
+    import torch
+
+    from merging_gym import MergeVecEnv
+    from merging_gym.policy import NUM_GOALS, QNet
+
+    n, T, seed, dev = 1000, 16, 6, "cuda:0"
+    rng = np.random.default_rng(5)
+    meta = QNet.from_state_dict(_net(rng, 10, NUM_GOALS), device=dev)
+    lower = QNet.from_state_dict(_net(rng, 11, 5), device=dev)
+    outs = []
+    for opp in ("self", (meta, lower)):
+        env = MergeVecEnv(n, device=dev, final_observation=True)
+        for k in range(190):
+            env.step_random(seed, opponent_random=False, step_idx=k)
+        tr = env.rollout_hdqn(T, meta, lower, seed, opponent=opp, first_step=190)
+        outs.append({k: v.clone() for k, v in tr.items() if v is not None and k != "final_observation"})
+    a, b = outs
+    assert set(a) == set(b)
+    for k in a:
+        same = torch.equal(a[k], b[k])
+        if not same and k == "a2":
+            raise AssertionError(f"a2: {int((a[k] != b[k]).sum())} differ; self {a[k][0, :12].tolist()}, "
+                                 f"other {b[k][0, :12].tolist()}")
+        assert same, k
