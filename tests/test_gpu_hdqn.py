@@ -28,6 +28,17 @@ def _net(rng, in_dim, out_dim):
     return sd
 
 
+def _net_signed(rng, in_dim, out_dim):
+    """torch.nn.Linear's default initialisation, U(-1/sqrt(in), 1/sqrt(in)) for weights and
+    biases: signed weights, so the greedy choice varies from env to env and depends on every
+    input feature (the seeded uniform(0, 1) nets of hdqn.py:41-47 pick nearly one action)."""
+    sd = {}
+    for name, (o, i) in zip(("fc1", "fc2", "out"), [(200, in_dim), (100, 200), (out_dim, 100)]):
+        sd[f"{name}.weight"] = rng.uniform(-i ** -0.5, i ** -0.5, (o, i)).astype(np.float32)
+        sd[f"{name}.bias"] = rng.uniform(-i ** -0.5, i ** -0.5, o).astype(np.float32)
+    return sd
+
+
 def _selector_net(c=10.0):
     """A lower-level Net (11 -> 5) whose greedy choice reads one input: Q0 = relu(x[1]),
     Q1 = c, Q2..4 = 0, so argmax = 0 iff x[1] > c. x[1] is state[0] on the ego's goal state and
@@ -156,7 +167,7 @@ def _swap(o):
 
 @pytest.mark.parametrize("n,opponent", [(2048, "none"), (1000, "none"), (2048, "self"), (1000, "self"),
                                         (2048, "other"), (1000, "other"), (1000, "self-selector"),
-                                        (1000, "other-selector")])
+                                        (1000, "other-selector"), (1000, "self-signed"), (1000, "other-signed")])
 def test_fused_hdqn_rollout(coracle, n, opponent):
     """mg_rollout_hdqn -- hdqn.py:280-323 in one launch -- against the loop restated on the CPU:
     every transition equals the C oracle's given the kernel's actions; every action, next goal and
@@ -176,15 +187,16 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
 
     T, seed, dev = 24, 9, "cuda:0"
     rng = np.random.default_rng(21)
-    meta_sd, lower_sd = _net(rng, 10, NUM_GOALS), _net(rng, 11, 5)
+    mk = _net_signed if opponent.endswith("-signed") else _net
+    meta_sd, lower_sd = mk(rng, 10, NUM_GOALS), mk(rng, 11, 5)
     if opponent == "self-selector":  # both players act through the one-feature net
         lower_sd = _selector_net()
     meta, lower = QNet.from_state_dict(meta_sd, device=dev), QNet.from_state_dict(lower_sd, device=dev)
     op_meta_sd, op_lower_sd = meta_sd, lower_sd  # self-play: upper_op = upper, lower_op = lower
-    opp_arg = "self" if opponent == "self-selector" else opponent
-    if opponent in ("other", "other-selector"):
-        op_meta_sd = _net(rng, 10, NUM_GOALS)
-        op_lower_sd = _net(rng, 11, 5) if opponent == "other" else _selector_net()
+    opp_arg = "self" if opponent.startswith("self") else opponent
+    if opponent.startswith("other"):
+        op_meta_sd = mk(rng, 10, NUM_GOALS)
+        op_lower_sd = _selector_net() if opponent == "other-selector" else mk(rng, 11, 5)
         opp_arg = (QNet.from_state_dict(op_meta_sd, device=dev), QNet.from_state_dict(op_lower_sd, device=dev))
     thr = greedy_threshold()
     env = MergeVecEnv(n, device=dev, final_observation=True)
