@@ -363,7 +363,8 @@ def _philox_words(gidx, seed, step):
     return np.stack([w.astype(np.uint32) for w in u], axis=1)
 
 
-def test_fused_hdqn_rollout_full_size(coracle):
+@pytest.mark.parametrize("nets", ["uniform", "signed"])
+def test_fused_hdqn_rollout_full_size(coracle, nets):
     """hdqn.py's acting loop at the BASELINE batch, 2^20 envs x 16 steps in one launch (the
     kernel's 512-env blocks and the [T, N] goal outputs at full size). Whole batch: actions and
     goals in range, intrinsic rewards 0/1, no NaN, the step bookkeeping. 2,048 sampled global env
@@ -377,7 +378,8 @@ def test_fused_hdqn_rollout_full_size(coracle):
 
     n, T, seed, k0, burn, dev = 1 << 20, 16, 17, 900, 240, "cuda:0"
     rng = np.random.default_rng(5)
-    meta_sd, lower_sd = _net(rng, 10, NUM_GOALS), _net(rng, 11, 5)
+    mk = _net_signed if nets == "signed" else _net  # signed: choices that vary per env
+    meta_sd, lower_sd = mk(rng, 10, NUM_GOALS), mk(rng, 11, 5)
     meta, lower = QNet.from_state_dict(meta_sd, device=dev), QNet.from_state_dict(lower_sd, device=dev)
     env = MergeVecEnv(n, device=dev)
     for k in range(burn):
