@@ -9,9 +9,13 @@ episode statistics. Envs are sharded across ranks (rank r owns global envs [r E,
 Philox keyed by the global index), with no collective inside the timed loop; after it, one
 RCCL all-gather of each rank's 48-byte statistics totals (timed separately).
 
-Before the W warm-up steps the batch is burned in (--burn-in steps, untimed, fused rollout
-launches, then --burn-in-launches untimed one-step launches) so the timed window sees the
-steady state: envs finishing every step, autoreset, final observations and statistics writes.
+Before the W warm-up steps the batch is burned in (--burn-in-launches untimed one-step launches
+of the same kernel, optionally preceded by --burn-in steps of fused rollouts) so the timed window
+sees the steady state: envs finishing every step, autoreset, final observations and statistics
+writes. The burn-in runs the step kernel itself by default: after a rollout burn-in (VALU-heavy)
+plus 48 step launches, a 20-launch window measured 26.2-26.4 us per launch against 25.1-25.6
+after 1,072 step launches, the env state at the window being the same (tools/gpu_burnin_ab.sh,
+profiles/r02/ab/burnin/).
 The K timed launches are host launches (the host enqueues one in ~4 us, the kernel takes ~25),
 or a HIP-graph replay with --graph 1.
 
@@ -53,11 +57,12 @@ def parse():
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, one GPU per rank) or gloo (multi-rank rehearsal, ranks may share a GPU)")
-    ap.add_argument("--burn-in", type=int, default=1024,
-                    help="untimed steps (16-step fused rollouts) before the warm-up: steady state")
-    ap.add_argument("--burn-in-launches", type=int, default=48,
-                    help="untimed one-step launches closing the burn-in, so the clocks have left the "
-                         "rollout kernel's regime before the warm-up (tools/window_probe.py)")
+    ap.add_argument("--burn-in", type=int, default=0,
+                    help="untimed steps as 16-step fused rollouts before the burn-in launches (faster "
+                         "to run, but the window after them starts in the rollout kernel's regime)")
+    ap.add_argument("--burn-in-launches", type=int, default=1072,
+                    help="untimed one-step launches before the warm-up: the steady state (episodes "
+                         "need >= 106 steps, the mean is ~210) reached by the timed kernel itself")
     ap.add_argument("--graph", type=int, default=0,
                     help="1: replay the K timed launches from a HIP graph captured before the window "
                          "(at K = 20 host launches measured 1.04x event time on the wall, the graph's "
