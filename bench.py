@@ -83,9 +83,11 @@ def parse():
                     help="T of the fused rollout leg (mg_rollout_random); 0 disables it")
     ap.add_argument("--rollout-launches", type=int, default=200,
                     help="timed launches of the rollout leg (after --leg-warmup untimed ones)")
-    ap.add_argument("--leg-warmup", type=int, default=10,
-                    help="untimed launches before each rollout / Q-net leg: a compute-heavy kernel after the "
-                         "memory-bound step leg first runs through a clock transient (tools/rollout_sustain.py)")
+    ap.add_argument("--leg-warmup", type=int, default=60,
+                    help="untimed launches before each rollout / Q-net / h-DQN leg: a compute-heavy kernel "
+                         "after the memory-bound step leg first runs through a clock transient "
+                         "(tools/rollout_sustain.py); 10 left part of it in the window: rollout 11.1 vs "
+                         "10.5 us per step, config-5 ego 51.4-52.1 vs 49.6-49.7 (tools/gpu_legwarm_ab.sh)")
     ap.add_argument("--replay-stores", type=int, default=20,
                     help="timed mg_replay_store calls of the replay-memory leg; 0 disables it")
     ap.add_argument("--qnet-launches", type=int, default=40,
