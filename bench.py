@@ -7,7 +7,7 @@ A step = one launch of mg_step_random over this rank's 2^20 envs: Philox actions
 players drawn on the device, the full reference step (merging_env.py:138-195), autoreset,
 episode statistics. Envs are sharded across ranks (rank r owns global envs [r E, (r+1) E),
 Philox keyed by the global index), with no collective inside the timed loop; after it, one
-RCCL all-gather of each rank's 48-byte statistics totals (timed separately).
+RCCL all-gather of each rank's 72-byte statistics totals (timed separately).
 
 Before the W warm-up steps the batch is burned in (--burn-in-launches untimed one-step launches
 of the same kernel, optionally preceded by --burn-in steps of fused rollouts) so the timed window
@@ -44,6 +44,11 @@ sys.path.insert(0, os.path.join(ROOT, "merging-gym_amd"))
 # (final_obs / episode-statistics writes happen only for the ~0.5 % of envs that finish
 #  in a step and are not counted.)
 BYTES_PER_ENV_STEP = 152
+# SURVEY.md 8(d)'s count for device-drawn actions: fp32 returns (8 B, not 16, each way), no
+# action write-back, separate done / winner bytes: 136 B. The 16-B fp64-return premium is this
+# build's choice (r{1,2}_accumulate stay the reference's fp64 sums);
+# roofline.frac_8d reports the line against 136 B.
+BYTES_PER_ENV_STEP_8D = 136
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 KERNEL_NAME = "step_kernel<1, false>"
 
@@ -73,7 +78,7 @@ def parse():
                     help="envs of the post-Infinity-Cache leg (N = 1 only); 0 disables it")
     ap.add_argument("--size2-steps", type=int, default=100)
     ap.add_argument("--gather", choices=("summary", "per-env"), default="summary",
-                    help="statistics collective: 48-byte totals per rank, or every env's row")
+                    help="statistics collective: 72-byte totals per rank, or every env's row")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="per CPU-baseline leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="skip per-launch HIP events")
@@ -203,13 +208,14 @@ def size2_leg(args, torch):
     torch.cuda.synchronize()
     kernel_ms = ev0.elapsed_time(ev1) / args.size2_steps
     achieved = BYTES_PER_ENV_STEP * E / (kernel_ms * 1e-3) / 1e9
+    frac_8d = BYTES_PER_ENV_STEP_8D * E / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS
     completed = int(env.counts[:, 0].sum())
     del env
     torch.cuda.empty_cache()
     return {"envs": E, "steps": args.size2_steps, "burn_in_steps": args.burn_in + max(5, args.burn_in_launches),
             "kernel_ms": kernel_ms,
             "value": E / (kernel_ms * 1e-3), "unit": "env-steps/s", "achieved": achieved, "peak": HBM_PEAK_GBPS,
-            "unit_bw": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": load_pmc(E),
+            "unit_bw": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "frac_8d": frac_8d, "traffic": load_pmc(E),
             "episodes_completed": completed}
 
 
@@ -321,8 +327,12 @@ HDQN_USEFUL_FLOP = 2 * (10 * 200 + 200 * 100 + 100 * 3) + 2 * (11 * 200 + 200 * 
 def hdqn_leg(env, args, world, dist, torch):
     """hdqn.py's acting loop (scripts/hdqn.py:280-323) fused with the env step (mg_rollout_hdqn):
     per env-step Goal_DQN's meta-net (10 -> 3) on the next state and the lower-level Net
-    (11 -> 5) on the goal state, both bf16 MFMA, L0 opponent. The nets are seeded draws with
-    hdqn.py:41-47's initialisation (no h-DQN checkpoint ships with the reference)."""
+    (11 -> 5) on the goal state, both bf16 MFMA, L0 opponent. No h-DQN checkpoint ships with the
+    reference, so the nets are seeded draws with torch.nn.Linear's default (signed) initialisation,
+    U(-1/sqrt(in), 1/sqrt(in)) for weights and biases -- as the GPU tests use: their choices vary
+    from env to env (hdqn.py:41-47's uniform(0, 1) weights pick one action for > 90 % of inputs,
+    tests/test_hdqn_test_nets.py, which would measure an almost constant policy). The goal-break
+    rate (the share of env-steps that end an inner loop, :322) is reported beside it."""
     import numpy as np
 
     from merging_gym.policy import NUM_GOALS, QNet
@@ -332,7 +342,7 @@ def hdqn_leg(env, args, world, dist, torch):
     def net(i, o):
         sd = {}
         for name, (a, b) in zip(("fc1", "fc2", "out"), [(200, i), (100, 200), (o, 100)]):
-            sd[f"{name}.weight"] = rng.uniform(0, 1, (a, b)).astype(np.float32)
+            sd[f"{name}.weight"] = rng.uniform(-b ** -0.5, b ** -0.5, (a, b)).astype(np.float32)
             sd[f"{name}.bias"] = rng.uniform(-b ** -0.5, b ** -0.5, a).astype(np.float32)
         return QNet.from_state_dict(sd, device=env.device)
 
@@ -358,6 +368,14 @@ def hdqn_leg(env, args, world, dist, torch):
     elapsed = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / L
     per_s = E * T / (kernel_ms * 1e-3)
+    # untimed: one launch with Goal_DQN's columns, for the inner-loop break rate (:322)
+    tr = env.rollout_hdqn(T, meta, lower, args.seed, first_step=k, final_observation=False, goal_memory=True)
+    k += T
+    nb = tr["no_break"].cpu().numpy()  # [T, ceil(E/64)] bits: set where the step did not end the inner loop
+    cont = int(np.unpackbits(nb.view(np.uint8), bitorder="little").reshape(T, -1)[:, :E].sum())
+    break_rate = 1.0 - cont / (T * E)
+    greedy_goal_spread = torch.bincount(tr["next_goal"].flatten().to(torch.int64), minlength=NUM_GOALS)
+    greedy_goal_spread = (greedy_goal_spread.double() / greedy_goal_spread.sum()).tolist()
 
     # with hdqn.py's lower-level memory (HDQN.store_transition, :316, every transition): the
     # store fused into the launch vs the rollout followed by mg_replay_store from its outputs
@@ -427,7 +445,9 @@ def hdqn_leg(env, args, world, dist, torch):
             "dtype": "bf16 (fp32 accumulate)", "value": world * E * T * L / elapsed, "unit": "env-steps/s",
             "ms_per_step": elapsed / (L * T) * 1e3, "kernel_ms_mean": kernel_ms,
             "useful_tflops": HDQN_USEFUL_FLOP * per_s / 1e12, "peak_tflops": MFMA_BF16_PEAK_TFLOPS,
-            "frac_useful": HDQN_USEFUL_FLOP * per_s / 1e12 / MFMA_BF16_PEAK_TFLOPS}
+            "frac_useful": HDQN_USEFUL_FLOP * per_s / 1e12 / MFMA_BF16_PEAK_TFLOPS,
+            "nets": "seeded, torch.nn.Linear default init U(-1/sqrt(in), 1/sqrt(in)) (signed)",
+            "goal_break_rate_per_step": break_rate, "next_goal_share": greedy_goal_spread}
 
 
 def replay_algorithmic_bytes(n, T, kept, done_rows, capacity):
@@ -636,27 +656,34 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kernel_ms_max = float(t[0]), float(t[1])
 
-    # episode statistics (every episode completed since the window opened): each rank's 48-byte
-    # totals all-gathered over RCCL (xGMI) and reduced on every rank, outside the timed loop
-    from merging_gym.distributed import (PARTIAL_BYTES, gather_episode_stats, gather_episode_summary,
-                                         summarize)
+    # episode statistics (every episode completed since the window opened), the quantities the
+    # reference's scripts log: each rank reduces its shard on the device to 72 bytes of totals,
+    # which one RCCL all-gather (xGMI) brings to every rank, outside the timed loop. The device
+    # reduction and the collective are timed apart; at world size 1 there is no collective.
+    from merging_gym.distributed import (NUM_COUNTS, NUM_RETURNS, PARTIAL_BYTES, gather_episode_stats,
+                                         gather_episode_summary, summarize)
 
+    timings = {}
     torch.cuda.synchronize()
-    g0 = time.perf_counter()
     if world > 1 and args.gather == "per-env":
-        episodes = summarize(*gather_episode_stats(env.ret_sum, env.counts))
-        payload = E * 32
-    elif world > 1:
-        episodes = gather_episode_summary(env.ret_sum, env.counts)
-        payload = PARTIAL_BYTES
+        g0 = time.perf_counter()
+        rows = gather_episode_stats(env.returns, env.counts)
+        torch.cuda.synchronize()
+        timings["allgather_ms"] = (time.perf_counter() - g0) * 1e3
+        g0 = time.perf_counter()
+        episodes = summarize(*rows)
+        timings["reduce_ms"] = (time.perf_counter() - g0) * 1e3
+        payload = E * (NUM_RETURNS + NUM_COUNTS // 2) * 8
     else:
-        episodes = summarize(env.ret_sum, env.counts)
-        payload = 0
-    torch.cuda.synchronize()
-    gather_ms = (time.perf_counter() - g0) * 1e3
-    episodes.update(allgather_ms=gather_ms, allgather_bytes_per_rank=payload,
+        episodes = gather_episode_summary(env.returns, env.counts, timings=timings)
+        payload = PARTIAL_BYTES if world > 1 else 0
+    episodes.update(allgather_ms=timings.get("allgather_ms"), reduce_ms=timings.get("reduce_ms"),
+                    allgather_bytes_per_rank=payload,
                     completed_in_timed_window_rank0=completed_in_window,
-                    counted_since="start of the timed window (statistics cleared after the warm-up)")
+                    counted_since="start of the timed window (statistics cleared after the warm-up)",
+                    logged_as=("mean_return_ego / win_rate_hdqn: hdqn.py:312, :342 (terminal observation); "
+                               "mean_ep_reward_main / win_rate_main: main.py:209-211, :225 (winner-filtered "
+                               "reward, pre-terminal observation); ego_first_rate: winner == 1"))
 
     # the step kernel past the Infinity Cache first, while device memory is unfragmented: allocated
     # after the Q-net and h-DQN legs (gigabytes of trajectory buffers and rings, some freed) the
@@ -708,6 +735,12 @@ def main():
                          "frac": (achieved / HBM_PEAK_GBPS) if achieved else None,
                          "traffic": pmc, "kernel": KERNEL_NAME,
                          "bytes_per_env_step": BYTES_PER_ENV_STEP,
+                         "frac_8d": (BYTES_PER_ENV_STEP_8D * E / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS
+                                     if kernel_ms else None),
+                         "bytes_per_env_step_8d": BYTES_PER_ENV_STEP_8D,
+                         "bytes_note": ("frac: this layout's 152 B (fp64 returns 16 B each way, the action "
+                                        "write-back 2 B, done / collision / actions as one 4-B record); "
+                                        "frac_8d: SURVEY.md 8(d)'s 136 B (fp32 returns)"),
                          "kernel_ms_mean": kernel_ms, "kernel_ms_mean_max_rank": kernel_ms_max,
                          "timing": ("HIP events recorded on the launch stream around the K timed launches "
                                     f"({'one HIP-graph replay' if args.graph else 'K host launches'}), / K"),

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 16
+#define MG_ABI_VERSION 17
 #define MG_OBS_DIM 10   /* merging_env.py:75 observation_shape = (10) */
 #define MG_NUM_ACTIONS 5 /* merging_env.py:101-102 action_dict / Discrete(5) */
 #define MG_ACTION_NONE (-1) /* action2=None: the constant-speed "L0" opponent, merging_env.py:152 */
@@ -101,14 +101,19 @@ typedef struct mg_params {
   int32_t _pad;
   double inv_R;        /* 1 / R, rounded: the kernel divides by R (and by qp_nz) with an
                           FMA-corrected reciprocal multiply (still correctly rounded) */
-  /* mpc_1d's QP (scripts/helper.py:152-191) as the Goldfarb-Idnani solver quadprog runs it
-   * (helper.py:182): with P = D'D + 0.01 I factored by Cholesky and n = A[1] the equality's
-   * normal, z = P^-1 n and the first control is u0 = (b / n'z) * z0, b = vt - v0. The two
-   * constants depend only on prediction_t; mg_params_default computes them the solver's way,
-   * so the kernel's u0 carries the solver's rounding, not that of the closed form (vt-v0)/t. */
-  double qp_nz;        /* n'P^-1 n = 90.00000000000153 (t = 3) */
-  double qp_z0;        /* (P^-1 n)[0] = 30.000000000000544 */
+  /* mpc_1d's QP (scripts/helper.py:152-191) as quadprog 0.1.11's qpgen2 (the Goldfarb-Idnani
+   * dual method, reached through qpsolvers 1.8.0 at helper.py:182) runs it: P = R'R by LINPACK
+   * dpofa, J = R^-1 by dpori, then for the one equality (normal n = A[1], b = vt - v0, its sign
+   * folded into n when the residual is positive) d = J'n, z = J d, t = |b| / z'n and
+   * u = 0 + t z; a residual |b| < vsmall counts as satisfied (u = 0). So u0 = (b / z'n) * z0
+   * with the two constants below computed in that operation order by mg_params_default (ABI
+   * 17; ABI <= 16 used Cholesky substitution, an ulp apart). Restated from the published
+   * algorithm -- quadprog is not importable here, so bit parity with it is unpinned. */
+  double qp_nz;        /* z'n = 90.0000000000015 (t = 3) */
+  double qp_z0;        /* z[0] = 30.000000000000533 */
   double qp_inv_nz;    /* 1 / qp_nz, rounded */
+  double qp_vsmall;    /* qpgen2's vsmall: the first 1e-60 * 2^k with 1 + 0.1 vsmall > 1 and
+                          1 + 0.2 vsmall > 1 (1.4272476927059598e-15) */
 } mg_params;
 
 /* Per-env state, struct of arrays, n entries each (device pointers). */
@@ -202,17 +207,34 @@ typedef struct mg_transitions {
                                goal NULL, skip_ego_won ignored */
 } mg_transitions;
 
-/* Completed-episode statistics of one env, updated only when it finishes (MG_AUTORESET):
- * the returns and counts the reference's training scripts log (hdqn.py:330-346,
- * main.py:221-228). One 32-byte record per env, so a finishing env's read-modify-write touches
- * one DRAM sector: as two arrays ([n,2] f64 + [n,4] u32, ABI <= 7) those scattered updates cost
- * the one-step kernel 12 % of its time at 2^22 envs (tools/steady_probe.py). */
+/* Completed-episode statistics of one env, updated when it finishes (MG_AUTORESET): the
+ * quantities the reference's training scripts log per episode, summed over the env's episodes
+ * (ABI 17). One 64-byte record per env, so a finishing env's read-modify-write stays within one
+ * cache line: as separate arrays (ABI <= 7) those scattered updates cost the one-step kernel 12 %
+ * of its time at 2^22 envs (tools/steady_probe.py).
+ *   main.py:189-227   ep_reward sums the ego's reward only over steps after which
+ *                     `env.winner is not 1` (:209-211); win_count counts `state[8] > state[3]`
+ *                     on the observation the episode's LAST step acted on (`state = next_state`
+ *                     is skipped at the :218-220 break), i.e. END_POINT - p2 > END_POINT - p1
+ *                     in fp64 on the state before that step;
+ *   hdqn.py:276-346   ep_reward is every step's reward (= r1_accumulate, :312); win_count tests
+ *                     `state[8] > state[3]` on the terminal observation (state = next_state at
+ *                     :320 before the break).
+ * winner never returns to 1 once it is 2, and stays 1 once set, so main.py's filtered sum is
+ * r1_accumulate as it stood before the step on which the ego arrived first (or the whole
+ * r1_accumulate when it never did): the kernels keep that value in ret1_pending. */
 typedef struct mg_episode_stats {
-  double ret[2];        /* sum of completed-episode returns (ego, opponent) */
+  double ret[2];        /* sum of completed-episode returns r{1,2}_accumulate (hdqn.py's ep_reward) */
+  double ret_main;      /* sum of main.py's winner-filtered ep_reward */
+  double ret1_pending;  /* scratch (per env): r1_accumulate before the current episode's ego-first
+                           arrival step; read only while winner == 1 */
   uint32_t episodes;    /* completed episodes */
   uint32_t collisions;  /* of which ended in a collision */
   uint32_t ego_first;   /* of which the ego arrived first (winner == 1) */
   uint32_t steps;       /* total steps of the completed episodes */
+  uint32_t win_main;    /* main.py:225's win test on the pre-terminal observation */
+  uint32_t win_hdqn;    /* hdqn.py:342's win test on the terminal observation */
+  uint32_t reserved[2]; /* 0 */
 } mg_episode_stats;
 
 typedef struct mg_stats {
@@ -321,7 +343,9 @@ typedef struct mg_hdqn_traj {
  * chooses the next goal epsilon-greedily on the next state, goal_status gives the intrinsic
  * reward, and a fresh goal is chosen when that goal is already reached or the episode ended
  * (:320-322, :278-283; reset_goal = the meta-net's argmax on the reset observation, which the
- * caller computes once). goal [n] int8 holds each env's current goal across launches (< 0: none
+ * caller computes once). goal_status is evaluated on the fp64 x2 - x1 and v2 of the state (ABI 17;
+ * see mg_goal_status). flags must include MG_AUTORESET (hdqn.py resets at every episode end, :277;
+ * ABI 17 rejects a launch without it). goal [n] int8 holds each env's current goal across launches (< 0: none
  * yet -- chosen by the meta-net at the first step). Random draws: Philox4x32-10 with key seed,
  * counter (env_offset + i, first_step + t) for the action and next goal (x, y, z, w = explore,
  * action, explore, goal) and counter ((env_offset + i) ^ 2^63, first_step + t) for a fresh goal
@@ -342,7 +366,8 @@ typedef struct mg_hdqn_traj {
  * w goal of a fresh opponent goal at step t + 1 (the launch's first at step first_step - 1).
  * goal_op [n] int8 (required for modes 2 and 3, else ignored) holds each env's opponent goal across
  * launches like goal. ext_acc [n] double (required with htraj->ext_reward or no_break, ABI 15)
- * holds each env's extrinsic reward since its inner loop began, across launches (0 at a break).
+ * holds each env's extrinsic reward since its inner loop began, across launches (0 at a break);
+ * whenever it is given the sums are kept, with or without those outputs (ABI 17).
  * ring_rows (optional, 16-byte aligned [ring_capacity, 24] fp32, with ring_counter: one device
  * uint64): the launch also appends every transition to hdqn.py's lower-level memory
  * (HDQN.store_transition, :316, which stores them all) -- row [goal, s, a, r, next_goal, s'] of
@@ -357,6 +382,12 @@ int mg_rollout_hdqn(const mg_params* params, const mg_state* state, const mg_tra
                     uint64_t greedy_threshold, int32_t opponent_mode, const void* opp_meta_net,
                     const void* opp_lower_net, float* ring_rows,
                     uint64_t* ring_counter, int64_t ring_capacity, uint32_t flags, void* stream);
+
+/* status[i] = goal_status on (dx1[i], v2[i]) in fp64 (ABI 17): 0 if dx1 < -0.5 v2, 1 if dx1 < 0.5 v2,
+ * else 2 -- replaces hdqn.py's goal_status (scripts/hdqn.py:223-236, dx1 = state[0], v2 = state[9]),
+ * the same device function mg_rollout_hdqn evaluates on each step's fp64 x2 - x1 and v2 for the
+ * intrinsic reward (:314) and the inner-loop break (:322). Device pointers, stream-ordered. */
+int mg_goal_status(const double* dx1, const double* v2, int8_t* status, int64_t n, void* stream);
 
 /* ---- replay memory (scripts/main.py:91-92, :115-119, :130-135) --------------------------------
  * rows: [capacity, row_floats] fp32 device buffer, row = [s(10), a, r, s'(10)] like

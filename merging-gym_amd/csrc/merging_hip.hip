@@ -32,59 +32,9 @@
 
 namespace {
 
-// Compile-time knobs (A/B-tested in one process by tools/ab_kernels.py; defaults = shipped).
-#ifndef MG_FAST_SINCOS
-#define MG_FAST_SINCOS 1  // short polynomial for |theta| < 1/16 (every live-episode state)
-#endif
-#ifndef MG_NT_STORES
-#define MG_NT_STORES 1    // non-temporal stores for the per-step outputs
-#endif
-#ifndef MG_BLOCK
-#define MG_BLOCK 256
-#endif
-#ifndef MG_REPLAY_WIDE_STORES
-#define MG_REPLAY_WIDE_STORES 1  // replay store: 16-byte stores over each contiguous run of rows
-#endif
-#ifndef MG_REPLAY_TCHUNK
-#define MG_REPLAY_TCHUNK 2  // replay store: steps one block walks (obs carried in registers)
-#endif
-#ifndef MG_REPLAY_PREFETCH
-#define MG_REPLAY_PREFETCH 1  // replay store: next step's obs row loaded before this step's work
-#endif
-#ifndef MG_COPY_FULL_WAVE
-#define MG_COPY_FULL_WAVE 1  // wave_copy_rows: unrolled path for a full 64-row wave
-#endif
-#ifndef MG_SINCOS_COLD
-#define MG_SINCOS_COLD 1  // the |t| >= 1/16 sincos fallback as an out-of-line call
-#endif
-#ifndef MG_QNET_STAMPS
-#define MG_QNET_STAMPS 0  // diagnostic build: phase clocks of the specialised Q-net kernel
-#endif
-#ifndef MG_QNET_SWP
-#define MG_QNET_SWP 1  // Q-net waves of the specialised kernel: software-pipelined hidden tiles
-#endif
-#ifndef MG_QNET_WS_ENV_WAVES
-// specialised kernel: env waves per block. 4 = 512-env blocks (shipped); 8 = 1024-env blocks,
-// 3 waves per SIMD, which needs a Q-net wave within 168 VGPRs -- measured 19 % slower with the
-// unpaired forward that fits
-#define MG_QNET_WS_ENV_WAVES 4
-#endif
-#ifndef MG_QNET_WS_ILP
-// specialised kernel: envs each env-wave lane steps per phase, in lockstep (independent fp64
-// chains interleaved in one instruction stream); the Q-net waves take ILP tiles per phase
-#define MG_QNET_WS_ILP 2
-#endif
-#ifndef MG_QNET_WS
-#define MG_QNET_WS 1  // Q-net rollout: specialised waves (4 Q-net + 4 env) instead of uniform ones
-#endif
-#ifndef MG_QNET_BLOCK
-#define MG_QNET_BLOCK 512  // Q-net rollout: threads per block (one LDS copy of the net each)
-#endif
-#ifndef MG_QNET_WAVES_PER_EU
-#define MG_QNET_WAVES_PER_EU 2  // Q-net rollout: waves per SIMD the register budget is cut for
-#endif
-
-constexpr int kBlock = MG_BLOCK;  // 4 waves of 64 by default
+// One build, no compile-time variants: every alternative measured against the shipped choice
+// (profiles/r01, profiles/r02/ab) was removed from the product source once it lost.
+constexpr int kBlock = 256;  // 4 waves of 64 (128 and 512 measured within 0.8 %)
 constexpr int kObs = MG_OBS_DIM;
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -95,11 +45,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // next step reads it back (write-through or non-temporal state stores measured 0 to +4 %).
 template <class T>
 __device__ __forceinline__ void st_out(T* p, T v) {
-#if MG_NT_STORES
   __builtin_nontemporal_store(v, p);
-#else
-  *p = v;
-#endif
 }
 
 template <class T>
@@ -129,13 +75,9 @@ __device__ __forceinline__ double div_const(double x, double d, double inv) {
 // The device library's sincos for |t| >= 1/16 (only reached off the live-episode range, e.g.
 // stepping far past done). Kept out of line: inlined, the compiler hoists its polynomial
 // constants into VGPRs for the whole step loop of the T-step kernels, which then spill.
-#if MG_SINCOS_COLD
 __device__ __attribute__((noinline)) void sincos_cold(double t, double* s, double* c) {
   sincos(t, s, c);
 }
-#else
-__device__ __forceinline__ void sincos_cold(double t, double* s, double* c) { sincos(t, s, c); }
-#endif
 
 // the polynomial branch (|t| < 1/16)
 __device__ __forceinline__ void sincos_poly(double t, double& s, double& c) {
@@ -153,15 +95,11 @@ __device__ __forceinline__ void sincos_poly(double t, double& s, double& c) {
 }
 
 __device__ __forceinline__ void arc_sincos(double t, double& s, double& c) {
-#if MG_FAST_SINCOS
   if (fabs(t) < 0.0625) {
     sincos_poly(t, s, c);
     return;
   }
   sincos_cold(t, &s, &c);
-#else
-  sincos(t, &s, &c);
-#endif
 }
 
 // arc_sincos of M angles: when every one is in the polynomial's range (the usual case) the M
@@ -169,7 +107,6 @@ __device__ __forceinline__ void arc_sincos(double t, double& s, double& c) {
 // takes arc_sincos's own branch. Same results as M arc_sincos calls.
 template <int M>
 __device__ __forceinline__ void arc_sincos_n(const double (&t)[M], double (&s)[M], double (&c)[M]) {
-#if MG_FAST_SINCOS
   bool fast = true;
 #pragma unroll
   for (int k = 0; k < M; ++k) fast = fast && fabs(t[k]) < 0.0625;
@@ -178,7 +115,6 @@ __device__ __forceinline__ void arc_sincos_n(const double (&t)[M], double (&s)[M
     for (int k = 0; k < M; ++k) sincos_poly(t[k], s[k], c[k]);
     return;
   }
-#endif
 #pragma unroll
   for (int k = 0; k < M; ++k) arc_sincos(t[k], s[k], c[k]);
 }
@@ -250,11 +186,18 @@ __device__ __forceinline__ void observe(const mg_params& P, double p1, double v1
 }
 
 template <class OT>
-__device__ __forceinline__ void reset_obs(const mg_params& P, OT (&o)[kObs]) {
+__device__ __forceinline__ void reset_obs(const mg_params& P, OT (&o)[kObs], double* dx1 = nullptr) {
   double x1, y1, x2, y2;
   lon2coord(P, P.start_point, true, x1, y1);
   lon2coord(P, P.start_point, false, x2, y2);
   observe(P, P.start_point, P.start_vel, P.start_point, P.start_vel, x1, y1, x2, y2, o);
+  if (dx1) *dx1 = x2 - x1;
+}
+
+// goal_status (scripts/hdqn.py:223-236) on the reference's fp64 values: dx1 = state[0] = x2 - x1,
+// v2 = state[9] (an int 0 after max(0, ...) compares as 0.0). 0: dx1 < -v2/2, 1: dx1 < v2/2, else 2.
+__device__ __forceinline__ int goal_status(double dx1, double v2) {
+  return dx1 < -0.5 * v2 ? 0 : (dx1 < 0.5 * v2 ? 1 : 2);
 }
 
 // Philox4x32-10 (Salmon et al., SC'11 "Parallel random numbers: as easy as 1, 2, 3").
@@ -319,19 +262,16 @@ __device__ __forceinline__ void store_env(const mg_state& S, int64_t i, const En
 // The observation a step hands back, held as fp32: every batched output is fp32, and fp32
 // here frees 10 VGPRs (66 -> fewer in the one-step kernel). The single-env record, which returns
 // the reference's fp64 floats, recomputes its observation in fp64 from the state.
-#ifndef MG_OBS_F32
-#define MG_OBS_F32 1
-#endif
-#if MG_OBS_F32
 typedef float obs_t;
-#else
-typedef double obs_t;
-#endif
 
 struct StepOut {
   obs_t o[kObs];  // observation (the reset observation once autoreset has fired)
   double r1, r2, acc1, acc2;
+  double dx1;     // x2 - x1 of o in fp64 (hdqn.py goal_status's dx1; the reset one after autoreset)
+  double ret_pre; // r1_accumulate before this step (read where first1)
   bool done, coll, r1_int, r2_int, v1_int, v2_int;
+  bool first1;    // the ego arrived first on this step (winner None -> 1, merging_env.py:164-166)
+  bool win_pre;   // main.py:225's END_POINT - p2 > END_POINT - p1 on the state this step acted on
   int bad;  // 1: action1 invalid, 2: action2 invalid (the reference's KeyError)
 };
 
@@ -383,14 +323,18 @@ __device__ __forceinline__ void env_clock(const mg_params& P, Env& e) {
 }
 
 // mpc_1d (helper.py:152-191): min u'(D'D + 0.01 I)u s.t. A[1] u = b, b = vt - v0 (only the
-// velocity row of the constraint reaches solve_qp, :172-173, :182). The dual active-set solver
-// starts at the unconstrained minimiser u = 0 and adds the one equality in a single step,
-// u = (b / n'z) z with z = P^-1 n; action() = u[0]. n'z and z[0] are per-launch constants
-// (mg_params.qp_nz / qp_z0, computed by mg_params_default the solver's way), so this is two
-// correctly rounded operations with the solver's own rounding. (Mathematically u0 = b / t,
-// since D.1 = 0; evaluating that closed form instead moves u0 by an ulp in ~97 % of steps.)
+// velocity row of the constraint reaches solve_qp, :172-173, :182). quadprog's dual active-set
+// method starts at the unconstrained minimiser u = 0 and adds the one equality in a single step,
+// u = (b / z'n) z with z = J J'n, J = R^-1; action() = u[0]. z'n and z[0] are per-launch
+// constants (mg_params.qp_nz / qp_z0, computed by mg_params_default in qpgen2's operation order),
+// so this is two correctly rounded operations with the solver's own rounding; a residual |b| below
+// qpgen2's vsmall counts as already satisfied and leaves the unconstrained minimiser u = -0.0 (dposl
+// of a = -q, q = 0). (Mathematically u0 = b / t, since
+// D.1 = 0; evaluating that closed form instead moves u0 by an ulp in most steps.)
 __device__ __forceinline__ double mpc_acc(const mg_params& P, int a, double v) {
-  return div_const(P.action_speed[a] - v, P.qp_nz, P.qp_inv_nz) * P.qp_z0;
+  const double b = P.action_speed[a] - v;
+  const double u = div_const(b, P.qp_nz, P.qp_inv_nz) * P.qp_z0;
+  return fabs(b) < P.qp_vsmall ? -0.0 : u;  // dposl's -0.0 (a = -q = -0.0): nothing violated
 }
 
 // v = max(0, v + acc*dT) (an int 0 when the max picks 0), p += v*dT  (:149-150, :153-154)
@@ -410,6 +354,9 @@ __device__ __forceinline__ void score_step(const mg_params& P, Env& e, double x1
 // its zeroed outputs are not compiled in.
 template <bool CHECKED = true>
 __device__ __forceinline__ void env_step(const mg_params& P, Env& e, int a1, int a2, StepOut& r) {
+  r.win_pre = (P.end_point - e.p2) > (P.end_point - e.p1);  // main.py:225 on the state acted on
+  r.first1 = false;
+  r.dx1 = 0.0;
   env_clock(P, e);
   const bool bad1 = CHECKED && !valid_action(a1);
   const bool bad2 = CHECKED && !(a2 == MG_ACTION_NONE || valid_action(a2));
@@ -454,6 +401,8 @@ __device__ __forceinline__ void env_step_lockstep(const mg_params& P, Env (&e)[N
     bad[j] = bad1 || bad2;
     r[j].bad = (bad1 ? 1 : 0) | (bad2 ? 2 : 0);
     r[j].r1_int = r[j].r2_int = false;
+    r[j].win_pre = (P.end_point - e[j].p2) > (P.end_point - e[j].p1);
+    r[j].first1 = false;
     env_clock(P, e[j]);
     const double acc1 = mpc_acc(P, bad1 ? 0 : a1[j], e[j].v1);
     r[j].acc1 = bad1 ? 0.0 : acc1;
@@ -491,6 +440,8 @@ __device__ __forceinline__ void env_step_lockstep(const mg_params& P, Env (&e)[N
 __device__ __forceinline__ void score_step(const mg_params& P, Env& e, double x1, double y1,
                                            double x2, double y2, StepOut& r, bool frozen) {
   observe(P, e.p1, e.v1, e.p2, e.v2, x1, y1, x2, y2, r.o);
+  r.dx1 = x2 - x1;
+  r.ret_pre = e.ret1;
   if (frozen) {
 #pragma unroll
     for (int k = 0; k < kObs; ++k) r.o[k] = 0.0;
@@ -505,6 +456,7 @@ __device__ __forceinline__ void score_step(const mg_params& P, Env& e, double x1
     if (e.winner == 0) {
       e.winner = 1;
       r1 += P.r_first;
+      r.first1 = true;
     } else if (e.winner == 1) {
       r1 = 0.0;
       r.r1_int = true;
@@ -542,61 +494,113 @@ __device__ __forceinline__ void score_step(const mg_params& P, Env& e, double x1
   r.done = !frozen && e.done;
 }
 
-// Completed-episode statistics of one env held in registers for a multi-step launch: loaded
-// once, accumulated in the same order as the per-step read-modify-write (so bit-identical),
-// stored once if anything finished. A finishing lane then never waits on a global load.
+// Completed-episode statistics (mg_episode_stats) of one env held in registers for a multi-step
+// launch: the fp64 sums and ret1_pending are loaded once and accumulated in the same order as the
+// per-step read-modify-write (so bit-identical); the counts are this launch's increments, added
+// to the record once at the end. A finishing lane then never waits on a global load.
+// The counts are 16-bit fields of three words (a launch finishes at most num_steps <= 65535
+// episodes per env, mg_rollout_random checks it): two VGPRs fewer, which keeps the rollout
+// kernel within 128 VGPRs (4 waves per SIMD).
 struct EpStats {
-  double r1, r2;
-  uint4 c;
-  bool dirty;
+  double r1, r2, rm, pend;
+  uint32_t ep_coll;   // episodes | collisions << 16
+  uint32_t ego_wm;    // ego_first | win_main << 16
+  uint32_t wh;        // win_hdqn
+  uint32_t steps;
+  bool dirty_f, dirty_c;  // the fp64 half / the counts changed
 };
 
+// the record as 4 x 16 bytes: {ret[0], ret[1]}, {ret_main, ret1_pending}, counts 0-3, counts 4-7
+__device__ __forceinline__ double2* stats_f64(const mg_stats& St, int64_t i) {
+  return reinterpret_cast<double2*>(St.rec + i);
+}
+__device__ __forceinline__ uint4* stats_u32(const mg_stats& St, int64_t i) {
+  return reinterpret_cast<uint4*>(St.rec + i) + 2;
+}
+
 __device__ __forceinline__ void stats_load(const mg_stats& St, int64_t i, EpStats& s) {
-  s.dirty = false;
-  s.r1 = s.r2 = 0.0;
-  s.c = make_uint4(0u, 0u, 0u, 0u);
+  s.dirty_f = s.dirty_c = false;
+  s.r1 = s.r2 = s.rm = s.pend = 0.0;
+  s.ep_coll = s.ego_wm = s.wh = s.steps = 0u;
   if (St.rec) {
-    const double2 r = reinterpret_cast<const double2*>(St.rec + i)[0];
-    s.r1 = r.x;
-    s.r2 = r.y;
-    s.c = reinterpret_cast<const uint4*>(St.rec + i)[1];
+    const double2 a = stats_f64(St, i)[0], b = stats_f64(St, i)[1];
+    s.r1 = a.x;
+    s.r2 = a.y;
+    s.rm = b.x;
+    s.pend = b.y;
   }
 }
 
 __device__ __forceinline__ void stats_store(const mg_stats& St, int64_t i, const EpStats& s) {
-  if (!s.dirty || !St.rec) return;
-  reinterpret_cast<double2*>(St.rec + i)[0] = make_double2(s.r1, s.r2);
-  reinterpret_cast<uint4*>(St.rec + i)[1] = s.c;
+  if (!St.rec) return;
+  if (s.dirty_f) {
+    stats_f64(St, i)[0] = make_double2(s.r1, s.r2);
+    stats_f64(St, i)[1] = make_double2(s.rm, s.pend);
+  }
+  if (s.dirty_c) {  // once per launch: the load's latency is not on the step loop
+    uint4 c = stats_u32(St, i)[0], d = stats_u32(St, i)[1];
+    c.x += s.ep_coll & 0xFFFFu;
+    c.y += s.ep_coll >> 16;
+    c.z += s.ego_wm & 0xFFFFu;
+    c.w += s.steps;
+    d.x += s.ego_wm >> 16;
+    d.y += s.wh;
+    stats_u32(St, i)[0] = c;
+    stats_u32(St, i)[1] = d;
+  }
+}
+
+// The ego arrived first on a step that did not end the episode: keep r1_accumulate as it stood
+// before that step -- main.py's ep_reward stops there (:209-211), since winner stays 1.
+__device__ __forceinline__ void note_first_arrival(const mg_stats& St, int64_t i, const StepOut& r,
+                                                   EpStats* sreg = nullptr) {
+  if (sreg) {
+    sreg->pend = r.ret_pre;
+    sreg->dirty_f = true;
+  } else if (St.rec) {
+    reinterpret_cast<double*>(St.rec + i)[3] = r.ret_pre;  // ret1_pending
+  }
 }
 
 // gym.vector autoreset: record the finished episode, keep its terminal observation, reset
 // the env (merging_env.py:208-230) and put the reset observation in r.o. sreg: statistics held
-// in registers (nullptr: read-modify-write them in memory).
+// in registers (nullptr: read-modify-write them in memory). The episode's statistics:
+// r{1,2}_accumulate (hdqn.py's ep_reward), main.py's winner-filtered ep_reward (r1_accumulate
+// before the ego-first step while winner == 1), main.py:225's win test on the state the last step
+// acted on (r.win_pre) and hdqn.py:342's on the terminal state.
 __device__ __forceinline__ void finish_episode(const mg_params& P, Env& e, StepOut& r,
                                                const mg_stats& St, float* final_obs_row,
                                                int64_t i, EpStats* sreg = nullptr) {
+  const bool ego_won = e.winner == 1;
+  const bool win_hdqn = (P.end_point - e.p2) > (P.end_point - e.p1);
   if (sreg) {
+    const double pend = r.first1 ? r.ret_pre : sreg->pend;
     sreg->r1 += e.ret1;
     sreg->r2 += e.ret2;
-    sreg->c.x += 1;
-    sreg->c.y += r.coll ? 1u : 0u;
-    sreg->c.z += e.winner == 1 ? 1u : 0u;
-    sreg->c.w += e.steps;
-    sreg->dirty = true;
-  } else {
-    // one 32-byte record per env: a finishing env reads and writes one sector
-    if (St.rec) {
-      double2* rp = reinterpret_cast<double2*>(St.rec + i);
-      uint4* cp = reinterpret_cast<uint4*>(St.rec + i) + 1;
-      const double2 rv = *rp;
-      uint4 cv = *cp;
-      cv.x += 1;
-      cv.y += r.coll ? 1u : 0u;
-      cv.z += e.winner == 1 ? 1u : 0u;
-      cv.w += e.steps;
-      *rp = make_double2(rv.x + e.ret1, rv.y + e.ret2);
-      *cp = cv;
-    }
+    sreg->rm += ego_won ? pend : e.ret1;
+    sreg->ep_coll += 1u + (r.coll ? 0x10000u : 0u);
+    sreg->ego_wm += (ego_won ? 1u : 0u) + (r.win_pre ? 0x10000u : 0u);
+    sreg->wh += win_hdqn ? 1u : 0u;
+    sreg->steps += e.steps;
+    sreg->dirty_f = sreg->dirty_c = true;
+  } else if (St.rec) {
+    // one 64-byte record per env: a finishing env reads and writes one cache line
+    double2* fp = stats_f64(St, i);
+    const double2 a = fp[0], b = fp[1];
+    const double pend = r.first1 ? r.ret_pre : b.y;
+    fp[0] = make_double2(a.x + e.ret1, a.y + e.ret2);
+    fp[1] = make_double2(b.x + (ego_won ? pend : e.ret1), b.y);
+    uint4* cp = stats_u32(St, i);
+    uint4 c = cp[0];
+    uint2 d = reinterpret_cast<const uint2*>(cp + 1)[0];
+    c.x += 1;
+    c.y += r.coll ? 1u : 0u;
+    c.z += ego_won ? 1u : 0u;
+    c.w += e.steps;
+    d.x += r.win_pre ? 1u : 0u;
+    d.y += win_hdqn ? 1u : 0u;
+    cp[0] = c;
+    reinterpret_cast<uint2*>(cp + 1)[0] = d;
   }
   if (final_obs_row) {
 #pragma unroll
@@ -608,7 +612,16 @@ __device__ __forceinline__ void finish_episode(const mg_params& P, Env& e, StepO
   e.steps = 0;
   e.winner = 0;
   e.done = false;
-  reset_obs(P, r.o);
+  reset_obs(P, r.o, &r.dx1);
+}
+
+// After a step with statistics: the first-arrival bookkeeping, then autoreset where done.
+__device__ __forceinline__ void after_step(const mg_params& P, Env& e, StepOut& r, const mg_stats& St,
+                                           float* final_obs_row, int64_t i, bool autoreset,
+                                           EpStats* sreg = nullptr) {
+  const bool finish = autoreset && r.done;
+  if (r.first1 && !finish) note_first_arrival(St, i, r, sreg);
+  if (finish) finish_episode(P, e, r, St, final_obs_row, i, sreg);
 }
 
 // Write a block's [rows,10] fp32 observation tile through LDS as contiguous 16-byte stores
@@ -690,7 +703,6 @@ __device__ __forceinline__ void wave_store_obs_n(float* wtile, const StepOut (&r
 // A wave's nrows x 10 fp32 LDS slice to dst: 16-byte stores when dst allows, else 8-byte.
 __device__ __forceinline__ void wave_copy_rows(const float* wtile, float* dst, int nrows) {
   const int lane = threadIdx.x & 63;
-#if MG_COPY_FULL_WAVE
   // a full wave (64 rows = 160 16-byte pieces) into a 16-byte aligned destination: three fixed
   // lane passes instead of the strided loop (wave-uniform test)
   if (dst != nullptr && nrows == 64 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
@@ -703,7 +715,6 @@ __device__ __forceinline__ void wave_copy_rows(const float* wtile, float* dst, i
     if (lane < 32) st_out(d4 + 128 + lane, v2);
     return;
   }
-#endif
   if (dst != nullptr && nrows > 0) {
     const int nfl = nrows * kObs;
     if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
@@ -733,13 +744,8 @@ __device__ __forceinline__ void store_won_mask(uint64_t* mask, bool won, int t, 
 
 // The env index through an empty asm: the state stores recompute their addresses from it
 // instead of keeping the load addresses (two VGPRs per array) live across the step.
-#ifndef MG_STEP_OPAQUE_INDEX
-#define MG_STEP_OPAQUE_INDEX 1
-#endif
 __device__ __forceinline__ int64_t opaque_index(int64_t i) {
-#if MG_STEP_OPAQUE_INDEX
   asm volatile("" : "+v"(i));
-#endif
   return i;
 }
 
@@ -769,10 +775,7 @@ struct Launch {
 
 // The step kernel. OUT64 = the single-env path (packed fp64 record, no LDS staging).
 template <int ACT, bool OUT64>
-#ifndef MG_STEP_WAVES_PER_EU
-#define MG_STEP_WAVES_PER_EU 1  // step kernel: minimum waves per SIMD the register budget must allow
-#endif
-__global__ __launch_bounds__(kBlock, MG_STEP_WAVES_PER_EU) void step_kernel(const Launch L) {
+__global__ __launch_bounds__(kBlock) void step_kernel(const Launch L) {
   __shared__ __attribute__((aligned(16))) float obs_tile[kBlock * kObs];
 
   const mg_params& P = L.P;
@@ -804,9 +807,6 @@ __global__ __launch_bounds__(kBlock, MG_STEP_WAVES_PER_EU) void step_kernel(cons
     } else {
       if constexpr (OUT64) {
         mg_rec64* rec = L.O.rec64 + i;
-#pragma unroll
-        for (int k = 0; k < kObs; ++k) rec->obs[k] = r.o[k];
-#if MG_OBS_F32
         {  // the fp64 observation of the state after the step (score_step's values, recomputed)
           double x1, y1, x2, y2, od[kObs];
           lon2coord(P, e.p1, true, x1, y1);
@@ -815,7 +815,6 @@ __global__ __launch_bounds__(kBlock, MG_STEP_WAVES_PER_EU) void step_kernel(cons
 #pragma unroll
           for (int k = 0; k < kObs; ++k) rec->obs[k] = od[k];
         }
-#endif
         rec->rew[0] = r.r1;
         rec->rew[1] = r.r2;
         rec->acc[0] = r.acc1;
@@ -841,8 +840,8 @@ __global__ __launch_bounds__(kBlock, MG_STEP_WAVES_PER_EU) void step_kernel(cons
         if (L.O.coll) st_out(L.O.coll + i, static_cast<uint8_t>(r.coll ? 1 : 0));
       }
       won = e.winner == 1;
-      if ((L.flags & MG_AUTORESET) && r.done)
-        finish_episode(P, e, r, L.St, L.O.final_obs ? L.O.final_obs + i * kObs : nullptr, i);
+      after_step(P, e, r, L.St, L.O.final_obs ? L.O.final_obs + i * kObs : nullptr, i,
+                 (L.flags & MG_AUTORESET) != 0);
       store_env(L.S, opaque_index(i), e);
     }
   }
@@ -893,18 +892,12 @@ struct Rollout {
 
 // num_steps consecutive mg_step_random steps with the env kept in registers: the state is
 // read once and written once per launch; step t's outputs go to slice t of the trajectory.
-#ifndef MG_ROLLOUT_LEAN
-#define MG_ROLLOUT_LEAN 1  // rollout: unchecked step for device-drawn actions, per-step StepOut
-#endif
-#ifndef MG_ROLLOUT_WAVES_PER_EU
-#define MG_ROLLOUT_WAVES_PER_EU 1  // rollout kernel: minimum waves per SIMD the register budget must allow
-#endif
 // FULL: the outputs every MergeVecEnv rollout passes are present (obs, rew, the interleaved step
 // record, statistics, autoreset; final observations and the won mask stay optional). The
 // instance assumes so, which drops null tests the compiler otherwise keeps live across the loop
 // as 64-bit lane masks (SGPR pairs, spilled into VGPR lanes: a v_readlane per use).
 template <bool FULL>
-__global__ __launch_bounds__(kBlock, MG_ROLLOUT_WAVES_PER_EU) void rollout_kernel(const Rollout R) {
+__global__ __launch_bounds__(kBlock) void rollout_kernel(const Rollout R) {
   __shared__ __attribute__((aligned(16))) float obs_tile[kBlock * kObs];
 
   if constexpr (FULL) {
@@ -930,15 +923,10 @@ __global__ __launch_bounds__(kBlock, MG_ROLLOUT_WAVES_PER_EU) void rollout_kerne
     e = load_env(R.S, i);
     stats_load(R.St, i, sreg);
   }
-#if !MG_ROLLOUT_LEAN
-  StepOut r;
-#endif
   bool won = false;
   uint4 u = make_uint4(0u, 0u, 0u, 0u);  // the Philox block of the current eight steps
   for (int t = 0; t < R.num_steps; ++t) {
-#if MG_ROLLOUT_LEAN
     StepOut r;  // per step: no loop-carried copy of the observation (dead lanes store nothing)
-#endif
     const int64_t row = static_cast<int64_t>(t) * R.n + i;
     const uint64_t k = R.first_step + t;
     if (t == 0 || k % kStepsPerPhilox == 0)  // wave-uniform
@@ -946,14 +934,13 @@ __global__ __launch_bounds__(kBlock, MG_ROLLOUT_WAVES_PER_EU) void rollout_kerne
     if (live) {
       int a1, a2;
       actions_from_block(u, k, R.opp_random, a1, a2);
-      env_step<!MG_ROLLOUT_LEAN>(P, e, a1, a2, r);  // Philox actions are always valid
+      env_step<false>(P, e, a1, a2, r);  // Philox actions are always valid: the unchecked step
       if (R.T.rew)
         st_out(reinterpret_cast<f32x2*>(R.T.rew) + row,
                f32x2{static_cast<float>(r.r1), static_cast<float>(r.r2)});
       store_step_bytes(R.T, row, a1, a2, r.done, r.coll);
       won = e.winner == 1;
-      if (autoreset && r.done)
-        finish_episode(P, e, r, R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i, &sreg);
+      after_step(P, e, r, R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i, autoreset, &sreg);
     }
     store_won_mask(R.T.won_mask, won, t, R.n, wbase, wrows);
     if (R.T.obs)  // staged per wave: waves never wait for each other
@@ -1002,11 +989,14 @@ constexpr int kQBiasIn = 13;       // first of the three layer-1 input slots hol
 constexpr int kQOne1 = 200;        // hidden-1 units 200..202 = 1.0
 constexpr int kQOne2 = 100;        // hidden-2 units 100..102 = 1.0
 constexpr int kQMaxIn = kQBiasIn;  // widest net input: 13
-constexpr int kQBlock = MG_QNET_BLOCK;                             // waves sharing one LDS copy
-// specialised kernel: 4 Q-net waves + MG_QNET_WS_ENV_WAVES env waves; each env lane steps
-// MG_QNET_WS_ILP envs per phase, so a group is 64 x env waves x ILP envs and a block holds two
-constexpr int kQWsThreads = 64 * (4 + MG_QNET_WS_ENV_WAVES);
-constexpr int kQWsWavesPerSimd = (4 + MG_QNET_WS_ENV_WAVES) / 4;
+// specialised kernel: 4 Q-net waves + kQWsEnvWaves env waves (8 env waves -- 3 waves per SIMD,
+// a Q-net wave within 168 VGPRs -- measured 19 % slower); each env lane steps kQWsIlp envs per
+// phase, in lockstep (independent fp64 chains interleaved in one instruction stream), so a group
+// is 64 x env waves x ILP envs and a block holds two
+constexpr int kQWsEnvWaves = 4;
+constexpr int kQWsIlp = 2;
+constexpr int kQWsThreads = 64 * (4 + kQWsEnvWaves);
+constexpr int kQWsWavesPerSimd = (4 + kQWsEnvWaves) / 4;
 static_assert(kQOffW2 % 16 == 0 && kQOffW3 % 16 == 0 && kQNetBytes % 16 == 0,
               "packed Q-net sections must stay 16-byte aligned");
 
@@ -1381,43 +1371,10 @@ struct QRollout {
   uint32_t flags;
 };
 
-__device__ __forceinline__ void qnet_forward_ws(const uint8_t* net, const float* tile, int row0,
-                                                bool swap, float (&q)[8]) {
-#if MG_QNET_SWP
-  qnet_forward_swp(net, tile, row0, swap, q);
-#else
-  qnet_forward(net, tile, row0, swap, q);
-#endif
-}
 
-// One epsilon-greedy step of env i given the greedy actions (main.py:99-112): Philox4x32-10
-// per (global env, step): u.x ego explore draw, u.y ego random action, u.z opponent explore
-// draw, u.w opponent random action. Then the env step and its trajectory outputs.
-template <int OPP>
-__device__ __forceinline__ void qnet_policy_step(const QRollout& R, Env& e, StepOut& r, int64_t i,
-                                                 int t, int greedy1, int greedy2, bool& won) {
-  const int64_t row = static_cast<int64_t>(t) * R.n + i;
-  const uint64_t gi = static_cast<uint64_t>(R.env_offset + i);
-  const uint64_t step = R.first_step + t;
-  const uint4 u = philox4x32_10(
-      make_uint4(static_cast<uint32_t>(gi), static_cast<uint32_t>(gi >> 32),
-                 static_cast<uint32_t>(step), static_cast<uint32_t>(step >> 32)),
-      static_cast<uint32_t>(R.seed), static_cast<uint32_t>(R.seed >> 32));
-  const int a1 = (static_cast<uint64_t>(u.x) < R.greedy_thr) ? greedy1 : action_from_u32(u.y);
-  int a2 = MG_ACTION_NONE;
-  if constexpr (OPP == 1) a2 = action_from_u32(u.w);
-  if constexpr (OPP >= 2)
-    a2 = (static_cast<uint64_t>(u.z) < R.opp_greedy_thr) ? greedy2 : action_from_u32(u.w);
-  env_step(R.P, e, a1, a2, r);
-  if (R.T.rew)
-    st_out(reinterpret_cast<f32x2*>(R.T.rew) + row, f32x2{static_cast<float>(r.r1), static_cast<float>(r.r2)});
-  store_step_bytes(R.T, row, a1, a2, r.done, r.coll);
-  won = e.winner == 1;
-  if ((R.flags & MG_AUTORESET) && r.done)
-    finish_episode(R.P, e, r, R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i);
-}
-
-// qnet_policy_step for the N envs i0 + 64 j of one env-wave lane, stepped in lockstep. Envs
+// One epsilon-greedy step (main.py:99-112) of the N envs i0 + 64 j of one env-wave lane given their
+// greedy actions, stepped in lockstep: Philox4x32-10 per (global env, step) gives u.x the ego's
+// explore draw, u.y its random action, u.z the opponent's explore draw, u.w its random action. Envs
 // past n (live[j] false) are stepped too but never stored. A greedy action outside 0..4 (a
 // net with out_dim > 5) gets env_step's KeyError semantics (env_step_lockstep).
 template <int OPP, int N>
@@ -1452,8 +1409,8 @@ __device__ __forceinline__ void qnet_policy_step_n(const QRollout& R, Env (&e)[N
              f32x2{static_cast<float>(r[j].r1), static_cast<float>(r[j].r2)});
     store_step_bytes(R.T, row, a1[j], a2[j], r[j].done, r[j].coll);
     won[j] = e[j].winner == 1;
-    if ((R.flags & MG_AUTORESET) && r[j].done)
-      finish_episode(R.P, e[j], r[j], R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i);
+    after_step(R.P, e[j], r[j], R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i,
+               (R.flags & MG_AUTORESET) != 0);
   }
 }
 
@@ -1484,84 +1441,6 @@ __device__ __forceinline__ bool qnet_load_env(const QRollout& R, int64_t i, Env&
   return live;
 }
 
-// T epsilon-greedy Q-net steps per launch, every wave doing both jobs for its own 64 envs.
-// OPP: 0 = None (L0 opponent), 1 = uniform random, 2 = the same net on the swapped observation
-// (self-play, main.py:165-166 / :199).
-template <int OPP>
-__global__ __launch_bounds__(kQBlock, MG_QNET_WAVES_PER_EU) void qnet_rollout_kernel(const QRollout R) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds_net[kQNetBytes];
-  __shared__ __attribute__((aligned(16))) float tile[kQBlock * kObs];
-
-  const int tid = threadIdx.x;
-  const int64_t base = static_cast<int64_t>(blockIdx.x) * kQBlock;
-  const int64_t i = base + tid;
-  const int row0 = (tid >> 6) * 64;
-
-  qnet_to_lds(R.net, lds_net);
-  Env e;
-  StepOut r;
-  const bool live = qnet_load_env(R, i, e, tile + tid * kObs);
-  // this wave's 64 rows of the tile; waves never read each other's rows, so after the one
-  // barrier that publishes the weights they run unsynchronised
-  float* wtile = tile + row0 * kObs;
-  const int64_t wbase = base + row0;
-  const int64_t wrem = R.n - wbase;
-  const int wrows = wrem <= 0 ? 0 : (wrem < 64 ? static_cast<int>(wrem) : 64);
-#pragma unroll
-  for (int k = 0; k < kObs; ++k) r.o[k] = 0.0;
-  __syncthreads();
-
-  bool won = false;
-  for (int t = 0; t < R.num_steps; ++t) {
-    float q[8];
-    qnet_forward(lds_net, tile, row0, false, q);
-    const int greedy1 = argmax_first(q, R.out_dim);
-    int greedy2 = 0;
-    if constexpr (OPP == 2) {
-      qnet_forward(lds_net, tile, row0, true, q);
-      greedy2 = argmax_first(q, R.out_dim);
-    }
-    wave_lds_sync();  // the wave is done reading its rows before they are overwritten
-    if (live) qnet_policy_step<OPP>(R, e, r, i, t, greedy1, greedy2, won);
-    store_won_mask(R.T.won_mask, won, t, R.n, wbase, wrows);
-    // the new observations: this wave's tile rows (next step's network input) and the output
-    wave_store_obs(wtile, r.o,
-                   R.T.obs ? R.T.obs + (static_cast<int64_t>(t) * R.n + wbase) * kObs : nullptr,
-                   wrows);
-  }
-  if (live) store_env(R.S, i, e);
-}
-
-#if MG_QNET_STAMPS
-// Diagnostic build only (-DMG_QNET_STAMPS=1, tools/qnet_stamps.py): per role, shader-clock
-// cycles spent working in a phase and waiting at its closing barrier, summed over waves.
-// [0] Q work, [1] Q wait, [2] env work, [3] env wait, [4] phases x waves, [5] memtime, [6] realtime
-__device__ unsigned long long g_qstamps[8];
-struct PhaseClock {
-  unsigned long long work = 0, wait = 0, t = 0;
-  __device__ void start() { t = __builtin_amdgcn_s_memtime(); }
-  __device__ void before_barrier() {
-    const unsigned long long n = __builtin_amdgcn_s_memtime();
-    work += n - t;
-    t = n;
-  }
-  __device__ void after_barrier() {
-    const unsigned long long n = __builtin_amdgcn_s_memtime();
-    wait += n - t;
-    t = n;
-  }
-  __device__ void flush(int role, int phases) {
-    if ((threadIdx.x & 63) == 0) {
-      atomicAdd(&g_qstamps[2 * role], work);
-      atomicAdd(&g_qstamps[2 * role + 1], wait);
-      if (role == 0) atomicAdd(&g_qstamps[4], static_cast<unsigned long long>(phases));
-    }
-  }
-};
-#define MG_STAMP(x) x
-#else
-#define MG_STAMP(x)
-#endif
 
 // The same T steps with the waves specialised: waves 0-3 run only the Q-net (matrix cores +
 // ReLU), waves 4-7 only the fp64 env step, so each SIMD pairs a matrix-heavy wave with a
@@ -1574,9 +1453,9 @@ struct PhaseClock {
 // keeps a second packed net in LDS; the two nets and a 1,024-env tile would pass the CU's 160 KB,
 // so that instance runs ILP 1: 512-env blocks, one env per env-wave lane.
 template <int OPP>
-constexpr int qws_ilp() { return OPP == 3 ? 1 : MG_QNET_WS_ILP; }
+constexpr int qws_ilp() { return OPP == 3 ? 1 : kQWsIlp; }
 template <int OPP>
-constexpr int qws_envs() { return 2 * 64 * MG_QNET_WS_ENV_WAVES * qws_ilp<OPP>(); }
+constexpr int qws_envs() { return 2 * 64 * kQWsEnvWaves * qws_ilp<OPP>(); }
 
 template <int OPP>
 __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws_kernel(const QRollout R) {
@@ -1584,7 +1463,7 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
   constexpr int kEnvs = qws_envs<OPP>();  // envs per block
   constexpr int kHalf = kEnvs / 2;        // envs per group
   constexpr int kTiles = kHalf / 256;     // 64-env tiles each Q-net wave computes per phase
-  constexpr int kEnvWaves = MG_QNET_WS_ENV_WAVES;
+  constexpr int kEnvWaves = kQWsEnvWaves;
   static_assert(kTiles >= 1 && kHalf == 64 * kEnvWaves * kIlp && kHalf % 256 == 0,
                 "group = 4 Q-net waves x kTiles x 64 envs = env waves x ILP x 64 envs");
   __shared__ __attribute__((aligned(16))) uint8_t lds_net[kQNetBytes];
@@ -1605,32 +1484,22 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
     // (roles are whole waves, so s_barrier pairs up; the two loops keep each role's live
     // registers apart -- in one loop the env state sat beside the accumulators and spilled)
     __syncthreads();
-    MG_STAMP(PhaseClock clk; clk.start(); unsigned long long m0 = clk.t; unsigned long long r0 = __builtin_amdgcn_s_memrealtime();)
     for (int p = 0; p < phases; ++p) {
       if (p < 2 * R.num_steps) {
 #pragma unroll 1
         for (int tt = 0; tt < kTiles; ++tt) {
           const int row0 = (p & 1) * kHalf + (4 * tt + wave) * 64;
           float q[8];
-          qnet_forward_ws(lds_net, tile, row0, false, q);
+          qnet_forward_swp(lds_net, tile, row0, false, q);
           greedy[0][row0 + lane] = static_cast<uint8_t>(argmax_first(q, R.out_dim));
           if constexpr (OPP >= 2) {  // the opponent's view state[5:] + state[:5] (main.py:199)
-            qnet_forward_ws(OPP == 3 ? lds_net2 : lds_net, tile, row0, true, q);
+            qnet_forward_swp(OPP == 3 ? lds_net2 : lds_net, tile, row0, true, q);
             greedy[1][row0 + lane] = static_cast<uint8_t>(argmax_first(q, R.out_dim));
           }
         }
       }
-      MG_STAMP(clk.before_barrier();)
       __syncthreads();
-      MG_STAMP(clk.after_barrier();)
     }
-#if MG_QNET_STAMPS
-    clk.flush(0, phases);
-    if (tid == 0) {
-      atomicAdd(&g_qstamps[5], __builtin_amdgcn_s_memtime() - m0);
-      atomicAdd(&g_qstamps[6], __builtin_amdgcn_s_memrealtime() - r0);
-    }
-#endif
     return;
   }
   // env lane: envs lbase + 64 j + lane (j < kIlp) of group 0 (e0) and of group 1 (e1)
@@ -1647,7 +1516,6 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
     for (int k = 0; k < kObs; ++k) r[j].o[k] = 0.0;
   }
   __syncthreads();
-  MG_STAMP(PhaseClock clk; clk.start();)
   for (int p = 0; p < phases; ++p) {
     if (p > 0) {
       const int g = (p - 1) & 1, t = (p - 1) >> 1;
@@ -1677,11 +1545,8 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
                              R.T.obs ? R.T.obs + (static_cast<int64_t>(t) * R.n + wbase) * kObs : nullptr,
                              wrows);
     }
-    MG_STAMP(clk.before_barrier();)
     __syncthreads();
-    MG_STAMP(clk.after_barrier();)
   }
-  MG_STAMP(clk.flush(1, phases);)
 #pragma unroll
   for (int j = 0; j < kIlp; ++j) {
     const int la = lbase + 64 * j + lane;
@@ -1752,12 +1617,6 @@ constexpr int kHEnvs = 512;              // envs per block: two groups of 256
 constexpr int kRowGoalF = 2 * kObs + 4;  // goal ring row floats (hdqn.py:158)
 constexpr int kHHalf = kHEnvs / 2;
 constexpr uint8_t kHGreedy = 0xFF;       // draw byte: take the greedy choice
-
-// goal_status (hdqn.py:223-237) of an fp32 observation: dx1 = o[0], v2 = o[9]
-__device__ __forceinline__ int goal_status(const obs_t (&o)[kObs]) {
-  const float dx1 = static_cast<float>(o[0]), v2 = static_cast<float>(o[9]);
-  return dx1 < -0.5f * v2 ? 0 : (dx1 < 0.5f * v2 ? 1 : 2);
-}
 
 __device__ __forceinline__ uint8_t draw_byte(uint32_t explore, uint32_t pick, uint64_t thr, int k) {
   return static_cast<uint8_t>(static_cast<uint64_t>(explore) < thr
@@ -1916,8 +1775,8 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
   // ------------------------------------------------------------------ the env step
   const int ew = wave - 4;
   Env e[2];
-  StepOut r[2];
   bool live[2];
+  int stc[2];  // goal_status of each group's current state, from its fp64 dx1 and v2
   // the fused ring row of each group's last step, completed once the Q-net waves have chosen
   // its next goal: s, s' (terminal where done), goal, action
   float ps[2][kObs], ps2[2][kObs];
@@ -1925,7 +1784,9 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
   // Goal_DQN's memory (hdqn.py:286, :311-313, :322, :325): the extrinsic reward since each env's
   // inner loop began, and at each step whether that loop ended (known once Q(X, t + 1) has chosen
   // the step's next goal, so it is emitted together with the ring row of the step)
-  const bool outer = R.H.ext_reward != nullptr || R.H.no_break != nullptr;
+  // kept whenever the caller holds the running sums (ext_acc), so turning ext_reward / no_break
+  // on in a later launch continues the loops already in flight correctly
+  const bool outer = R.ext_acc != nullptr;
   double acc[2] = {0.0, 0.0};
   auto finish_outer = [&](int g, int t, double& ac) __attribute__((always_inline)) {
     const int j = g * kHHalf + 64 * ew + lane;
@@ -1990,11 +1851,10 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
 #pragma unroll
       for (int k = 0; k < kObs; ++k) o[k] = 0.0;
     }
-#pragma unroll
-    for (int k = 0; k < kObs; ++k) r[g].o[k] = static_cast<obs_t>(o[k]);
+    stc[g] = goal_status(o[0], o[9]);
     float2* t2 = reinterpret_cast<float2*>(tile + j * kObs);
 #pragma unroll
-    for (int k = 0; k < kObs / 2; ++k) t2[k] = make_float2(static_cast<float>(r[g].o[2 * k]), static_cast<float>(r[g].o[2 * k + 1]));
+    for (int k = 0; k < kObs / 2; ++k) t2[k] = make_float2(static_cast<float>(o[2 * k]), static_cast<float>(o[2 * k + 1]));
     const uint64_t gi = static_cast<uint64_t>(R.env_offset + i);
     const uint4 fb = philox_env_step(gi ^ (uint64_t{1} << 63), R.first_step - 1, R.seed);
     b_df[j] = draw_byte(fb.x, fb.y, R.greedy_thr, R.num_goals);
@@ -2036,12 +1896,18 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
             finish_outer(1, t - 1, acc[1]);
         }
       }
-      auto step = [&](Env& ev, StepOut& rv, bool lv, float (&s0)[kObs], float (&s1)[kObs], int& pg,
-                      int& pa, double& ac) __attribute__((always_inline)) {
-        b_st_old[j] = static_cast<uint8_t>(goal_status(rv.o));  // status of the state acted on
+      auto step = [&](Env& ev, bool lv, float (&s0)[kObs], float (&s1)[kObs], int& pg, int& pa, double& ac,
+                      int& st) __attribute__((always_inline)) {
+        StepOut rv;  // per step: the state acted on is the env's tile row, so no observation is carried
+        b_st_old[j] = static_cast<uint8_t>(st);  // status of the state acted on (:314)
         if (ring) {
+          const f32x2* trow = reinterpret_cast<const f32x2*>(tile + j * kObs);
 #pragma unroll
-          for (int q = 0; q < kObs; ++q) s0[q] = static_cast<float>(rv.o[q]);
+          for (int q = 0; q < kObs / 2; ++q) {
+            const f32x2 v = trow[q];
+            s0[2 * q] = v[0];
+            s0[2 * q + 1] = v[1];
+          }
           pg = b_goal[j];
           pa = a1;
         }
@@ -2057,7 +1923,8 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
           store_step_bytes(R.T, row, a1, a2, rv.done, rv.coll);
         }
         b_done[j] = rv.done ? 1 : 0;
-        b_st_new[j] = static_cast<uint8_t>(goal_status(rv.o));
+        st = goal_status(rv.dx1, ev.v2);  // of the next state (:322), terminal where done
+        b_st_new[j] = static_cast<uint8_t>(st);
         b_dg[j] = draw_byte(ua.z, ua.w, R.greedy_thr, R.num_goals);
         b_df[j] = draw_byte(ub.x, ub.y, R.greedy_thr, R.num_goals);
         if constexpr (kOpNets) b_dfo[j] = draw_byte(uc.z, uc.w, R.greedy_thr, R.num_goals);
@@ -2071,6 +1938,9 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
             sd[q2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(
                                                       f32x2{static_cast<float>(rv.o[2 * q2]), static_cast<float>(rv.o[2 * q2 + 1])}, bf16x2));
           finish_episode(R.P, ev, rv, R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i);
+          st = goal_status(rv.dx1, ev.v2);  // the reset state the next step acts on
+        } else if (lv && rv.first1) {
+          note_first_arrival(R.St, i, rv);
         }
         const int64_t wrem = R.n - wbase;
         wave_store_obs(tile + (g * kHHalf + 64 * ew) * kObs, rv.o,
@@ -2078,9 +1948,9 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
                        wrem <= 0 ? 0 : (wrem < 64 ? static_cast<int>(wrem) : 64));
       };
       if (g == 0)
-        step(e[0], r[0], live[0], ps[0], ps2[0], pgoal[0], pact[0], acc[0]);
+        step(e[0], live[0], ps[0], ps2[0], pgoal[0], pact[0], acc[0], stc[0]);
       else
-        step(e[1], r[1], live[1], ps[1], ps2[1], pgoal[1], pact[1], acc[1]);
+        step(e[1], live[1], ps[1], ps2[1], pgoal[1], pact[1], acc[1], stc[1]);
     }
     __syncthreads();
   }
@@ -2164,7 +2034,7 @@ __global__ __launch_bounds__(kBlock) void observe_kernel(const mg_params P, cons
 //                             straight from the won bits, a wave scan (in-group offsets), the
 //                             group's total;
 //   replay_group_scan_kernel  one wave: group totals -> ring positions, memory_counter advanced;
-//   replay_write_kernel       one block per 256 envs x MG_REPLAY_TCHUNK steps, the step's
+//   replay_write_kernel       one block per 256 envs x kRTChunk steps, the step's
 //                             observation kept in registers as the next transition's s; rows
 //                             gathered in LDS in ring order and written as contiguous 8-byte
 //                             stores (a row is 88 B: 16-byte alignment alternates).
@@ -2173,6 +2043,8 @@ __global__ __launch_bounds__(kBlock) void observe_kernel(const mg_params P, cons
 constexpr int kRow = 2 * kObs + 2;       // 22
 constexpr int kRowGoal = 2 * kObs + 4;   // 24
 constexpr int kRBlock = 256;        // envs per write block
+constexpr int kRTChunk = 2;         // steps one write block walks (obs carried in registers; 1 step
+                                    // measured +6 %, all 16 per block +11 %: DESIGN.md section 4)
 constexpr int kRGroup = 64;         // write blocks per scan wave
 
 struct ReplayIn {
@@ -2321,8 +2193,8 @@ __global__ __launch_bounds__(kRBlock) void replay_write_kernel(const ReplayIn R,
   const int64_t bx = blockIdx.x;
   const int64_t i = bx * kRBlock + threadIdx.x;
   const bool live = i < R.n;
-  const int t0 = blockIdx.y * MG_REPLAY_TCHUNK;
-  const int t1 = t0 + MG_REPLAY_TCHUNK < R.T ? t0 + MG_REPLAY_TCHUNK : R.T;
+  const int t0 = blockIdx.y * kRTChunk;
+  const int t1 = t0 + kRTChunk < R.T ? t0 + kRTChunk : R.T;
   const uint64_t end = *counter;  // memory_counter after this whole store
   // Only the newest `cap` transitions survive sequential stores; they occupy distinct slots,
   // so no two writes of this launch collide.
@@ -2330,19 +2202,13 @@ __global__ __launch_bounds__(kRBlock) void replay_write_kernel(const ReplayIn R,
   float s[kObs], o[kObs];
   if (live) {
     load_row10(t0 == 0 ? R.X.obs_first + i * kObs : R.X.obs + ((t0 - 1) * R.n + i) * kObs, s);
-#if MG_REPLAY_PREFETCH
     load_row10(R.X.obs + (t0 * R.n + i) * kObs, o);
-#endif
   }
   for (int t = t0; t < t1; ++t) {
     const int64_t row = static_cast<int64_t>(t) * R.n + i;
     const bool keep = replay_keep(R, t, i);
-#if MG_REPLAY_PREFETCH
     float on[kObs];  // next step's row in flight while this step is gathered and written
     if (live && t + 1 < t1) load_row10(R.X.obs + (row + R.n) * kObs, on);
-#else
-    if (live) load_row10(R.X.obs + row * kObs, o);
-#endif
     int total;
     const int rank = block_rank(keep, wave_cnt, total);
     if (total > 0) {  // uniform across the block
@@ -2376,7 +2242,6 @@ __global__ __launch_bounds__(kRBlock) void replay_write_kernel(const ReplayIn R,
       const int skip = base >= first ? 0 : static_cast<int>(min<uint64_t>(first - base, total));
       const uint64_t slot0 = (base + skip) % static_cast<uint64_t>(cap);
       const int cnt = total - skip;  // <= cap: at most one wrap
-#if MG_REPLAY_WIDE_STORES
       // the kept rows are one contiguous byte run of the ring (two at a wrap): an 8-byte head
       // when the run starts off 16-byte alignment, then 16-byte stores, then an 8-byte tail
       const int n_a = static_cast<int>(min<uint64_t>(static_cast<uint64_t>(cnt), static_cast<uint64_t>(cap) - slot0));
@@ -2400,24 +2265,12 @@ __global__ __launch_bounds__(kRBlock) void replay_write_kernel(const ReplayIn R,
           st_out(d4 + k, f32x4{lo[0], lo[1], hi[0], hi[1]});
         }
       }
-#else
-      const int nel = cnt * (kRow / 2);
-      const f32x2* src = reinterpret_cast<const f32x2*>(tile + skip * kRow);
-      for (int e2 = threadIdx.x; e2 < nel; e2 += kRBlock) {
-        const int rr = e2 / (kRow / 2), part = e2 - rr * (kRow / 2);
-        uint64_t slot = slot0 + rr;
-        if (slot >= static_cast<uint64_t>(cap)) slot %= static_cast<uint64_t>(cap);
-        st_out(reinterpret_cast<f32x2*>(rows + slot * kRow) + part, src[e2]);
-      }
-#endif
     }
     __syncthreads();  // tile and wave counts are reused by the next step
 #pragma unroll
     for (int k = 0; k < kObs; ++k) s[k] = o[k];
-#if MG_REPLAY_PREFETCH
 #pragma unroll
     for (int k = 0; k < kObs; ++k) o[k] = on[k];
-#endif
   }
 }
 
@@ -2515,10 +2368,7 @@ int launch_rollout(const Rollout& R, hipStream_t stream) {
   const unsigned blocks = static_cast<unsigned>((R.n + kBlock - 1) / kBlock);
   hipEvent_t start = g_ev_start, stop = g_ev_stop;
   g_ev_start = g_ev_stop = nullptr;
-#ifndef MG_ROLLOUT_FULL
-#define MG_ROLLOUT_FULL 1  // A/B knob: 0 always launches the generic instance
-#endif
-  const bool full = MG_ROLLOUT_FULL && R.T.obs && R.T.rew && R.T.flags && R.St.rec &&
+  const bool full = R.T.obs && R.T.rew && R.T.flags && R.St.rec &&
                     (R.flags & MG_AUTORESET);
   if (start || stop) {
     if (full)
@@ -2533,48 +2383,82 @@ int launch_rollout(const Rollout& R, hipStream_t stream) {
   return finish_launch("mg_rollout_random");
 }
 
-// The constants of mpc_1d's equality step (helper.py:152-191), computed in the order the
-// solver computes them (file compiled without contraction): the horizon's 10 controls of
-// dt = t / 10; the constraint normal n = A[1] = (dt, ..., dt) (the velocity row of
-// [a^9 b, ..., a b, b], a = [[1, dt], [0, 1]], b = [0, dt]); P = D'D + 0.01 I with D the
-// 9 x 10 first-difference operator, factored P = L L' column by column; z = L'^-1 L^-1 n by
-// forward then back substitution; nz = sum_i n_i z_i in index order.
-void mpc_qp_constants(double t, double* nz_out, double* z0_out) {
+// The constants of mpc_1d's equality step (helper.py:152-191) in the operation order of quadprog
+// 0.1.11's qpgen2 (Goldfarb-Idnani; helper.py:182 -> qpsolvers 1.8.0 -> quadprog.solve_qp with
+// G = P, C = -A[1]', b = -B, meq = 1), file compiled without contraction:
+//   n = A[1] = (dt, ..., dt), dt = t / 10 (the velocity row of [a^9 b, ..., b]);
+//   P = D'D + 0.01 I, D the 9 x 10 first-difference operator (integer sums, then + 0.01);
+//   dpofa: P = R'R, column by column, s accumulating t*t before a(j,j) - s;
+//   dpori: J = R^-1 in place (a(k,k) = 1 / a(k,k), column k scaled by -a(k,k), then
+//          a(1:k, j) += a(k, j) a(1:k, k) for j > k);
+//   d = J'n (d_i = sum_j J(j,i) n_j), z = J d (z_i = sum_j J(i,j) d_j, accumulated in j order),
+//   z'n (sum in index order).
+// The residual's sign only negates n, d, z and the step exactly, so u0 = (b / z'n) z0 for either
+// sign of b = vt - v0. Restated from the published algorithm (LINPACK dpofa / dpori and
+// Goldfarb & Idnani 1983 as coded in Turlach's solve.QP.f); quadprog is not in this image.
+void mpc_qp_constants(double t, double* nz_out, double* z0_out, double* vsmall_out) {
   constexpr int kT = 10;
   const double dt = t / kT;
-  double n[kT], P[kT][kT] = {}, L[kT][kT] = {}, y[kT], z[kT];
+  double n[kT], a[kT][kT] = {}, d[kT], z[kT];  // a[i][j] = LINPACK's a(i+1, j+1)
   for (int i = 0; i < kT; ++i) n[i] = 0.0 * 0.0 + 1.0 * dt;  // row [0 1] of a^k times b
   for (int i = 0; i + 1 < kT; ++i) {
-    P[i][i] += 1.0;
-    P[i + 1][i + 1] += 1.0;
-    P[i][i + 1] -= 1.0;
-    P[i + 1][i] -= 1.0;
+    a[i][i] += 1.0;
+    a[i + 1][i + 1] += 1.0;
+    a[i][i + 1] -= 1.0;
+    a[i + 1][i] -= 1.0;
   }
-  for (int i = 0; i < kT; ++i) P[i][i] += 0.01;
-  for (int j = 0; j < kT; ++j) {
-    double d = P[j][j];
-    for (int k = 0; k < j; ++k) d -= L[j][k] * L[j][k];
-    L[j][j] = std::sqrt(d);
-    for (int i = j + 1; i < kT; ++i) {
-      double v = P[i][j];
-      for (int k = 0; k < j; ++k) v -= L[i][k] * L[j][k];
-      L[i][j] = v / L[j][j];
+  for (int i = 0; i < kT; ++i) a[i][i] += 0.01;
+  for (int j = 0; j < kT; ++j) {  // dpofa (upper triangle)
+    double s = 0.0;
+    for (int k = 0; k < j; ++k) {
+      double dot = 0.0;
+      for (int l = 0; l < k; ++l) dot = dot + a[l][k] * a[l][j];
+      double tk = a[k][j] - dot;
+      tk = tk / a[k][k];
+      a[k][j] = tk;
+      s = s + tk * tk;
+    }
+    s = a[j][j] - s;
+    a[j][j] = std::sqrt(s);
+  }
+  for (int k = 0; k < kT; ++k) {  // dpori
+    a[k][k] = 1.0 / a[k][k];
+    const double tk = -a[k][k];
+    for (int i = 0; i < k; ++i) a[i][k] = tk * a[i][k];
+    for (int j = k + 1; j < kT; ++j) {
+      const double tj = a[k][j];
+      a[k][j] = 0.0;
+      if (tj == 0.0) continue;  // daxpy returns early for a zero multiplier
+      for (int i = 0; i <= k; ++i) a[i][j] = a[i][j] + tj * a[i][k];
     }
   }
-  for (int i = 0; i < kT; ++i) {
-    double v = n[i];
-    for (int k = 0; k < i; ++k) v -= L[i][k] * y[k];
-    y[i] = v / L[i][i];
+  for (int i = 0; i < kT; ++i) {  // d = J'n (J is upper triangular: a[j][i] = 0 for j > i)
+    double s = 0.0;
+    for (int j = 0; j < kT; ++j) s = s + (j <= i ? a[j][i] : 0.0) * n[j];
+    d[i] = s;
   }
-  for (int i = kT - 1; i >= 0; --i) {
-    double v = y[i];
-    for (int k = i + 1; k < kT; ++k) v -= L[k][i] * z[k];
-    z[i] = v / L[i][i];
-  }
+  for (int i = 0; i < kT; ++i) z[i] = 0.0;
+  for (int j = 0; j < kT; ++j)  // z = J d
+    for (int i = 0; i < kT; ++i) z[i] = z[i] + (i <= j ? a[i][j] : 0.0) * d[j];
   double nz = 0.0;
-  for (int i = 0; i < kT; ++i) nz += n[i] * z[i];
+  for (int i = 0; i < kT; ++i) nz = nz + z[i] * n[i];
+  // qpgen2's machine-precision probe: a constraint residual below vsmall is set to 0
+  volatile double vs = 1e-60;
+  for (;;) {
+    vs = vs + vs;
+    const double ta = vs * 0.1 + 1.0, tb = vs * 0.2 + 1.0;
+    if (ta > 1.0 && tb > 1.0) break;
+  }
   *nz_out = nz;
   *z0_out = z[0];
+  *vsmall_out = vs;
+}
+
+// goal_status of n (dx1, v2) pairs, the function the h-DQN kernel evaluates (tests, evaluation)
+__global__ __launch_bounds__(kBlock) void goal_status_kernel(const double* dx1, const double* v2, int8_t* out,
+                                                             int64_t n) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (i < n) out[i] = static_cast<int8_t>(goal_status(dx1[i], v2[i]));
 }
 
 }  // namespace
@@ -2583,15 +2467,6 @@ extern "C" {
 
 int mg_abi_version(void) { return MG_ABI_VERSION; }
 
-#if MG_QNET_STAMPS
-// diagnostic build only: copy out (and clear) the Q-net kernel's phase clocks
-int mg_debug_qstamps(unsigned long long* out8) {
-  hipError_t e = hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_qstamps), sizeof(unsigned long long) * 8);
-  if (e != hipSuccess) return static_cast<int>(e);
-  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  return static_cast<int>(hipMemcpyToSymbol(HIP_SYMBOL(g_qstamps), z, sizeof(z)));
-}
-#endif
 
 int mg_time_next_launch(void* start_event, void* stop_event) {
   g_ev_start = static_cast<hipEvent_t>(start_event);
@@ -2625,8 +2500,17 @@ void mg_params_default(mg_params* p) {
   p->veh_h = 8;
   p->timeout_steps = 2501;
   p->inv_R = 1.0 / p->R;
-  mpc_qp_constants(p->prediction_t, &p->qp_nz, &p->qp_z0);
+  mpc_qp_constants(p->prediction_t, &p->qp_nz, &p->qp_z0, &p->qp_vsmall);
   p->qp_inv_nz = 1.0 / p->qp_nz;
+}
+
+int mg_goal_status(const double* dx1, const double* v2, int8_t* status, int64_t n, void* stream) {
+  if (!dx1 || !v2 || !status) return fail(hipErrorInvalidValue, "%s", "mg_goal_status: NULL pointer");
+  if (n < 0) return fail(hipErrorInvalidValue, "%s", "n < 0");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(goal_status_kernel, dim3(static_cast<unsigned>((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                     static_cast<hipStream_t>(stream), dx1, v2, status, n);
+  return finish_launch("mg_goal_status");
 }
 
 int mg_step(const mg_params* params, const mg_state* state, const int8_t* a1, const int8_t* a2,
@@ -2678,7 +2562,8 @@ int mg_rollout_random(const mg_params* params, const mg_state* state, const mg_t
   mg_outputs none{};
   if (int e = check_common(params, state, &none, n)) return e;
   if (!traj) return fail(hipErrorInvalidValue, "%s", "traj is NULL (pass a zeroed mg_traj)");
-  if (num_steps < 0) return fail(hipErrorInvalidValue, "%s", "num_steps < 0");
+  if (num_steps < 0 || num_steps > 65535)
+    return fail(hipErrorInvalidValue, "%s", "need 0 <= num_steps <= 65535 (split longer rollouts)");
   if ((traj->obs && (reinterpret_cast<uintptr_t>(traj->obs) & 15)) ||
       (traj->final_obs && (reinterpret_cast<uintptr_t>(traj->final_obs) & 7)) ||
       (traj->rew && (reinterpret_cast<uintptr_t>(traj->rew) & 7)) ||
@@ -2751,10 +2636,6 @@ int mg_rollout_qnet(const mg_params* params, const mg_state* state, const mg_tra
                 "opponent_mode must be 0 (None), 1 (uniform), 2 (same net) or 3 (opp_net)");
   if (opponent_mode == 3 && (!opp_net || (reinterpret_cast<uintptr_t>(opp_net) & 15)))
     return fail(hipErrorInvalidValue, "%s", "opponent_mode 3 needs opp_net, a 16-byte aligned packed Q-net");
-#if !MG_QNET_WS
-  if (opponent_mode == 3)
-    return fail(hipErrorInvalidValue, "%s", "opponent_mode 3 needs the specialised-wave kernel (MG_QNET_WS)");
-#endif
   if ((traj->obs && (reinterpret_cast<uintptr_t>(traj->obs) & 15)) ||
       (traj->final_obs && (reinterpret_cast<uintptr_t>(traj->final_obs) & 7)) ||
       (traj->rew && (reinterpret_cast<uintptr_t>(traj->rew) & 7)) ||
@@ -2777,25 +2658,17 @@ int mg_rollout_qnet(const mg_params* params, const mg_state* state, const mg_tra
   R.num_steps = num_steps;
   R.out_dim = out_dim;
   R.flags = flags;
-  unsigned blocks = static_cast<unsigned>((n + kQBlock - 1) / kQBlock);
+  const int64_t block_envs = opponent_mode == 3 ? qws_envs<3>() : qws_envs<0>();
+  const unsigned blocks = static_cast<unsigned>((n + block_envs - 1) / block_envs);
   hipStream_t st = static_cast<hipStream_t>(stream);
   hipEvent_t ev0 = g_ev_start, ev1 = g_ev_stop;
   g_ev_start = g_ev_stop = nullptr;
-#if MG_QNET_WS
-#define MG_QKERNEL qnet_rollout_ws_kernel
-  const unsigned threads = kQWsThreads;
-  const int64_t block_envs = opponent_mode == 3 ? qws_envs<3>() : qws_envs<0>();
-  blocks = static_cast<unsigned>((n + block_envs - 1) / block_envs);
-#else
-#define MG_QKERNEL qnet_rollout_kernel
-  const unsigned threads = kQBlock;
-#endif
-#define MG_LAUNCH_Q(OPPV)                                                                         \
-  do {                                                                                            \
-    if (ev0 || ev1)                                                                               \
-      hipExtLaunchKernelGGL(MG_QKERNEL<OPPV>, dim3(blocks), dim3(threads), 0, st, ev0, ev1, 0, R); \
-    else                                                                                          \
-      hipLaunchKernelGGL(MG_QKERNEL<OPPV>, dim3(blocks), dim3(threads), 0, st, R);               \
+#define MG_LAUNCH_Q(OPPV)                                                                                   \
+  do {                                                                                                      \
+    if (ev0 || ev1)                                                                                         \
+      hipExtLaunchKernelGGL(qnet_rollout_ws_kernel<OPPV>, dim3(blocks), dim3(kQWsThreads), 0, st, ev0, ev1, 0, R); \
+    else                                                                                                    \
+      hipLaunchKernelGGL(qnet_rollout_ws_kernel<OPPV>, dim3(blocks), dim3(kQWsThreads), 0, st, R);         \
   } while (0)
   if (opponent_mode == 0)
     MG_LAUNCH_Q(0);
@@ -2803,12 +2676,9 @@ int mg_rollout_qnet(const mg_params* params, const mg_state* state, const mg_tra
     MG_LAUNCH_Q(1);
   else if (opponent_mode == 2)
     MG_LAUNCH_Q(2);
-#if MG_QNET_WS
   else
     MG_LAUNCH_Q(3);
-#endif
 #undef MG_LAUNCH_Q
-#undef MG_QKERNEL
   return finish_launch("mg_rollout_qnet");
 }
 
@@ -2849,6 +2719,8 @@ int mg_rollout_hdqn(const mg_params* params, const mg_state* state, const mg_tra
       (reinterpret_cast<uintptr_t>(traj->flags) & 3))
     return fail(hipErrorInvalidValue, "%s", "traj.obs must be 16-byte, rew/final_obs 8-byte, flags 4-byte aligned");
   if (n == 0 || num_steps == 0) return 0;
+  if (!(flags & MG_AUTORESET))  // hdqn.py's loop resets at every episode end (:276-277)
+    return fail(hipErrorInvalidValue, "%s", "mg_rollout_hdqn needs MG_AUTORESET (hdqn.py resets every episode)");
   HRollout R{};
   R.P = *params;
   R.S = *state;
@@ -2925,7 +2797,7 @@ int mg_replay_store(float* rows, uint64_t* counter, int64_t capacity, int32_t ro
     return fail(hipErrorInvalidValue, "%s", "mg_replay_store: n * num_steps exceeds the grid limit");
   if (!scratch || scratch_bytes < mg_replay_scratch_bytes(n, num_steps))
     return fail(hipErrorInvalidValue, "%s", "mg_replay_store: scratch smaller than mg_replay_scratch_bytes(n, num_steps)");
-  const unsigned chunks = static_cast<unsigned>((num_steps + MG_REPLAY_TCHUNK - 1) / MG_REPLAY_TCHUNK);
+  const unsigned chunks = static_cast<unsigned>((num_steps + kRTChunk - 1) / kRTChunk);
   if (chunks > 65535) return fail(hipErrorInvalidValue, "%s", "mg_replay_store: num_steps too large");
   ReplayIn R{};
   R.X = *tr;

@@ -15,7 +15,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libmerging_hip.so"
 LIB_PATH = os.environ.get("MERGING_HIP_LIB", os.path.join(_HERE, LIB_NAME))
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 OBS_DIM = 10
 NUM_ACTIONS = 5
@@ -42,7 +42,7 @@ class Params(_c.Structure):
         "angle0")] + [("action_speed", _c.c_double * NUM_ACTIONS), ("veh_w", _c.c_int32),
                       ("veh_h", _c.c_int32), ("timeout_steps", _c.c_int32), ("_pad", _c.c_int32),
                       ("inv_R", _c.c_double), ("qp_nz", _c.c_double), ("qp_z0", _c.c_double),
-                      ("qp_inv_nz", _c.c_double)]
+                      ("qp_inv_nz", _c.c_double), ("qp_vsmall", _c.c_double)]
 
 
 class State(_c.Structure):
@@ -68,10 +68,16 @@ class HdqnTraj(_c.Structure):
 
 
 class Stats(_c.Structure):
-    _fields_ = [("rec", _P)]  # mg_episode_stats [n]: f64 ret[2], u32 episodes/collisions/ego_first/steps
+    _fields_ = [("rec", _P)]  # mg_episode_stats [n] (64 bytes each, see EPISODE_STATS_DTYPE)
 
 
-EPISODE_STATS_BYTES = 32
+# numpy view of struct mg_episode_stats (ABI 17): the fp64 sums, main.py's pending r1_accumulate,
+# then the counts (episodes, collisions, ego_first, steps, win_main, win_hdqn) and two reserved
+EPISODE_STATS_DTYPE = np.dtype([("ret", np.float64, (2,)), ("ret_main", np.float64),
+                                ("ret1_pending", np.float64), ("counts", np.uint32, (6,)),
+                                ("reserved", np.uint32, (2,))])
+EPISODE_STATS_BYTES = 64
+assert EPISODE_STATS_DTYPE.itemsize == EPISODE_STATS_BYTES
 
 
 # numpy view of struct mg_rec64 (168 bytes)
@@ -118,6 +124,7 @@ def _load():
                                     _c.c_int32, _c.c_uint64, _c.c_int32, _P, _P, _P, _P, _c.c_int64, _c.c_uint32,
                                     _P]
     lib.mg_time_next_launch.argtypes = [_P, _P]
+    lib.mg_goal_status.argtypes = [_P, _P, _P, _c.c_int64, _P]
     lib.mg_replay_scratch_bytes.argtypes = [_c.c_int64, _c.c_int32]
     lib.mg_replay_scratch_bytes.restype = _c.c_size_t
     lib.mg_replay_store.argtypes = [_P, _P, _c.c_int64, _c.c_int32, _c.POINTER(Transitions), _c.c_int64,
@@ -126,7 +133,7 @@ def _load():
                                      _P, _c.c_int64, _P]
     for f in (lib.mg_step, lib.mg_step_random, lib.mg_reset, lib.mg_observe, lib.mg_rollout_random,
               lib.mg_time_next_launch, lib.mg_qnet_pack, lib.mg_qnet_forward, lib.mg_rollout_qnet,
-              lib.mg_rollout_hdqn, lib.mg_replay_store, lib.mg_replay_sample):
+              lib.mg_rollout_hdqn, lib.mg_replay_store, lib.mg_replay_sample, lib.mg_goal_status):
         f.restype = _c.c_int
     v = lib.mg_abi_version()
     if v != ABI_VERSION:

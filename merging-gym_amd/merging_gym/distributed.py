@@ -4,12 +4,13 @@ Envs never interact, so the step needs no exchange: rank r owns global envs
 [offset, offset + count) and steps them alone (MergeVecEnv(env_offset=offset) keys its
 Philox stream by the global index, so a sharded run draws exactly the unsharded actions).
 The only collective is reducing completed-episode statistics after a rollout: by default
-each rank contributes its shard's six totals (return sums of both players as f64 bits, and
-episodes / collisions / ego-first arrivals / steps as int64 -- 48 bytes) to one all-gather
-over RCCL (torch backend "nccl" on ROCm, xGMI between MI355X GPUs), and every rank reduces
-the [world, 6] result in rank order (hdqn.py:330-346 and main.py:221-228 log exactly these
-rates). `gather_episode_stats` gathers the per-env rows instead ([N/W, 4] int64 per rank),
-for a caller that needs them. gloo carries the same calls on CPU tensors in tests.
+each rank contributes its shard's nine totals (three return sums as f64 bits -- both players'
+r_accumulate and main.py's winner-filtered ep_reward -- and episodes / collisions / ego-first
+arrivals / steps / main.py wins / hdqn.py wins as int64: 72 bytes) to one all-gather over RCCL
+(torch backend "nccl" on ROCm, xGMI between MI355X GPUs), and every rank reduces the [world, 9]
+result in rank order (the quantities hdqn.py:330-346 and main.py:221-228 log).
+`gather_episode_stats` gathers the per-env rows instead ([N/W, 6] int64 per rank), for a caller
+that needs them. gloo carries the same calls on CPU tensors in tests.
 """
 
 from __future__ import annotations
@@ -25,31 +26,32 @@ def shard(global_envs: int, world: int, rank: int):
     return offset, count
 
 
-def pack_stats(ret_sum, counts):
-    """[n,2] f64 returns + [n,4] i32 counts -> one [n,4] int64 tensor (bit-preserving)."""
+def pack_stats(returns, counts):
+    """[n,R] f64 return sums + [n,C] i32 counts (C even) -> one [n, R + C/2] int64 tensor
+    (bit-preserving)."""
     import torch
 
-    return torch.cat([ret_sum.contiguous().view(torch.int64), counts.contiguous().view(torch.int64)], dim=1)
+    return torch.cat([returns.contiguous().view(torch.int64), counts.contiguous().view(torch.int64)], dim=1)
 
 
-def unpack_stats(packed):
+def unpack_stats(packed, num_returns: int = 3):
     import torch
 
-    ret_sum = packed[:, :2].contiguous().view(torch.float64)
-    counts = packed[:, 2:].contiguous().view(torch.int32)
-    return ret_sum, counts
+    returns = packed[:, :num_returns].contiguous().view(torch.float64)
+    counts = packed[:, num_returns:].contiguous().view(torch.int32)
+    return returns, counts
 
 
-def gather_episode_stats(ret_sum, counts, group=None):
+def gather_episode_stats(returns, counts, group=None):
     """All-gather every rank's per-env statistics (equal shard sizes). Returns the global
-    (ret_sum [N,2] f64, counts [N,4] i32) on every rank."""
+    (returns [N,R] f64, counts [N,C] i32) on every rank -- MergeVecEnv.returns / .counts."""
     import torch
     import torch.distributed as dist
 
-    packed = pack_stats(ret_sum, counts)
+    packed = pack_stats(returns, counts)
     world = dist.get_world_size(group)
     if world == 1:
-        return unpack_stats(packed)
+        return unpack_stats(packed, returns.shape[1])
     if dist.get_backend(group) == "nccl":
         out = torch.empty((world * packed.shape[0], packed.shape[1]), dtype=packed.dtype,
                           device=packed.device)
@@ -59,60 +61,83 @@ def gather_episode_stats(ret_sum, counts, group=None):
         parts = [torch.empty_like(host) for _ in range(world)]
         dist.all_gather(parts, host, group=group)
         out = torch.cat(parts).to(packed.device)
-    return unpack_stats(out)
+    return unpack_stats(out, returns.shape[1])
 
 
-PARTIAL_BYTES = 6 * 8  # one rank's contribution to gather_episode_summary
+NUM_RETURNS, NUM_COUNTS = 3, 6
+PARTIAL_BYTES = (NUM_RETURNS + NUM_COUNTS) * 8  # one rank's contribution to gather_episode_summary
 
 
-def partial_stats(ret_sum, counts):
-    """This shard's totals as one [6] int64 tensor on the stats' device: return sums of ego and
-    opponent (f64, bit-preserved), then episodes, collisions, ego-first arrivals, steps."""
+def partial_stats(returns, counts):
+    """This shard's totals as one [9] int64 tensor on the stats' device: the three return sums
+    (r1_accumulate, r2_accumulate, main.py's filtered ep_reward; f64, bit-preserved), then
+    episodes, collisions, ego-first arrivals, steps, main.py wins, hdqn.py wins."""
     import torch
 
-    r = ret_sum.sum(0).contiguous().view(torch.int64)
+    if returns.shape[1] != NUM_RETURNS or counts.shape[1] != NUM_COUNTS:
+        raise ValueError(f"need returns [n,{NUM_RETURNS}] and counts [n,{NUM_COUNTS}] (MergeVecEnv.returns / .counts)")
+    r = returns.sum(0).contiguous().view(torch.int64)
     c = counts.to(torch.int64).sum(0)
     return torch.cat([r, c])
 
 
 def summarize_partials(parts):
-    """[world, 6] partial totals (partial_stats rows) -> the summary dict, reduced in rank order."""
+    """[world, 9] partial totals (partial_stats rows) -> the summary dict, reduced in rank order:
+    the quantities the reference's scripts log per episode, as rates / means over all completed
+    episodes -- hdqn.py:330-346 (reward = r1_accumulate, collision_rate, win_rate on the terminal
+    observation) and main.py:221-228 (reward = the winner-filtered ep_reward, win on the
+    pre-terminal observation) -- plus the ego-first rate (winner == 1) and the mean length."""
     import torch
 
-    parts = parts.reshape(-1, 6).cpu()
-    r = parts[:, :2].contiguous().view(torch.float64)
-    c = parts[:, 2:].sum(0).tolist()
-    r1 = r2 = 0.0
-    for a, b in r.tolist():
-        r1 += a
-        r2 += b
+    w = NUM_RETURNS + NUM_COUNTS
+    parts = parts.reshape(-1, w).cpu()
+    r = parts[:, :NUM_RETURNS].contiguous().view(torch.float64)
+    c = parts[:, NUM_RETURNS:].sum(0).tolist()
+    sums = [0.0] * NUM_RETURNS
+    for row in r.tolist():
+        sums = [a + b for a, b in zip(sums, row)]
     ep = max(c[0], 1)
-    return {"completed": c[0], "mean_return_ego": r1 / ep, "mean_return_opp": r2 / ep,
-            "collision_rate": c[1] / ep, "ego_first_rate": c[2] / ep, "mean_length": c[3] / ep}
+    return {"completed": c[0], "mean_return_ego": sums[0] / ep, "mean_return_opp": sums[1] / ep,
+            "mean_ep_reward_main": sums[2] / ep, "collision_rate": c[1] / ep, "ego_first_rate": c[2] / ep,
+            "win_rate_main": c[4] / ep, "win_rate_hdqn": c[5] / ep, "mean_length": c[3] / ep}
 
 
-def gather_episode_summary(ret_sum, counts, group=None):
-    """All-gather every rank's 48-byte partial totals and reduce them: the global summary on
-    every rank (the default collective of a sharded run)."""
+def gather_episode_summary(returns, counts, group=None, timings=None):
+    """All-gather every rank's 72-byte partial totals and reduce them: the global summary on
+    every rank (the default collective of a sharded run). timings (a dict, optional) receives
+    "reduce_ms" (this shard's device reduction to its partial totals, synchronised) and
+    "allgather_ms" (the collective alone; None without one, world size 1)."""
+    import time
+
     import torch
     import torch.distributed as dist
 
-    part = partial_stats(ret_sum, counts)
-    world = dist.get_world_size(group)
+    sync = (lambda: torch.cuda.synchronize(returns.device)) if returns.is_cuda else (lambda: None)  # noqa: E731
+    sync()
+    t0 = time.perf_counter()
+    part = partial_stats(returns, counts)
+    sync()
+    t1 = time.perf_counter()
+    world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    if timings is not None:
+        timings["reduce_ms"] = (t1 - t0) * 1e3
+        timings["allgather_ms"] = None
     if world == 1:
         return summarize_partials(part)
     if dist.get_backend(group) == "nccl":
-        out = torch.empty((world, 6), dtype=torch.int64, device=part.device)
+        out = torch.empty((world, part.numel()), dtype=torch.int64, device=part.device)
         dist.all_gather_into_tensor(out, part, group=group)
     else:  # gloo: host tensors
         host = part.cpu()
         rows = [torch.empty_like(host) for _ in range(world)]
         dist.all_gather(rows, host, group=group)
         out = torch.stack(rows)
+    sync()
+    if timings is not None:
+        timings["allgather_ms"] = (time.perf_counter() - t1) * 1e3
     return summarize_partials(out)
 
 
-def summarize(ret_sum, counts):
-    """Mean episode return / collision rate / ego-first rate / mean length (hdqn.py:330-346)
-    of one process's per-env statistics."""
-    return summarize_partials(partial_stats(ret_sum, counts))
+def summarize(returns, counts):
+    """The summary (summarize_partials) of one process's per-env statistics."""
+    return summarize_partials(partial_stats(returns, counts))

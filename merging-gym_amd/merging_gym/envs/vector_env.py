@@ -107,11 +107,16 @@ class MergeVecEnv:
                          if won_mask else None)
         self.error = torch.zeros(1, dtype=torch.int32, device=dev)
         self.strict_actions = bool(strict_actions)
-        # one 32-byte mg_episode_stats record per env; ret_sum [N,2] f64 and counts [N,4] i32
-        # (episodes, collisions, ego-first arrivals, steps) are strided views of it
-        self._ep_stats = torch.zeros((n, 4), dtype=torch.float64, device=dev) if episode_stats else None
+        # one 64-byte mg_episode_stats record per env (include/merging_hip.h), seen through strided
+        # views: returns [N,3] f64 = sums of r1_accumulate, r2_accumulate (hdqn.py's ep_reward) and
+        # main.py's winner-filtered ep_reward; ret_sum = returns[:, :2], ret_main = returns[:, 2];
+        # counts [N,6] i32 = episodes, collisions, ego-first arrivals, steps, main.py:225 wins,
+        # hdqn.py:342 wins
+        self._ep_stats = torch.zeros((n, 8), dtype=torch.float64, device=dev) if episode_stats else None
+        self.returns = self._ep_stats[:, :3] if episode_stats else None
         self.ret_sum = self._ep_stats[:, :2] if episode_stats else None
-        self.counts = self._ep_stats[:, 2:].view(torch.int32) if episode_stats else None
+        self.ret_main = self._ep_stats[:, 2] if episode_stats else None
+        self.counts = self._ep_stats[:, 4:].view(torch.int32)[:, :6] if episode_stats else None
 
         ptr = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
         self._state = _native.State(*(ptr(t) for t in (self.p1, self.v1, self.p2, self.v2,
@@ -195,12 +200,22 @@ class MergeVecEnv:
 
     def reset(self, mask=None):
         """Reset all envs (mask None) or those where mask is true; returns obs [N,10] f32.
-        merging_env.py:208-230."""
+        merging_env.py:208-230. rollout_hdqn's per-env loop state restarts with the episode, as
+        hdqn.py's outer loop does after env.reset() (:277-286): no goal yet (the next launch's
+        meta-net chooses one on the reset state) and a zero extrinsic-reward sum."""
         m = None
+        mt = None
         if mask is not None:
             mt = self._torch.as_tensor(mask, device=self.device).to(self._torch.uint8).contiguous()
             self._mask_keepalive = mt
             m = ctypes.c_void_p(mt.data_ptr())
+        for name, fresh in (("hdqn_goal", -1), ("hdqn_goal_op", -1), ("hdqn_ext", 0)):
+            t = getattr(self, name, None)
+            if t is not None:
+                if mt is None:
+                    t.fill_(fresh)
+                else:
+                    t.masked_fill_(mt.bool(), fresh)
         out = self._nat.Outputs(self._out.obs)
         self._nat.check(self._nat.lib.mg_reset(ctypes.byref(self.params), ctypes.byref(self._state),
                                                m, ctypes.byref(out), self.num_envs,
@@ -378,14 +393,19 @@ class MergeVecEnv:
             hb["_hm"] = nat.HdqnTraj(*(hb[k].data_ptr() for k in ("goal", "next_goal", "reward", "goal_op",
                                                                    "ext_reward", "no_break")))
             self._hdqn_bufs = hb
-        if goal_memory and getattr(self, "hdqn_ext", None) is None:
+        if not self.autoreset:
+            raise ValueError("rollout_hdqn runs hdqn.py's loop, which resets every finished episode: "
+                             "it needs MergeVecEnv(autoreset=True)")
+        if getattr(self, "hdqn_ext", None) is None:
+            # the extrinsic-reward sums are kept from the first launch on, whether or not this
+            # launch returns Goal_DQN's columns, so turning goal_memory on later is consistent
             self.hdqn_ext = torch.zeros(n, dtype=torch.float64, device=self.device)
         if getattr(self, "hdqn_goal", None) is None:
             self.hdqn_goal = torch.full((n,), -1, dtype=torch.int8, device=self.device)
         if mode >= 2 and getattr(self, "hdqn_goal_op", None) is None:
             self.hdqn_goal_op = torch.full((n,), -1, dtype=torch.int8, device=self.device)
         gop = getattr(self, "hdqn_goal_op", None)
-        ext = getattr(self, "hdqn_ext", None) if goal_memory else None
+        ext = self.hdqn_ext
         rc = nat.lib.mg_rollout_hdqn(
             self._p_ref, self._s_ref, ctypes.byref(buf["_traj"]), ctypes.byref(hb["_hm" if goal_memory else "_h"]),
             self._st_ref, self.hdqn_goal.data_ptr(), None if gop is None else gop.data_ptr(),
@@ -451,13 +471,19 @@ class MergeVecEnv:
                 "acc2": float(acc[1]), "r1": r1, "r2": r2}
 
     def episode_statistics(self):
-        """Completed-episode totals per env: returns sum [N,2] f64 and counts [N,4] i32
-        (episodes, collisions, ego-first arrivals, steps)."""
-        return {"ret_sum": self.ret_sum, "counts": self.counts}
+        """Completed-episode totals per env (views of the device records): "returns" [N,3] f64
+        (sums of r1_accumulate = hdqn.py's ep_reward, r2_accumulate, main.py's winner-filtered
+        ep_reward, scripts/main.py:209-211), "ret_sum" = returns[:, :2], "ret_main" =
+        returns[:, 2], "counts" [N,6] i32 (episodes, collisions, ego-first arrivals, steps,
+        main.py:225 wins, hdqn.py:342 wins)."""
+        return {"returns": self.returns, "ret_sum": self.ret_sum, "ret_main": self.ret_main,
+                "counts": self.counts}
 
     def clear_statistics(self):
+        """Zero the sums and counts (each env's pending main.py value stays: it belongs to the
+        episode in progress)."""
         if self.ret_sum is not None:
-            self.ret_sum.zero_()
+            self.returns.zero_()
             self.counts.zero_()
 
     # ------------------------------------------------------------------ checkpoint / resume
@@ -472,7 +498,7 @@ class MergeVecEnv:
         sd["step_idx"] = self._step_idx
         sd["env_offset"] = self.env_offset
         if self.ret_sum is not None:
-            sd["ret_sum"], sd["counts"] = self.ret_sum.clone(), self.counts.clone()
+            sd["episode_stats"] = self._ep_stats.clone()  # the 64-byte records, pending value included
         if getattr(self, "hdqn_goal", None) is not None:
             sd["hdqn_goal"] = self.hdqn_goal.clone()  # rollout_hdqn's current goals
         if getattr(self, "hdqn_goal_op", None) is not None:
@@ -491,9 +517,8 @@ class MergeVecEnv:
         if int(sd.get("env_offset", self.env_offset)) != self.env_offset:
             raise ValueError("the checkpoint is of another env shard (env_offset differs)")
         self._step_idx = int(sd["step_idx"])
-        if self.ret_sum is not None and "ret_sum" in sd:
-            self.ret_sum.copy_(self._torch.as_tensor(sd["ret_sum"]))
-            self.counts.copy_(self._torch.as_tensor(sd["counts"]))
+        if self.ret_sum is not None and "episode_stats" in sd:
+            self._ep_stats.copy_(self._torch.as_tensor(sd["episode_stats"]))
         if "hdqn_goal" in sd:
             self.hdqn_goal = self._torch.as_tensor(sd["hdqn_goal"]).to(self.device, self._torch.int8).clone()
         if "hdqn_goal_op" in sd:

@@ -66,7 +66,7 @@ def c_oracle(seconds: float, threads: int):
     n = 16384
     envs = co.new_envs(n)
     co.reset(envs)
-    ret_sum, counts = np.zeros((n, 2)), np.zeros((n, 4), np.uint32)
+    ret_sum, counts = np.zeros((n, 3)), np.zeros((n, 6), np.uint32)
     done_steps, chunk, k = 0, 25, 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:

@@ -14,10 +14,10 @@ oracle cites), one numpy expression per scalar statement, over arrays of envs:
   is_collided / corners                      merging_env.py:183-187, :198-206, :232-239
   accumulate returns                         merging_env.py:191-192
   reset (gym.vector autoreset)               merging_env.py:208-230
-mpc_1d's QP is solved once, numerically (Cholesky factor of P = D'D + 0.01 I, z = P^-1 n by
-forward / back substitution, n'z), exactly as the C oracle does per call: its first control is
-then (b / n'z) * z[0] for every env, b = vt - v0 -- the per-env arithmetic of the solver's
-equality step. Actions: Philox4x32-10 keyed by (global env, step), as the GPU workload draws them.
+mpc_1d's QP is factored once the way quadprog's qpgen2 does it (dpofa, dpori, z = J J'n, z'n),
+as the C oracle does per call: its first control is then (b / z'n) * z[0] for every env,
+b = vt - v0 (0 where |b| < qpgen2's vsmall) -- the per-env arithmetic of the solver's equality
+step. Actions: Philox4x32-10 keyed by (global env, step), as the GPU workload draws them.
 """
 
 from __future__ import annotations
@@ -36,48 +36,15 @@ ANGLE0 = math.atan2(H, R)  # merging_env.py:49 (np.arctan2(H, R) gives the same 
 
 
 def qp_step_constants(t: float = PREDICTION_T):
-    """(n'z, z[0]) of mpc_1d's QP (helper.py:152-191): z = P^-1 n, n = A[1] = (dt, .., dt)."""
-    steps = 10
-    dt = t / steps
-    n = [0.0 * 0.0 + 1.0 * dt for _ in range(steps)]
-    P = [[0.0] * steps for _ in range(steps)]
-    for i in range(steps - 1):
-        P[i][i] += 1.0
-        P[i + 1][i + 1] += 1.0
-        P[i][i + 1] -= 1.0
-        P[i + 1][i] -= 1.0
-    for i in range(steps):
-        P[i][i] += 0.01
-    L = [[0.0] * steps for _ in range(steps)]
-    for j in range(steps):
-        s = P[j][j]
-        for k in range(j):
-            s -= L[j][k] * L[j][k]
-        L[j][j] = math.sqrt(s)
-        for i in range(j + 1, steps):
-            v = P[i][j]
-            for k in range(j):
-                v -= L[i][k] * L[j][k]
-            L[i][j] = v / L[j][j]
-    y = [0.0] * steps
-    for i in range(steps):
-        v = n[i]
-        for k in range(i):
-            v -= L[i][k] * y[k]
-        y[i] = v / L[i][i]
-    z = [0.0] * steps
-    for i in reversed(range(steps)):
-        v = y[i]
-        for k in range(i + 1, steps):
-            v -= L[k][i] * z[k]
-        z[i] = v / L[i][i]
-    nz = 0.0
-    for i in range(steps):
-        nz += n[i] * z[i]
-    return nz, z[0]
+    """(z'n, z[0], vsmall) of mpc_1d's QP (helper.py:152-191) as quadprog's qpgen2 computes them
+    (merge_oracle.qpgen2_factor: dpofa, dpori, d = J'n, z = J d, z'n in the Fortran loop order)."""
+    from merge_oracle import qpgen2_factor
+
+    _, z, ztn, vsmall = qpgen2_factor(t)
+    return ztn, z[0], vsmall
 
 
-QP_NZ, QP_Z0 = qp_step_constants()
+QP_NZ, QP_Z0, QP_VSMALL = qp_step_constants()
 
 _M0, _M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
 _W0, _W1 = 0x9E3779B9, 0xBB67AE85
@@ -124,15 +91,17 @@ class NumpyMergeBatch:
     def __init__(self, n: int, env_offset: int = 0):
         self.n = int(n)
         self.gidx = np.arange(env_offset, env_offset + self.n, dtype=np.int64)
-        self.ret_sum = np.zeros((self.n, 2))
-        self.counts = np.zeros((self.n, 4), np.int64)
+        # per env: sums of r1_accumulate, r2_accumulate, main.py's ep_reward; episodes, collisions,
+        # ego-first arrivals, steps, main.py:225 wins, hdqn.py:342 wins (merge_oracle.STATS_DOC)
+        self.ret_sum = np.zeros((self.n, 3))
+        self.counts = np.zeros((self.n, 6), np.int64)
         self.reset()
 
     def reset(self, mask=None):
         """merging_env.py:208-230 for every env (mask None) or those where mask holds."""
         if mask is None:
             mask = np.ones(self.n, bool)
-            for name in ("p1", "v1", "p2", "v2", "time_stamp", "r1", "r2"):
+            for name in ("p1", "v1", "p2", "v2", "time_stamp", "r1", "r2", "ep_main"):
                 setattr(self, name, np.zeros(self.n))
             self.winner = np.zeros(self.n, np.int8)
             self.done = np.zeros(self.n, bool)
@@ -141,7 +110,7 @@ class NumpyMergeBatch:
         self.p2[mask] = START_POINT
         self.v1[mask] = 20.0
         self.v2[mask] = 20.0
-        for arr in (self.time_stamp, self.r1, self.r2, self.steps):
+        for arr in (self.time_stamp, self.r1, self.r2, self.ep_main, self.steps):
             arr[mask] = 0
         self.winner[mask] = 0
         self.done[mask] = False
@@ -164,14 +133,17 @@ class NumpyMergeBatch:
     def step(self, a1, a2, autoreset: bool = True):
         """One step of every env with valid actions a1 in 0..4, a2 in 0..4 or -1 (None).
         Returns obs [n,10] f64, rew [n,2], done [n] bool, coll [n] bool (before autoreset)."""
+        win_pre = (END_POINT - self.p2) > (END_POINT - self.p1)  # main.py:225 on the state acted on
         self.time_stamp += DT
         self.steps += 1
         self.done |= self.time_stamp > 500
-        acc1 = ((ACTION_SPEED[a1] - self.v1) / QP_NZ) * QP_Z0
+        b1 = ACTION_SPEED[a1] - self.v1
+        acc1 = np.where(np.abs(b1) < QP_VSMALL, -0.0, (b1 / QP_NZ) * QP_Z0)
         v = self.v1 + acc1 * DT
         self.v1 = np.where(v > 0, v, 0.0)
         self.p1 = self.p1 + self.v1 * DT
-        acc2 = np.where(a2 < 0, 0.0, ((ACTION_SPEED[np.maximum(a2, 0)] - self.v2) / QP_NZ) * QP_Z0)
+        b2 = ACTION_SPEED[np.maximum(a2, 0)] - self.v2
+        acc2 = np.where(a2 < 0, 0.0, np.where(np.abs(b2) < QP_VSMALL, -0.0, (b2 / QP_NZ) * QP_Z0))
         v = self.v2 + acc2 * DT
         self.v2 = np.where(v > 0, v, 0.0)
         self.p2 = self.p2 + self.v2 * DT
@@ -198,15 +170,19 @@ class NumpyMergeBatch:
         r2 = np.where(coll, r2 + R_COLLISION, r2)
         self.r1 += r1
         self.r2 += r2
+        self.ep_main = np.where(self.winner != 1, self.ep_main + r1, self.ep_main)  # main.py:209-211
         done = self.done.copy()
         if autoreset and done.any():
             d = done
             self.ret_sum[d, 0] += self.r1[d]
             self.ret_sum[d, 1] += self.r2[d]
+            self.ret_sum[d, 2] += self.ep_main[d]
             self.counts[d, 0] += 1
             self.counts[d, 1] += coll[d]
             self.counts[d, 2] += self.winner[d] == 1
             self.counts[d, 3] += self.steps[d]
+            self.counts[d, 4] += win_pre[d]
+            self.counts[d, 5] += ((END_POINT - self.p2) > (END_POINT - self.p1))[d]  # hdqn.py:342
             self.reset(d)
         return obs, np.stack([r1, r2], axis=1), done, coll
 

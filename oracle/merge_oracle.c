@@ -9,8 +9,8 @@
  *   lon2coord            merging_gym/envs/merging_env.py:48-58   (libm sin/cos/atan2)
  *   observe              merging_env.py:118-132
  *   action_to_acc        merging_env.py:134-136 -> mpc_1d scripts/helper.py:152-191: the QP
- *                        is built and solved (Cholesky + one Goldfarb-Idnani equality step),
- *                        not replaced by its closed form
+ *                        is built and solved as quadprog's qpgen2 solves it (dpofa, dpori, one
+ *                        Goldfarb-Idnani equality step, vsmall), not replaced by its closed form
  *   step                 merging_env.py:138-195 (fp64 clock accumulated with += 0.2)
  *   is_collided/corners  merging_env.py:198-206, :232-239 (pygame C-int truncation, fp64
  *                        Vector2 arithmetic, closed-box polygon intersection)
@@ -32,6 +32,7 @@ typedef struct oracle_env {
   double pos2, vel2, acc2; /* self.state2 */
   double time_stamp;       /* self.time_stamp */
   double r1_acc, r2_acc;   /* self.r1_accumulate, self.r2_accumulate */
+  double ep_reward_main;   /* scripts/main.py's ep_reward (:191, :209-211), the caller's sum */
   int32_t winner;          /* self.winner: 0 = None, 1, 2 */
   int32_t done;            /* self.done */
   int32_t steps;           /* steps since reset: bookkeeping for episode statistics only */
@@ -62,6 +63,94 @@ static void lon2coord(double lon, int ego, double* x, double* y) {
   *y = ego ? W / 2 + bulge : W / 2 - bulge;
 }
 
+/* quadprog 0.1.11's qpgen2 (helper.py:182 -> qpsolvers 1.8.0 quadprog_solve_qp: G = P, a = -q = 0,
+ * C = -A[1]', b = -B, meq = 1) for this problem, statement by statement from the published
+ * algorithm (Goldfarb & Idnani 1983 as coded in Turlach's solve.QP.f, LINPACK dpofa / dposl /
+ * dpori; quadprog itself is not in this image, so parity with it is unpinned). dm is G column-major
+ * (dm[j][i] = G(i, j)), n the equality's normal A[1], B its right-hand side. Returns sol[0]. */
+enum { QP_N = 10 };
+static double qpgen2_one_equality(double dm[QP_N][QP_N], const double n[QP_N], double B) {
+  const int N = QP_N;
+  /* vsmall: the machine-precision probe at the top of qpgen2 */
+  volatile double vsmall = 1e-60, tmpa, tmpb;
+  do {
+    vsmall = vsmall + vsmall;
+    tmpa = vsmall * 0.1 + 1.0;
+    tmpb = vsmall * 0.2 + 1.0;
+  } while (tmpa <= 1.0 || tmpb <= 1.0);
+  /* dpofa: G = R'R in the upper triangle, column j from its predecessors */
+  for (int j = 0; j < N; ++j) {
+    double s = 0.0;
+    for (int k = 0; k < j; ++k) {
+      double dot = 0.0; /* ddot(k-1, a(1,k), a(1,j)) */
+      for (int l = 0; l < k; ++l) dot = dot + dm[k][l] * dm[j][l];
+      double t = dm[j][k] - dot;
+      t = t / dm[k][k];
+      dm[j][k] = t;
+      s = s + t * t;
+    }
+    s = dm[j][j] - s;
+    dm[j][j] = sqrt(s);
+  }
+  /* dposl: sol = G^-1 a with a = -q = -0.0 (qpsolvers negates the zero q), R'y = a then R x = y:
+   * every entry stays -0.0 (the unconstrained minimiser) */
+  double sol[QP_N];
+  for (int i = 0; i < N; ++i) sol[i] = -0.0;
+  for (int k = 0; k < N; ++k) {
+    double dot = 0.0;
+    for (int l = 0; l < k; ++l) dot = dot + dm[k][l] * sol[l];
+    sol[k] = (sol[k] - dot) / dm[k][k];
+  }
+  for (int k = N - 1; k >= 0; --k) {
+    sol[k] = sol[k] / dm[k][k];
+    const double t = -sol[k];
+    if (t != 0.0)
+      for (int l = 0; l < k; ++l) sol[l] = sol[l] + t * dm[k][l];
+  }
+  /* dpori: R^-1 in place */
+  for (int k = 0; k < N; ++k) {
+    dm[k][k] = 1.0 / dm[k][k];
+    const double t = -dm[k][k];
+    for (int i = 0; i < k; ++i) dm[k][i] = t * dm[k][i]; /* dscal(k-1, t, a(1,k)) */
+    for (int j = k + 1; j < N; ++j) {
+      const double tj = dm[j][k];
+      dm[j][k] = 0.0;
+      if (tj == 0.0) continue; /* daxpy returns at once for a zero multiplier */
+      for (int i = 0; i <= k; ++i) dm[j][i] = dm[j][i] + tj * dm[k][i];
+    }
+  }
+  /* "set lower triangular of dmat to zero": J = dmat */
+  for (int j = 0; j < N; ++j)
+    for (int i = j + 1; i < N; ++i) dm[j][i] = 0.0;
+  /* the constraint C = -n, b = -B (qpsolvers' sign convention) and its residual at sol */
+  double amat[QP_N], bvec = -B;
+  for (int i = 0; i < N; ++i) amat[i] = -n[i];
+  double sum = -bvec;
+  for (int j = 0; j < N; ++j) sum = sum + amat[j] * sol[j];
+  if (fabs(sum) < vsmall) sum = 0.0;
+  if (sum > 0.0) { /* an equality with a positive residual is negated */
+    for (int j = 0; j < N; ++j) amat[j] = -amat[j];
+    bvec = -bvec;
+  }
+  const double sv = -fabs(sum);
+  if (!(sv < 0.0)) return sol[0]; /* nothing violated: the unconstrained minimiser */
+  /* d = J'n+, z = J d (no active constraints yet: all of J), t = -sv / z'n+, sol += t z */
+  double d[QP_N], z[QP_N];
+  for (int i = 0; i < N; ++i) {
+    double s = 0.0;
+    for (int j = 0; j < N; ++j) s = s + dm[i][j] * amat[j];
+    d[i] = s;
+  }
+  for (int i = 0; i < N; ++i) z[i] = 0.0;
+  for (int j = 0; j < N; ++j)
+    for (int i = 0; i < N; ++i) z[i] = z[i] + dm[j][i] * d[j];
+  double ztn = 0.0;
+  for (int i = 0; i < N; ++i) ztn = ztn + z[i] * amat[i];
+  const double tt = -sv / ztn;
+  for (int i = 0; i < N; ++i) sol[i] = sol[i] + tt * z[i];
+  return sol[0];
+}
+
 /* mpc_1d(x0, v0, xt, vt, t).action(): helper.py:152-191. */
 static double mpc_first_accel(double x0, double v0, double xt, double vt, double t) {
   enum { T = 10 };
@@ -78,44 +167,18 @@ static double mpc_first_accel(double x0, double v0, double xt, double vt, double
   }
   (void)xt; /* the position row of the constraint is dropped by the reference (:173) */
   const double rhs = vt - (pw[1][0] * x0 + pw[1][1] * v0);
-  /* P = D'D + 0.01 I, D[i][i] = 1, D[i][i+1] = -1 (i < T-1) */
-  double P[T][T];
-  memset(P, 0, sizeof(P));
+  /* P = D'D + 0.01 I, D[i][i] = 1, D[i][i+1] = -1 (i < T-1): dmat, stored column-major as in
+   * Fortran, dm[j][i] = dmat(i+1, j+1) */
+  double dm[T][T];
+  memset(dm, 0, sizeof(dm));
   for (int i = 0; i < T - 1; ++i) {
-    P[i][i] += 1.0;
-    P[i + 1][i + 1] += 1.0;
-    P[i][i + 1] -= 1.0;
-    P[i + 1][i] -= 1.0;
+    dm[i][i] += 1.0;
+    dm[i + 1][i + 1] += 1.0;
+    dm[i + 1][i] -= 1.0;
+    dm[i][i + 1] -= 1.0;
   }
-  for (int i = 0; i < T; ++i) P[i][i] += 0.01;
-  /* Cholesky P = L L' */
-  double L[T][T];
-  memset(L, 0, sizeof(L));
-  for (int j = 0; j < T; ++j) {
-    double s = P[j][j];
-    for (int k = 0; k < j; ++k) s -= L[j][k] * L[j][k];
-    L[j][j] = sqrt(s);
-    for (int i = j + 1; i < T; ++i) {
-      double v = P[i][j];
-      for (int k = 0; k < j; ++k) v -= L[i][k] * L[j][k];
-      L[i][j] = v / L[j][j];
-    }
-  }
-  /* z = P^-1 n with n = A[1] (the equality's normal); u = rhs / (n'z) * z */
-  double y[T], z[T];
-  for (int i = 0; i < T; ++i) {
-    double v = A[1][i];
-    for (int k = 0; k < i; ++k) v -= L[i][k] * y[k];
-    y[i] = v / L[i][i];
-  }
-  for (int i = T - 1; i >= 0; --i) {
-    double v = y[i];
-    for (int k = i + 1; k < T; ++k) v -= L[k][i] * z[k];
-    z[i] = v / L[i][i];
-  }
-  double nz = 0.0;
-  for (int i = 0; i < T; ++i) nz += A[1][i] * z[i];
-  return (rhs / nz) * z[0];
+  for (int i = 0; i < T; ++i) dm[i][i] += 0.01;
+  return qpgen2_one_equality(dm, A[1], rhs);
 }
 
 /* corners(agent, y=x, x=y, 0) (merging_env.py:232-239) as a closed box */
@@ -223,15 +286,39 @@ static uint32_t env_step(oracle_env* e, int a1, int a2, double o[10], double rew
   return st;
 }
 
+/* The training scripts' per-episode bookkeeping, literally (the reference has no vector env):
+ *   main.py:191     ep_reward = 0 at reset (env_reset zeroes it);
+ *   main.py:209-211 `if env.winner is not 1: ... ep_reward += reward` after each step
+ *                   (oracle_note_step below);
+ *   main.py:225     win if state[8] > state[3], state = the observation the last step acted on
+ *                   (win_pre: END_POINT - pos2 > END_POINT - pos1 before that step, obs :125, :130);
+ *   hdqn.py:312     ep_reward += reward every step = r1_accumulate;
+ *   hdqn.py:342     the same test on the terminal observation.
+ * ret_sum[3] = (sum r1_accumulate, sum r2_accumulate, sum main.py ep_reward); counts[6] =
+ * (episodes, collisions, winner == 1, steps, main.py wins, hdqn.py wins). */
+static int win_test(const oracle_env* e) { /* state[8] > state[3] of observe() */
+  return (END_POINT - e->pos2) > (END_POINT - e->pos1);
+}
+
+static void oracle_note_step(oracle_env* e, const double rew[2]) {
+  if (e->winner != 1) e->ep_reward_main += rew[0];
+}
+
 /* Episode bookkeeping + gym.vector autoreset (obs <- reset obs, fobs <- terminal obs). */
-static void finish_episode(oracle_env* e, int coll, double* o, double* fobs, double* ret_sum,
+static void finish_episode(oracle_env* e, int coll, int win_pre, double* o, double* fobs, double* ret_sum,
                            uint32_t* counts) {
-  if (ret_sum) { ret_sum[0] += e->r1_acc; ret_sum[1] += e->r2_acc; }
+  if (ret_sum) {
+    ret_sum[0] += e->r1_acc;
+    ret_sum[1] += e->r2_acc;
+    ret_sum[2] += e->ep_reward_main;
+  }
   if (counts) {
     counts[0] += 1;
     counts[1] += coll ? 1u : 0u;
     counts[2] += e->winner == 1 ? 1u : 0u;
     counts[3] += (uint32_t)e->steps;
+    counts[4] += win_pre ? 1u : 0u;
+    counts[5] += win_test(e) ? 1u : 0u;
   }
   if (fobs) memcpy(fobs, o, 10 * sizeof(double));
   env_reset(e, o);
@@ -306,6 +393,11 @@ int32_t oracle_max_threads(void) {
 #endif
 }
 
+/* observe() (merging_env.py:118-132) of n envs, no state change: obs[n,10] f64 */
+void oracle_observe_batch(const oracle_env* envs, int64_t n, double* obs) {
+  for (int64_t i = 0; i < n; ++i) observe(&envs[i], obs + 10 * i);
+}
+
 void oracle_reset_batch(oracle_env* envs, int64_t n, double* obs) {
   for (int64_t i = 0; i < n; ++i) env_reset(&envs[i], obs ? obs + 10 * i : NULL);
 }
@@ -321,13 +413,16 @@ int32_t oracle_step_batch(oracle_env* envs, int64_t n, const int8_t* a1, const i
   for (int64_t i = 0; i < n; ++i) {
     double o[10] = {0}, r[2] = {0, 0};
     int c = 0;
+    const int win_pre = win_test(&envs[i]);
     const uint32_t st = env_step(&envs[i], a1[i], a2 ? a2[i] : -1, o, r, &c);
     if (st & ST_ERR1) err |= 1;
     if (st & ST_ERR2) err |= 2;
-    const int d = (st & (ST_ERR1 | ST_ERR2)) ? 0 : envs[i].done;
+    const int bad = (st & (ST_ERR1 | ST_ERR2)) != 0;
+    if (!bad) oracle_note_step(&envs[i], r);
+    const int d = bad ? 0 : envs[i].done;
     if (autoreset && d)
-      finish_episode(&envs[i], c, o, final_obs ? final_obs + 10 * i : NULL,
-                     ret_sum ? ret_sum + 2 * i : NULL, counts ? counts + 4 * i : NULL);
+      finish_episode(&envs[i], c, win_pre, o, final_obs ? final_obs + 10 * i : NULL,
+                     ret_sum ? ret_sum + 3 * i : NULL, counts ? counts + 6 * i : NULL);
     if (obs) memcpy(obs + 10 * i, o, sizeof(o));
     if (rew) { rew[2 * i] = r[0]; rew[2 * i + 1] = r[1]; }
     if (done) done[i] = (uint8_t)d;
@@ -347,10 +442,12 @@ int64_t oracle_rollout_random(oracle_env* envs, int64_t n, int64_t steps, uint64
       int x, y, c = 0;
       double o[10], r[2];
       draw_actions(env_offset + i, seed, first_step + (uint64_t)k, opp_random, &x, &y);
+      const int win_pre = win_test(&envs[i]);
       env_step(&envs[i], x, y, o, r, &c);
+      oracle_note_step(&envs[i], r);
       if (envs[i].done)
-        finish_episode(&envs[i], c, o, NULL, ret_sum ? ret_sum + 2 * i : NULL,
-                       counts ? counts + 4 * i : NULL);
+        finish_episode(&envs[i], c, win_pre, o, NULL, ret_sum ? ret_sum + 3 * i : NULL,
+                       counts ? counts + 6 * i : NULL);
     }
   }
   return n * steps;

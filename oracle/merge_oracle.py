@@ -17,7 +17,7 @@ Two restatements of the reference algorithm live here:
 Parity pinning: both are checked against tests/golden/reference_golden.npz, produced by
 running the reference's own MergeEnv (tests/golden/gen_golden.py). Three third-party
 boundaries (quadprog's QP solve, pygame Rect/Vector2, shapely intersects) were not
-installable here; the oracle restates them (KKT/Goldfarb-Idnani equality step, C (int)
+installable here; the oracle restates them (quadprog's qpgen2 equality step, C (int)
 truncation + fp64 corner arithmetic, closed-box overlap) and their parity is pinned only
 through the reference's call sites ("Oracle").
 """
@@ -25,6 +25,7 @@ through the reference's call sites ("Oracle").
 from __future__ import annotations
 
 import ctypes
+import math
 import os
 import subprocess
 
@@ -50,31 +51,99 @@ def arc_position(lon, ego: bool):
     return x, (W / 2 + bulge) if ego else (W / 2 - bulge)
 
 
-def first_accel(x0, v0, xt, vt, t):
-    """mpc_1d(...).action() (helper.py:152-191) restated.
+_QP_CACHE = {}
 
-    The reference builds the 10-step double-integrator constraint A (2 x 10), keeps only its
-    velocity row (:172-173, :182) and asks quadprog for min u'Pu with P = D'D + 0.01 I,
-    D the first-difference operator, subject to A[1] u = vt - v0. Starting from the
-    unconstrained minimiser u = 0, the Goldfarb-Idnani method adds the single equality in
-    one step: z = P^-1 n, u = (b / n'z) z. That step is computed here with numpy.
-    """
+
+def qpgen2_factor(t):
+    """The part of quadprog 0.1.11's qpgen2 that depends only on the horizon t, for mpc_1d's QP
+    (helper.py:152-191 -> qpsolvers 1.8.0 -> quadprog.solve_qp, G = P = D'D + 0.01 I, one
+    equality with normal n = A[1]): dpofa (G = R'R), dpori (J = R^-1, lower triangle zeroed), then
+    for the normal n: d = J'n, z = J d and z'n, each sum in the Fortran loop order; plus qpgen2's
+    vsmall probe. Restated from the published algorithm (Goldfarb & Idnani 1983 as coded in
+    Turlach's solve.QP.f; LINPACK dpofa / dpori); quadprog is not in this image, so bit parity
+    with it is unpinned. Returns (n, z, z'n, vsmall) for n of the positive sign."""
+    if t in _QP_CACHE:
+        return _QP_CACHE[t]
     steps = 10
     dt = t / steps
-    a = np.array([[1.0, dt], [0.0, 1.0]])
-    b = np.array([0.0, dt])
-    A = np.zeros((2, steps))
-    power = np.eye(2)
-    for i in reversed(range(steps)):
-        A[:, i] = power @ b
-        power = a @ power
-    rhs = vt - (power @ np.array([x0, v0]))[1]
-    D = np.eye(steps - 1, steps) - np.eye(steps - 1, steps, k=1)
-    P = D.T @ D + 0.01 * np.eye(steps)
-    n = A[1]
-    z = np.linalg.solve(P, n)
-    u = (rhs / (n @ z)) * z
-    return u[0]
+    # A[1] = row [0 1] of a^k b for k = 9..0 (helper.py:166-170): 0 * 0 + 1 * dt
+    n = [0.0 * 0.0 + 1.0 * dt for _ in range(steps)]
+    g = [[0.0] * steps for _ in range(steps)]  # g[i][j] = G(i, j), symmetric
+    for i in range(steps - 1):
+        g[i][i] += 1.0
+        g[i + 1][i + 1] += 1.0
+        g[i][i + 1] -= 1.0
+        g[i + 1][i] -= 1.0
+    for i in range(steps):
+        g[i][i] += 0.01
+    a = [row[:] for row in g]
+    for j in range(steps):  # dpofa: upper triangle
+        s = 0.0
+        for k in range(j):
+            dot = 0.0
+            for m in range(k):
+                dot = dot + a[m][k] * a[m][j]
+            tk = (a[k][j] - dot) / a[k][k]
+            a[k][j] = tk
+            s = s + tk * tk
+        a[j][j] = math.sqrt(a[j][j] - s)
+    for k in range(steps):  # dpori
+        a[k][k] = 1.0 / a[k][k]
+        tk = -a[k][k]
+        for i in range(k):
+            a[i][k] = tk * a[i][k]
+        for j in range(k + 1, steps):
+            tj = a[k][j]
+            a[k][j] = 0.0
+            if tj != 0.0:
+                for i in range(k + 1):
+                    a[i][j] = a[i][j] + tj * a[i][k]
+    for j in range(steps):  # lower triangle of dmat set to zero
+        for i in range(j + 1, steps):
+            a[i][j] = 0.0
+    d = []
+    for i in range(steps):
+        s = 0.0
+        for j in range(steps):
+            s = s + a[j][i] * n[j]
+        d.append(s)
+    z = [0.0] * steps
+    for j in range(steps):
+        for i in range(steps):
+            z[i] = z[i] + a[i][j] * d[j]
+    ztn = 0.0
+    for i in range(steps):
+        ztn = ztn + z[i] * n[i]
+    vsmall = 1e-60
+    while True:
+        vsmall = vsmall + vsmall
+        if vsmall * 0.1 + 1.0 > 1.0 and vsmall * 0.2 + 1.0 > 1.0:
+            break
+    _QP_CACHE[t] = (n, z, ztn, vsmall)
+    return _QP_CACHE[t]
+
+
+def first_accel(x0, v0, xt, vt, t):
+    """mpc_1d(...).action() (helper.py:152-191) restated as quadprog's qpgen2 solves it.
+
+    The reference keeps only the velocity row of the 10-step constraint (:172-173, :182): the
+    residual is b = vt - (0 x0 + 1 v0), the equality's normal n = A[1]. qpsolvers hands quadprog
+    C = -n, b_c = -b; qpgen2 starts at the unconstrained minimiser sol = 0, evaluates the
+    residual -b_c + C'sol, zeroes it below vsmall, negates an equality whose residual is positive,
+    and takes the full step t = -sv / z'n along z = J J'n. The sign flips are exact negations, so
+    the magnitudes come from qpgen2_factor(t)."""
+    n, z, ztn, vsmall = qpgen2_factor(t)
+    rhs = vt - (0.0 * x0 + 1.0 * v0)
+    sol0 = -0.0  # dposl on a = -q = -0.0 leaves every entry -0.0 (the unconstrained minimiser)
+    res = rhs  # -b_c + sum(C * sol), the products all zero
+    if abs(res) < vsmall:
+        res = 0.0
+    if not res:
+        return sol0  # nothing violated
+    sign = 1.0 if res > 0 else -1.0  # positive residual: C negated back to +n
+    sv = -abs(res)
+    tt = -sv / ztn
+    return sol0 + tt * (sign * z[0])
 
 
 def vehicle_box(lateral, longitudinal):
@@ -195,13 +264,22 @@ class OracleEnvC(ctypes.Structure):
         ("pos1", ctypes.c_double), ("vel1", ctypes.c_double), ("acc1", ctypes.c_double),
         ("pos2", ctypes.c_double), ("vel2", ctypes.c_double), ("acc2", ctypes.c_double),
         ("time_stamp", ctypes.c_double), ("r1_acc", ctypes.c_double), ("r2_acc", ctypes.c_double),
-        ("winner", ctypes.c_int32), ("done", ctypes.c_int32),
+        ("ep_reward_main", ctypes.c_double), ("winner", ctypes.c_int32), ("done", ctypes.c_int32),
         ("steps", ctypes.c_int32), ("pad_", ctypes.c_int32),
     ]
 
 
+STATS_DOC = "ret_sum [n,3]: r1_accumulate, r2_accumulate, main.py ep_reward; counts [n,6]: " \
+    "episodes, collisions, ego_first, steps, win_main, win_hdqn"
+
+
+def new_stats(n):
+    """Zeroed (ret_sum [n,3] f64, counts [n,6] u32) for COracle.step / rollout_random."""
+    return np.zeros((n, 3)), np.zeros((n, 6), np.uint32)
+
+
 ENV_DTYPE = np.dtype([(n, np.float64) for n in (
-    "pos1", "vel1", "acc1", "pos2", "vel2", "acc2", "time_stamp", "r1_acc", "r2_acc")]
+    "pos1", "vel1", "acc1", "pos2", "vel2", "acc2", "time_stamp", "r1_acc", "r2_acc", "ep_reward_main")]
     + [("winner", np.int32), ("done", np.int32), ("steps", np.int32), ("pad_", np.int32)])
 
 
@@ -227,6 +305,7 @@ class COracle:
         lib = ctypes.CDLL(path)
         P = ctypes.POINTER
         lib.oracle_reset_batch.argtypes = [ctypes.c_void_p, ctypes.c_int64, P(ctypes.c_double)]
+        lib.oracle_observe_batch.argtypes = [ctypes.c_void_p, ctypes.c_int64, P(ctypes.c_double)]
         lib.oracle_step_batch.argtypes = [
             ctypes.c_void_p, ctypes.c_int64, P(ctypes.c_int8), P(ctypes.c_int8), ctypes.c_int32,
             P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_uint8), P(ctypes.c_uint8),
@@ -259,6 +338,12 @@ class COracle:
     def new_envs(n: int) -> np.ndarray:
         return np.zeros(n, dtype=ENV_DTYPE)
 
+    def observe(self, envs: np.ndarray) -> np.ndarray:
+        """observe() (merging_env.py:118-132) of every env in fp64, no state change."""
+        obs = np.empty((len(envs), 10), np.float64)
+        self.lib.oracle_observe_batch(envs.ctypes.data, len(envs), _ptr(obs, ctypes.c_double))
+        return obs
+
     def reset(self, envs: np.ndarray) -> np.ndarray:
         obs = np.empty((len(envs), 10), np.float64)
         self.lib.oracle_reset_batch(envs.ctypes.data, len(envs), _ptr(obs, ctypes.c_double))
@@ -266,7 +351,11 @@ class COracle:
 
     def step(self, envs, a1, a2=None, autoreset=False, final_obs=False, stats=None):
         """One step of every env. Returns obs[n,10] f64, rew[n,2] f64, done[n] u8, coll[n] u8,
-        status[n] u32 (MG_ST_* bits), and final_obs[n,10] (NaN rows for envs not finished)."""
+        status[n] u32 (MG_ST_* bits), and final_obs[n,10] (NaN rows for envs not finished).
+        stats = (ret_sum [n,3] f64, counts [n,6] u32), accumulated at autoreset: the sums of
+        r1_accumulate, r2_accumulate and main.py's winner-filtered ep_reward; episodes,
+        collisions, ego-first arrivals, steps, main.py:225 wins and hdqn.py:342 wins
+        (STATS_DOC)."""
         n = len(envs)
         a1 = np.ascontiguousarray(a1, np.int8)
         a2 = None if a2 is None else np.ascontiguousarray(a2, np.int8)
@@ -348,6 +437,42 @@ def qnet_reference(weights, obs, bf16: bool = True, swap: bool = False):
 
 
 # --------------------------------------------------------------------------- replay memory oracle
+
+def goal_status64(obs):
+    """hdqn.py's goal_status (:223-236) of fp64 observation rows [N, 10] (dx1 = obs[:, 0],
+    v2 = obs[:, 9]), evaluated in fp64 as the reference's Python floats are."""
+    obs = np.asarray(obs, np.float64)
+    dx1, v2 = obs[:, 0], obs[:, 9]
+    return np.where(dx1 < -0.5 * v2, 0, np.where(dx1 < 0.5 * v2, 1, 2))
+
+
+def oracle_envs_from(coracle, state, idx=None):
+    """C-oracle envs holding a device batch's state (MergeVecEnv or its state_dict), for replaying
+    it from mid-episode: positions, speeds, returns, step count, winner, the float clock the
+    count stands for, and main.py's running ep_reward (r1_accumulate, or the ego's
+    ret1_pending once winner == 1 -- what the device keeps, include/merging_hip.h)."""
+    get = (lambda name: getattr(state, name)) if not isinstance(state, dict) else state.__getitem__
+    sel = (lambda t: t) if idx is None else (lambda t: t[idx])
+    host = lambda name: sel(get(name)).cpu().numpy()  # noqa: E731
+    tf = host("tf").astype(np.int64) & 0xFFFF
+    n = len(tf)
+    envs = coracle.new_envs(n)
+    for name, key in (("p1", "pos1"), ("v1", "vel1"), ("p2", "pos2"), ("v2", "vel2"), ("ret1", "r1_acc"),
+                      ("ret2", "r2_acc")):
+        envs[key] = host(name)
+    envs["steps"] = tf & 0x1FFF
+    envs["winner"] = (tf & 0x6000) >> 13
+    envs["done"] = (tf & 0x8000) != 0
+    envs["time_stamp"] = np.cumsum(np.full(8200, 0.2))[np.maximum(envs["steps"] - 1, 0)] * (envs["steps"] > 0)
+    pending = None
+    if isinstance(state, dict) and "episode_stats" in state:
+        pending = sel(state["episode_stats"])[:, 3].cpu().numpy()
+    elif not isinstance(state, dict) and getattr(state, "_ep_stats", None) is not None:
+        pending = sel(state._ep_stats)[:, 3].cpu().numpy()
+    envs["ep_reward_main"] = envs["r1_acc"] if pending is None else np.where(envs["winner"] == 1, pending,
+                                                                              envs["r1_acc"])
+    return envs
+
 
 def step_with_won(coracle, envs, a1, a2=None):
     """One autoreset step of the C oracle that also reports env.winner == 1 after the step,

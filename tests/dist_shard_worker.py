@@ -1,7 +1,7 @@
 """One rank of the sharded-run GPU test (tests/test_gpu_distributed.py), launched by
 torch.distributed.run with the gloo backend; every rank steps its own contiguous shard of the
 global batch on cuda:0 (the test box has one GPU) exactly as bench.py's ranks do on their own
-GPUs, then the statistics are gathered -- the 48-byte summary (the default collective) and the
+GPUs, then the statistics are gathered -- the 72-byte summary (the default collective) and the
 per-env rows (opt-in) -- and rank 0 saves both with its shard bookkeeping.
 
     python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 \
@@ -36,12 +36,12 @@ def main():
         env.rollout_random(T, seed, first_step=k)
         k += T
     torch.cuda.synchronize()
-    summary = gather_episode_summary(env.ret_sum, env.counts)
-    ret_sum, counts = gather_episode_stats(env.ret_sum, env.counts)
+    summary = gather_episode_summary(env.returns, env.counts)
+    returns, counts = gather_episode_stats(env.returns, env.counts)
     p1 = [torch.empty(count, dtype=torch.float64) for _ in range(world)]
     dist.all_gather(p1, env.p1.cpu())
     if rank == 0:
-        torch.save({"summary": summary, "ret_sum": ret_sum.cpu(), "counts": counts.cpu(),
+        torch.save({"summary": summary, "returns": returns.cpu(), "counts": counts.cpu(),
                     "p1": torch.cat(p1), "world": world}, out)
     dist.barrier()
     dist.destroy_process_group()

@@ -13,8 +13,10 @@ lon2coord (:48-58) and mpc_1d's matrix build (scripts/helper.py:152-191). The st
 restate the arithmetic at three third-party boundaries, so parity there is pinned only by
 these restatements (see DESIGN.md "Oracle"):
 
-  * qpsolvers.solve_qp -> the equality-constrained KKT system solved with numpy.linalg.solve
-    (quadprog differs from it by fp64 rounding, ~1e-15 relative);
+  * qpsolvers.solve_qp -> quadprog's qpgen2 (the Goldfarb-Idnani dual method as coded in
+    Turlach's solve.QP.f: LINPACK dpofa / dposl / dpori, the vsmall precision probe, the sign
+    flip of an equality, the full step along z = J J'n), restated statement by statement on the
+    arrays the reference builds (until round 2: a KKT numpy.linalg.solve, an ulp away);
   * pygame Rect(center=...) -> C (int) truncation of the float centre, x = cx - w//2
     (pygame 2.1.2 pg_IntFromObj + pg_rect_setcenter); Vector2 +,-,scalar* in fp64 and
     rotate(0) = identity (pygame special-cases multiples of 90 degrees);
@@ -195,18 +197,89 @@ _SHIMS = {
                 pass
     """,
     "qpsolvers.py": """
+        import math
         import numpy as np
         def solve_qp(P, q, G=None, h=None, A=None, b=None, **kw):
-            # min 1/2 x'Px + q'x  s.t. Ax = b  (the only form helper.mpc_1d uses)
+            # qpsolvers 1.8.0 -> quadprog 0.1.11 for the one form helper.mpc_1d uses (one equality,
+            # no inequality): quadprog.solve_qp(G=P, a=-q, C=-A', b=-b, meq=1), i.e. qpgen2's
+            # dual active-set method (Goldfarb & Idnani; Turlach's solve.QP.f with LINPACK dpofa /
+            # dposl / dpori), restated statement by statement on the reference's own arrays.
             A = np.atleast_2d(np.asarray(A, dtype=float))
-            b = np.atleast_1d(np.asarray(b, dtype=float))
-            n, m = P.shape[0], A.shape[0]
-            K = np.zeros((n + m, n + m))
-            K[:n, :n] = P
-            K[:n, n:] = A.T
-            K[n:, :n] = A
-            rhs = np.concatenate([-np.asarray(q, dtype=float), b])
-            return np.linalg.solve(K, rhs)[:n]
+            assert A.shape[0] == 1 and G is None and h is None, 'stand-in: one equality only'
+            n = P.shape[0]
+            d = [[float(P[i][j]) for j in range(n)] for i in range(n)]   # d[i][j] = dmat(i+1, j+1)
+            dvec = [-float(x) for x in np.asarray(q, dtype=float)]       # a = -q (-0.0 for q = 0)
+            amat = [-float(x) for x in A[0]]                              # C = -A'
+            bvec = -float(np.atleast_1d(np.asarray(b, dtype=float))[0])   # b_c = -b
+            vsmall = 1e-60
+            while True:                                                   # qpgen2's precision probe
+                vsmall = vsmall + vsmall
+                if vsmall * 0.1 + 1.0 > 1.0 and vsmall * 0.2 + 1.0 > 1.0:
+                    break
+            for j in range(n):                                            # dpofa
+                s = 0.0
+                for k in range(j):
+                    dot = 0.0
+                    for l in range(k):
+                        dot = dot + d[l][k] * d[l][j]
+                    t = (d[k][j] - dot) / d[k][k]
+                    d[k][j] = t
+                    s = s + t * t
+                s = d[j][j] - s
+                assert s > 0.0, 'matrix not positive definite'
+                d[j][j] = math.sqrt(s)
+            for k in range(n):                                            # dposl: R'y = a ...
+                dot = 0.0
+                for l in range(k):
+                    dot = dot + d[l][k] * dvec[l]
+                dvec[k] = (dvec[k] - dot) / d[k][k]
+            for k in reversed(range(n)):                                  # ... then R x = y
+                dvec[k] = dvec[k] / d[k][k]
+                t = -dvec[k]
+                if t != 0.0:
+                    for l in range(k):
+                        dvec[l] = dvec[l] + t * d[l][k]
+            for k in range(n):                                            # dpori: J = R^-1
+                d[k][k] = 1.0 / d[k][k]
+                t = -d[k][k]
+                for l in range(k):
+                    d[l][k] = t * d[l][k]
+                for j in range(k + 1, n):
+                    t = d[k][j]
+                    d[k][j] = 0.0
+                    if t != 0.0:
+                        for l in range(k + 1):
+                            d[l][j] = d[l][j] + t * d[l][k]
+            for j in range(n):                                            # lower triangle := 0
+                for i in range(j + 1, n):
+                    d[i][j] = 0.0
+            sol = list(dvec)
+            sv = -bvec                                                    # the residual at sol
+            for j in range(n):
+                sv = sv + amat[j] * sol[j]
+            if abs(sv) < vsmall:
+                sv = 0.0
+            if sv > 0.0:                                                  # equality: flip its sign
+                amat = [-x for x in amat]
+                bvec = -bvec
+            sv = -abs(sv)
+            if not (sv < 0.0):                                            # nothing violated
+                return np.asarray(sol)
+            dd = []
+            for i in range(n):                                            # d = J'n+
+                s = 0.0
+                for j in range(n):
+                    s = s + d[j][i] * amat[j]
+                dd.append(s)
+            z = [0.0] * n                                                 # z = J d
+            for j in range(n):
+                for i in range(n):
+                    z[i] = z[i] + d[i][j] * dd[j]
+            ztn = 0.0
+            for i in range(n):
+                ztn = ztn + z[i] * amat[i]
+            tt = -sv / ztn                                                # the full step
+            return np.asarray([sol[i] + tt * z[i] for i in range(n)])
     """,
 }
 

@@ -56,7 +56,8 @@ def load_reference_env_recording():
     shutil.rmtree(os.path.join(shim_dir, "pygame"))  # the recording stand-in replaces it
     os.environ.setdefault("MPLBACKEND", "Agg")
     sys.dont_write_bytecode = True
-    sys.path[:0] = [STUBS, shim_dir, os.path.join(REFERENCE, "scripts"), REFERENCE]
+    # the shims first (gym etc.; their pygame is removed), so pygame resolves to the recording stub
+    sys.path[:0] = [shim_dir, STUBS, os.path.join(REFERENCE, "scripts"), REFERENCE]
     import pygame  # the recording stand-in
 
     assert os.path.dirname(pygame.__file__) == os.path.join(STUBS, "pygame"), pygame.__file__

@@ -78,6 +78,11 @@ int main() {
   bad += expect_error(mg_rollout_hdqn(&p, &sf, &tj0, &htm, nullptr, g8, nullptr, nullptr, 16, 0, 1, 0, 4, fake, 3,
                                       fake, 0, 1ull << 31, 0, nullptr, nullptr, nullptr, nullptr, 0, 0, nullptr),
                       "Goal_DQN outputs without ext_acc");
+  bad += expect_error(mg_rollout_hdqn(&p, &sf, &tj0, &ht, nullptr, g8, nullptr, nullptr, 16, 0, 1, 0, 4, fake, 3, fake, 0,
+                                      1ull << 31, 0, nullptr, nullptr, nullptr, nullptr, 0, 0, nullptr),
+                      "h-DQN loop without MG_AUTORESET");
+  bad += expect_error(mg_goal_status(nullptr, static_cast<double*>(fake), g8, 4, nullptr), "goal_status NULL");
+  bad += expect_error(mg_rollout_random(&p, &sf, &tj0, nullptr, 16, 0, 1, 0, 65536, 1, 0, nullptr), "T > 65535");
   if (mg_replay_scratch_bytes(1 << 20, 16) != 8 + 1024 * 8 + 65536 * 4 + 1024 * 4) bad += 1;
   if (mg_qnet_packed_bytes() % 16 != 0) bad += 1;
   // empty batches return before any launch

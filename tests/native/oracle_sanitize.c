@@ -8,7 +8,7 @@
 #include <string.h>
 
 typedef struct oracle_env { /* oracle/merge_oracle.c */
-  double pos1, vel1, acc1, pos2, vel2, acc2, time_stamp, r1_acc, r2_acc;
+  double pos1, vel1, acc1, pos2, vel2, acc2, time_stamp, r1_acc, r2_acc, ep_reward_main;
   int32_t winner, done, steps, pad_;
 } oracle_env;
 
@@ -28,8 +28,8 @@ int main(void) {
   double* obs = malloc(sizeof(double) * N * 10);
   double* fobs = malloc(sizeof(double) * N * 10);
   double* rew = malloc(sizeof(double) * N * 2);
-  double* ret_sum = calloc(N * 2, sizeof(double));
-  uint32_t* counts = calloc(N * 4, sizeof(uint32_t));
+  double* ret_sum = calloc(N * 3, sizeof(double)); /* [N,3] */
+  uint32_t* counts = calloc(N * 6, sizeof(uint32_t)); /* [N,6] */
   uint32_t* status = malloc(sizeof(uint32_t) * N);
   uint32_t* u = malloc(sizeof(uint32_t) * N * 4);
   uint8_t *done = malloc(N), *coll = malloc(N);

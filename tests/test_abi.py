@@ -35,15 +35,16 @@ def test_library_exports_every_declared_symbol():
 def test_struct_layouts_match_header():
     from merging_gym import _native
 
-    # mg_params: 15 doubles + 5 doubles + 4 int32 + 4 doubles; mg_rec64: 20 doubles + 2 uint32
-    assert ctypes.sizeof(_native.Params) == 20 * 8 + 16 + 32
+    # mg_params: 15 doubles + 5 doubles + 4 int32 + 5 doubles; mg_rec64: 20 doubles + 2 uint32
+    assert ctypes.sizeof(_native.Params) == 20 * 8 + 16 + 40
     assert ctypes.sizeof(_native.State) == 7 * 8
     assert ctypes.sizeof(_native.Outputs) == 10 * 8
     assert ctypes.sizeof(_native.Traj) == 9 * 8
     assert ctypes.sizeof(_native.Transitions) == 12 * 8
     assert ctypes.sizeof(_native.Stats) == 8
     assert ctypes.sizeof(_native.HdqnTraj) == 6 * 8
-    assert _native.EPISODE_STATS_BYTES == 32  # mg_episode_stats: 2 f64 + 4 u32
+    assert _native.EPISODE_STATS_BYTES == 64  # mg_episode_stats: 4 f64 + 8 u32 (ABI 17)
+    assert _native.EPISODE_STATS_DTYPE.fields["counts"][1] == 32
     assert _native.REC64_DTYPE.itemsize == 168
 
 
@@ -61,17 +62,24 @@ def test_default_params_are_the_reference_constants():
     assert (p.veh_w, p.veh_h, p.timeout_steps) == (4, 8, 2501)
     assert p.angle0 == float(np.arctan2(1000, 30000))
     assert p.inv_R == 1.0 / 30000.0
-    # mpc_1d's equality step (helper.py:152-191): n'P^-1 n and (P^-1 n)[0] for t = 3
-    assert (p.qp_nz, p.qp_z0) == (90.00000000000153, 30.000000000000544)
+    # mpc_1d's equality step (helper.py:152-191) in quadprog's qpgen2 order: z'n and z[0] of
+    # z = J J'n, J = R^-1 (dpofa, dpori), for t = 3; qpgen2's vsmall probe
+    assert (p.qp_nz, p.qp_z0) == (90.0000000000015, 30.000000000000533)
     assert p.qp_inv_nz == 1.0 / p.qp_nz
+    assert p.qp_vsmall == 1.4272476927059598e-15
 
 
 def test_qp_step_constants_reproduce_the_oracle_qp(coracle, golden):
-    """The kernel's u0 = (b / qp_nz) * qp_z0, b = vt - v0 (merging_hip.hip mpc_acc), is bit for
-    bit the first control of the oracle's full QP solve (Cholesky + the equality step), on the
-    golden mpc inputs and on every (action, speed) pair a step can meet."""
+    """The kernel's u0 = (b / qp_nz) * qp_z0, b = vt - v0, or -0.0 where |b| < qp_vsmall
+    (merging_hip.hip mpc_acc) is bit for bit -- sign of zero included -- the first control of the
+    oracle's full qpgen2 solve (dpofa, dposl, dpori, the equality step), and of the Python
+    restatement, on the golden mpc inputs and on every (action, speed) pair a step can meet,
+    including speeds decayed below vsmall under action 0 and speeds equal to the target."""
+    import math
+
     import numpy as np
 
+    import merge_oracle as mo
     from merging_gym import _native
 
     p = _native.default_params()
@@ -81,9 +89,17 @@ def test_qp_step_constants_reproduce_the_oracle_qp(coracle, golden):
               zip(rng.uniform(0, 1100, 4000), np.concatenate([rng.uniform(0, 45, 3000),
                                                               rng.uniform(0, 1e-3, 1000)]),
                   rng.integers(0, 5, 4000))]
+    vs = p.qp_vsmall
+    cases += [(50.0, v, 0.0) for v in (0.0, vs / 2, np.nextafter(vs, 0), vs, np.nextafter(vs, 1), 2 * vs, 1e-300)]
+    cases += [(50.0, 10.0 * a, 10.0 * a) for a in range(5)]  # b = 0 exactly
+    cases += [(50.0, np.nextafter(10.0 * a, 50), 10.0 * a) for a in range(5)]
     for x0, v0, vt in cases:
         ref = coracle.mpc_first_accel(float(x0), float(v0), 0.0, float(vt), 3.0)
-        assert ((float(vt) - float(v0)) / p.qp_nz) * p.qp_z0 == ref, (x0, v0, vt)
+        b = float(vt) - float(v0)
+        kern = -0.0 if abs(b) < vs else (b / p.qp_nz) * p.qp_z0
+        assert kern == ref and math.copysign(1, kern) == math.copysign(1, ref), (x0, v0, vt, kern, ref)
+        py = mo.first_accel(float(x0), float(v0), 0.0, float(vt), 3.0)
+        assert py == ref and math.copysign(1, py) == math.copysign(1, ref), (x0, v0, vt, py, ref)
 
 
 def test_argument_errors_without_gpu():
@@ -143,6 +159,14 @@ def test_argument_errors_without_gpu():
     assert hdqn(None, 0, ring=fake) != 0 and b"ring_counter" in _native.lib.mg_last_error()
     assert hdqn(None, 0, ring=ctypes.c_void_p((1 << 20) + 8), counter=fake, cap=16) != 0
     assert b"16-byte" in _native.lib.mg_last_error()
+    # hdqn.py resets at every episode end: a launch without MG_AUTORESET is refused (ABI 17)
+    assert hdqn(None, 0) != 0 and b"MG_AUTORESET" in _native.lib.mg_last_error()
+    # mg_goal_status: NULL arrays refused; n == 0 is a no-op
+    assert _native.lib.mg_goal_status(None, fake, fake, 4, None) != 0 and b"NULL" in _native.lib.mg_last_error()
+    assert _native.lib.mg_goal_status(fake, fake, fake, 0, None) == 0
+    # the rollout's register-held episode counts are 16-bit per launch: num_steps <= 65535
+    rc = _native.lib.mg_rollout_random(P, st, traj, None, 16, 0, 1, 0, 65536, 1, 0, None)
+    assert rc != 0 and b"65535" in _native.lib.mg_last_error()
     # Goal_DQN's outputs (ext_reward / no_break) need the running sums, ext_acc
     htm = _native.HdqnTraj(None, None, None, None, fake, None)
     rc = _native.lib.mg_rollout_hdqn(P, st, traj, ctypes.byref(htm), None, fake, None, None, 16, 0, 1, 0, 4, fake,

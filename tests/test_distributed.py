@@ -24,8 +24,8 @@ def _worker(rank, world, port, n_per_rank, out_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     g = torch.Generator().manual_seed(rank)
-    ret = torch.randn((n_per_rank, 2), generator=g, dtype=torch.float64)
-    cnt = torch.randint(0, 100, (n_per_rank, 4), generator=g, dtype=torch.int32)
+    ret = torch.randn((n_per_rank, 3), generator=g, dtype=torch.float64)
+    cnt = torch.randint(0, 100, (n_per_rank, 6), generator=g, dtype=torch.int32)
     all_ret, all_cnt = gather_episode_stats(ret, cnt)
     if rank == 0:
         torch.save({"ret": all_ret, "cnt": all_cnt}, out_path)
@@ -41,12 +41,14 @@ def test_gather_episode_stats_gloo(tmp_path):
     exp_ret, exp_cnt = [], []
     for r in range(world):
         g = torch.Generator().manual_seed(r)
-        exp_ret.append(torch.randn((n, 2), generator=g, dtype=torch.float64))
-        exp_cnt.append(torch.randint(0, 100, (n, 4), generator=g, dtype=torch.int32))
+        exp_ret.append(torch.randn((n, 3), generator=g, dtype=torch.float64))
+        exp_cnt.append(torch.randint(0, 100, (n, 6), generator=g, dtype=torch.int32))
     assert torch.equal(res["ret"], torch.cat(exp_ret))  # bit-exact through the int64 packing
     assert torch.equal(res["cnt"], torch.cat(exp_cnt))
     s = summarize(res["ret"], res["cnt"])
-    assert s["completed"] == int(torch.cat(exp_cnt)[:, 0].sum())
+    c = torch.cat(exp_cnt).to(torch.int64).sum(0)
+    assert s["completed"] == int(c[0])
+    assert s["win_rate_main"] == int(c[4]) / int(c[0]) and s["win_rate_hdqn"] == int(c[5]) / int(c[0])
 
 
 def _summary_worker(rank, world, port, n_per_rank, out_path):
@@ -55,8 +57,8 @@ def _summary_worker(rank, world, port, n_per_rank, out_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     g = torch.Generator().manual_seed(10 + rank)
-    ret = torch.randn((n_per_rank, 2), generator=g, dtype=torch.float64)
-    cnt = torch.randint(0, 100, (n_per_rank, 4), generator=g, dtype=torch.int32)
+    ret = torch.randn((n_per_rank, 3), generator=g, dtype=torch.float64)
+    cnt = torch.randint(0, 100, (n_per_rank, 6), generator=g, dtype=torch.int32)
     assert partial_stats(ret, cnt).numel() * 8 == PARTIAL_BYTES
     s = gather_episode_summary(ret, cnt)
     torch.save(s, out_path + f".{rank}")
@@ -64,7 +66,7 @@ def _summary_worker(rank, world, port, n_per_rank, out_path):
 
 
 def test_gather_episode_summary_gloo(tmp_path):
-    """The default collective: 48 bytes per rank, every rank gets the global summary, equal to
+    """The default collective: 72 bytes per rank, every rank gets the global summary, equal to
     summarizing the concatenated per-env statistics (counts exactly, returns to fp64 rounding)."""
     world, n = 2, 1500
     out = str(tmp_path / "s")
@@ -75,8 +77,8 @@ def test_gather_episode_summary_gloo(tmp_path):
     rets, cnts = [], []
     for r in range(world):
         g = torch.Generator().manual_seed(10 + r)
-        rets.append(torch.randn((n, 2), generator=g, dtype=torch.float64))
-        cnts.append(torch.randint(0, 100, (n, 4), generator=g, dtype=torch.int32))
+        rets.append(torch.randn((n, 3), generator=g, dtype=torch.float64))
+        cnts.append(torch.randint(0, 100, (n, 6), generator=g, dtype=torch.int32))
     exp = summarize(torch.cat(rets), torch.cat(cnts))
     for k, v in exp.items():
         if k == "completed":

@@ -1,0 +1,145 @@
+"""The statistics the reference's training scripts log per episode, pinned on the CPU oracles.
+
+tests/golden/replay_golden.npz (gen_replay.py) holds them as the reference's own loops compute
+them over the reference env: scripts/main.py:189-227 (ep_reward summed only after steps where
+`env.winner is not 1`, :209-211; win = `state[8] > state[3]` on the observation the episode's last
+step acted on, :218-225) and scripts/hdqn.py:276-346 (ep_reward = every step's reward, :312;
+the same win test on the terminal observation, :320, :342). The C oracle (literal per-step
+restatement) and the NumPy restatement must give every episode's values bit for bit; so must the
+device kernels (tests/test_gpu_episode_stats.py).
+"""
+
+import os
+
+import numpy as np
+import pytest
+
+import merge_numpy as mn
+import merge_oracle as mo
+from conftest import ROOT
+
+REPLAY = os.path.join(ROOT, "tests", "golden", "replay_golden.npz")
+STATS_TAGS = ["SU0", "SUU", "SFU", "SSU"]
+
+
+@pytest.fixture(scope="module")
+def g():
+    return np.load(REPLAY)
+
+
+def _trace(g, tag):
+    return {k[len(tag) + 1:]: g[k] for k in g.files if k.startswith(tag + "_")}
+
+
+def oracle_episodes(coracle, a1, a2):
+    """Step one C-oracle env through the actions with autoreset; after every episode read and
+    clear its statistics: per-episode (returns [3], counts [6]) rows (merge_oracle.STATS_DOC)."""
+    envs = coracle.new_envs(1)
+    coracle.reset(envs)
+    ret, cnt = mo.new_stats(1)
+    rows_r, rows_c = [], []
+    for t in range(len(a1)):
+        _, _, d, _, _, _, err = coracle.step(envs, a1[t:t + 1], None if a2[t] < 0 else a2[t:t + 1],
+                                             autoreset=True, stats=(ret, cnt))
+        assert err == 0
+        if d[0]:
+            rows_r.append(ret[0].copy())
+            rows_c.append(cnt[0].copy())
+            ret[:] = 0
+            cnt[:] = 0
+    return np.array(rows_r), np.array(rows_c)
+
+
+@pytest.mark.parametrize("tag", STATS_TAGS)
+def test_c_oracle_episode_statistics_equal_reference_loops(coracle, g, tag):
+    tr = _trace(g, tag)
+    r, c = oracle_episodes(coracle, tr["a1"], tr["a2"])
+    assert len(r) == len(tr["length"]) > 20
+    np.testing.assert_array_equal(r[:, 0], tr["hdqn_reward"])  # = r1_accumulate
+    np.testing.assert_array_equal(r[:, 0], tr["r1_accumulate"])
+    np.testing.assert_array_equal(r[:, 1], tr["r2_accumulate"])
+    np.testing.assert_array_equal(r[:, 2], tr["main_reward"])
+    np.testing.assert_array_equal(c[:, 0], 1)
+    np.testing.assert_array_equal(c[:, 1].astype(bool), tr["collision"])
+    np.testing.assert_array_equal(c[:, 2].astype(bool), tr["winner"] == 1)
+    np.testing.assert_array_equal(c[:, 3], tr["length"])
+    np.testing.assert_array_equal(c[:, 4].astype(bool), tr["main_win"])
+    np.testing.assert_array_equal(c[:, 5].astype(bool), tr["hdqn_win"])
+
+
+def test_golden_statistics_cover_the_cases(g):
+    """The recorded trajectories exercise what makes the scripts' statistics differ from the
+    plain ones: ego-first episodes (main.py's filter drops their tail), episodes whose two win
+    tests disagree, and opponent-first / collision endings."""
+    tr = {t: _trace(g, t) for t in STATS_TAGS}
+    filt = sum(int((x["main_reward"] != x["hdqn_reward"]).sum()) for x in tr.values())
+    ego_first = sum(int((x["winner"] == 1).sum()) for x in tr.values())
+    differ = sum(int((x["main_win"] != x["hdqn_win"]).sum()) for x in tr.values())
+    coll = sum(int(x["collision"].sum()) for x in tr.values())
+    assert filt == ego_first > 50 and coll > 10 and differ >= 1, (filt, ego_first, coll, differ)
+    # main.py's sum stops at the ego's first arrival: for an ego-first episode that ends without a
+    # collision it omits the arrival bonus (RFirst = 2 less the speed penalty), so it is below the
+    # full return by more than 1
+    for x in tr.values():
+        e = (x["winner"] == 1) & ~x["collision"]
+        assert e.any() or not (x["winner"] == 1).any()
+        assert (x["hdqn_reward"][e] - x["main_reward"][e] > 1.0).all()
+
+
+@pytest.mark.parametrize("tag", ["L0", "RR"])
+def test_main_loop_statistics(coracle, g, tag):
+    """main.py's own loop (gen_replay.run: the DQN memory run) -- its reward_list and win test."""
+    tr = _trace(g, tag)
+    r, c = oracle_episodes(coracle, tr["a1"], tr["a2"])
+    np.testing.assert_array_equal(r[:, 2], tr["ep_reward"])
+    np.testing.assert_array_equal(c[:, 4].astype(bool), tr["ep_win"])
+
+
+@pytest.mark.parametrize("tag", ["HL0", "HRR"])
+def test_hdqn_loop_statistics(coracle, g, tag):
+    """hdqn.py's own loop (gen_replay.run_hdqn) -- its reward_list and win test."""
+    tr = _trace(g, tag)
+    r, c = oracle_episodes(coracle, tr["a1"], tr["a2"])
+    np.testing.assert_array_equal(r[:, 0], tr["ep_reward"])
+    np.testing.assert_array_equal(c[:, 5].astype(bool), tr["ep_win"])
+
+
+def test_numpy_restatement_episode_statistics(g):
+    """The vectorised NumPy restatement, the four traces as four envs of one batch."""
+    trs = [_trace(g, t) for t in STATS_TAGS]
+    T = min(len(t["a1"]) for t in trs)
+    nb = mn.NumpyMergeBatch(len(trs))
+    a1 = np.stack([t["a1"][:T] for t in trs], 1).astype(np.int64)
+    a2 = np.stack([t["a2"][:T] for t in trs], 1).astype(np.int64)
+    seen = [0] * len(trs)
+    for k in range(T):
+        before_r, before_c = nb.ret_sum.copy(), nb.counts.copy()
+        _, _, done, _ = nb.step(a1[k], a2[k])
+        for i in np.flatnonzero(done):
+            e, t = seen[i], trs[i]
+            assert nb.ret_sum[i, 0] == before_r[i, 0] + t["hdqn_reward"][e]  # sums start at 0: exact per episode
+            seen[i] += 1
+            for col, key in ((4, "main_win"), (5, "hdqn_win")):
+                assert nb.counts[i, col] - before_c[i, col] == int(t[key][e]), (i, e, key)
+    for i, t in enumerate(trs):
+        e = seen[i]
+        np.testing.assert_array_equal(nb.counts[i, :4], [e, t["collision"][:e].sum(), (t["winner"][:e] == 1).sum(),
+                                                         t["length"][:e].sum()])
+        exp = 0.0
+        for v in t["main_reward"][:e]:
+            exp += v
+        assert nb.ret_sum[i, 2] == exp
+
+
+def test_goal_status_rows(g):
+    """hdqn.py's goal_status (:223-236) itself, on fp64 values at and around its thresholds:
+    merging_gym.policy.goal_status (the list form the drop-in callers use) agrees on every row;
+    evaluating the same rows after rounding to fp32 would not (what ABI <= 16's kernel did)."""
+    from merging_gym.policy import goal_status
+
+    dx1, v2, st = g["GS_dx1"], g["GS_v2"], g["GS_status"]
+    got = np.array([goal_status([d, 0, 0, 0, 0, 0, 0, 0, 0, v]) for d, v in zip(dx1, v2)])
+    np.testing.assert_array_equal(got, st)
+    f32 = np.where(dx1.astype(np.float32) < np.float32(-0.5) * v2.astype(np.float32), 0,
+                   np.where(dx1.astype(np.float32) < np.float32(0.5) * v2.astype(np.float32), 1, 2))
+    assert (f32 != st).sum() > 10  # the rows do separate fp64 from fp32 evaluation

@@ -2,7 +2,7 @@
 launched with torch.distributed.run (gloo; both ranks on cuda:0 of the one-GPU test box), each
 step a MergeVecEnv(env_offset=...) shard for 200 Philox steps and gather the statistics. The
 result must equal one unsharded run of the whole batch: per-env statistics and positions bit
-for bit (Philox is keyed by the global env index, envs never interact), the 48-byte-per-rank
+for bit (Philox is keyed by the global env index, envs never interact), the 72-byte-per-rank
 summary to fp64 summation order. The reference has no parallelism (its envs are independent,
 merging_env.py:138-195); this pins the build's own sharding."""
 
@@ -50,9 +50,9 @@ def test_two_rank_shards_equal_unsharded_run(tmp_path):
         full.rollout_random(T, seed, first_step=k)
         k += T
     assert torch.equal(got["counts"], full.counts.cpu())
-    assert torch.equal(got["ret_sum"], full.ret_sum.cpu())
+    assert torch.equal(got["returns"], full.returns.cpu())
     assert torch.equal(got["p1"], full.p1.cpu())
-    exp = summarize(full.ret_sum, full.counts)
+    exp = summarize(full.returns, full.counts)
     assert exp["completed"] > 0 and got["summary"]["completed"] == exp["completed"]
     for key, v in exp.items():
         assert abs(got["summary"][key] - v) <= 1e-12 * max(1.0, abs(v)), key

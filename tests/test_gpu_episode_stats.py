@@ -1,0 +1,171 @@
+"""The statistics the reference's training scripts log, computed on the device (SURVEY.md 8(f)
+row 2), against the reference's own loops; and hdqn.py's goal_status on fp64 values.
+
+* tests/golden/replay_golden.npz holds, per episode of four long trajectories of the reference
+  env, what scripts/main.py:189-227 logs (ep_reward summed only after steps where `env.winner is
+  not 1`, :209-211; a win when `state[8] > state[3]` on the observation the last step acted on,
+  :218-225) and what scripts/hdqn.py:276-346 logs (ep_reward = every reward, :312; the same test
+  on the terminal observation, :320, :342). MergeVecEnv replays the four action sequences as four
+  envs of one batch through mg_step with autoreset; after every finished episode the env's
+  64-byte record (include/merging_hip.h mg_episode_stats) must hold exactly that episode's
+  values. The device keeps main.py's filtered sum as r1_accumulate before the ego-first step
+  (winner stays 1 once set); the oracle and the golden loops filter step by step -- equal bit
+  for bit, so the shortcut is the reference's sum.
+* goal_status (hdqn.py:223-236): mg_goal_status -- the device function mg_rollout_hdqn evaluates --
+  equals the reference's own goal_status on fp64 rows around its thresholds; and the fused h-DQN
+  kernel's intrinsic reward follows the fp64 status on states built so that fp32 evaluation
+  would disagree.
+"""
+
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import merge_oracle as mo
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+REPLAY = os.path.join(ROOT, "tests", "golden", "replay_golden.npz")
+TAGS = ["SU0", "SUU", "SFU", "SSU"]
+
+
+@pytest.fixture(scope="module")
+def g():
+    return np.load(REPLAY)
+
+
+def _trace(g, tag):
+    return {k[len(tag) + 1:]: g[k] for k in g.files if k.startswith(tag + "_")}
+
+
+def test_device_statistics_equal_reference_loops(g):
+    import torch
+
+    from merging_gym import MergeVecEnv
+
+    trs = [_trace(g, t) for t in TAGS]
+    T = min(len(t["a1"]) for t in trs)
+    n = len(trs)
+    env = MergeVecEnv(n, device="cuda:0")
+    a1 = torch.from_numpy(np.stack([t["a1"][:T] for t in trs], 1).astype(np.int8)).cuda()
+    a2 = torch.from_numpy(np.stack([t["a2"][:T] for t in trs], 1).astype(np.int8)).cuda()  # -1 = None
+    seen = [0] * n
+    rec = env._ep_stats  # [n, 8] f64 view of the records
+    for k in range(T):
+        _, _, done, _ = env.step(a1[k], a2[k])
+        d = done.cpu().numpy()
+        if not d.any():
+            continue
+        r = env.returns.cpu().numpy()
+        c = env.counts.cpu().numpy()
+        for i in np.flatnonzero(d):
+            e, t = seen[i], trs[i]
+            assert r[i, 0] == t["hdqn_reward"][e] == t["r1_accumulate"][e], (TAGS[i], e)
+            assert r[i, 1] == t["r2_accumulate"][e], (TAGS[i], e)
+            assert r[i, 2] == t["main_reward"][e], (TAGS[i], e, r[i, 2], t["main_reward"][e])
+            assert c[i].tolist() == [1, int(t["collision"][e]), int(t["winner"][e] == 1), int(t["length"][e]),
+                                     int(t["main_win"][e]), int(t["hdqn_win"][e])], (TAGS[i], e, c[i])
+            seen[i] += 1
+        rec[torch.from_numpy(d).cuda(), :3] = 0.0  # sums; the pending value (column 3) is the next episode's
+        rec[torch.from_numpy(d).cuda(), 4:] = 0.0  # counts
+    assert sum(seen) > 100 and all(s >= 20 for s in seen), seen
+
+
+def test_rollout_and_step_keep_the_same_records():
+    """The T-step kernel (statistics held in registers, counts as 16-bit fields, the pending value
+    carried across launches) leaves the records exactly as T one-step launches do, for several
+    launch lengths over the same stream of episodes."""
+    import torch
+
+    from merging_gym import MergeVecEnv
+
+    n, seed = 5000, 123
+    a = MergeVecEnv(n, device="cuda:0")
+    b = MergeVecEnv(n, device="cuda:0")
+    k = 0
+    for T in (1, 7, 64, 300, 16, 211):
+        for t in range(T):
+            a.step_random(seed, step_idx=k + t)
+        b.rollout_random(T, seed, first_step=k)
+        k += T
+        assert torch.equal(a._ep_stats, b._ep_stats), T
+    c = b.counts.to(torch.int64)
+    assert int(c[:, 0].sum()) > 5000 and int(c[:, 4].sum()) > 0 and int(c[:, 5].sum()) > 0
+    assert bool((b.ret_main != b.ret_sum[:, 0]).any())
+
+
+def test_goal_status_device_rows(g):
+    """mg_goal_status on the golden rows: the reference's goal_status, bit for bit."""
+    import torch
+
+    from merging_gym import _native
+
+    dx1 = torch.from_numpy(g["GS_dx1"]).cuda()
+    v2 = torch.from_numpy(g["GS_v2"]).cuda()
+    out = torch.full(dx1.shape, -1, dtype=torch.int8, device="cuda:0")
+    _native.check(_native.lib.mg_goal_status(dx1.data_ptr(), v2.data_ptr(), out.data_ptr(), dx1.numel(), None),
+                  "mg_goal_status")
+    np.testing.assert_array_equal(out.cpu().numpy(), g["GS_status"])
+
+
+def _rec64_obs(env):
+    """The kernel's own fp64 observation of every env (mg_observe into mg_rec64 records)."""
+    import torch
+
+    nat = env._nat
+    buf = torch.empty((env.num_envs, nat.REC64_DTYPE.itemsize), dtype=torch.uint8, device=env.device)
+    out = nat.Outputs()
+    out.rec64 = ctypes.c_void_p(buf.data_ptr())
+    nat.check(nat.lib.mg_observe(ctypes.byref(env.params), ctypes.byref(env._state), ctypes.byref(out),
+                                 env.num_envs, None), "mg_observe")
+    torch.cuda.synchronize()
+    return buf.cpu().numpy().view(nat.REC64_DTYPE)["obs"].reshape(env.num_envs, 10)
+
+
+def test_hdqn_intrinsic_reward_uses_fp64_goal_status():
+    """States where goal_status differs between fp64 (the reference's Python floats) and fp32:
+    dx1 = x2 - x1 of each env's positions (the kernel's own fp64 value), v2 = 2 |dx1| and its
+    neighbouring doubles, so dx1 sits exactly on, or one ulp inside / outside, +-v2 / 2. One
+    fused h-DQN step: its intrinsic reward (hdqn.py:314) must be 1 exactly where the goal chosen
+    on the next state equals the fp64 status of the state acted on."""
+    import torch
+
+    from merging_gym import MergeVecEnv
+    from merging_gym.policy import NUM_GOALS, QNet
+
+    rng = np.random.default_rng(4)
+    n = 3 * 2048
+    env = MergeVecEnv(n, device="cuda:0")
+    p1 = rng.uniform(300.0, 900.0, n // 3)
+    p2 = p1 + rng.uniform(-25.0, 25.0, n // 3)
+    for name, v in (("p1", np.repeat(p1, 3)), ("p2", np.repeat(p2, 3))):
+        getattr(env, name).copy_(torch.from_numpy(v))
+    o = _rec64_obs(env)
+    dx1 = o[:, 0]
+    base = 2.0 * np.abs(dx1)
+    v2 = base.copy()
+    v2[1::3] = np.nextafter(base[1::3], np.inf)
+    v2[2::3] = np.nextafter(base[2::3], -np.inf)
+    env.v2.copy_(torch.from_numpy(v2))
+    status64 = mo.goal_status64(np.stack([dx1] + [np.zeros(n)] * 8 + [v2], 1))
+    f32 = lambda x: x.astype(np.float32)  # noqa: E731
+    status32 = np.where(f32(dx1) < np.float32(-0.5) * f32(v2), 0, np.where(f32(dx1) < np.float32(0.5) * f32(v2), 1, 2))
+    assert (status64 != status32).sum() > n // 6  # the construction separates the two evaluations
+    nets = np.random.default_rng(9)
+
+    def net(i, out):
+        sd = {}
+        for name, (a, b) in zip(("fc1", "fc2", "out"), [(200, i), (100, 200), (out, 100)]):
+            sd[f"{name}.weight"] = nets.uniform(-b ** -0.5, b ** -0.5, (a, b)).astype(np.float32)
+            sd[f"{name}.bias"] = nets.uniform(-b ** -0.5, b ** -0.5, a).astype(np.float32)
+        return QNet.from_state_dict(sd, device="cuda:0")
+
+    tr = env.rollout_hdqn(1, net(10, NUM_GOALS), net(11, 5), seed=3, first_step=50)
+    r_int = tr["reward"][0].cpu().numpy()
+    g2 = tr["next_goal"][0].cpu().numpy().astype(np.int64)
+    np.testing.assert_array_equal(r_int, (g2 == status64).astype(np.float32))
+    # and some of those rewards are ones fp32 evaluation would have got wrong
+    assert ((g2 == status64) != (g2 == status32)).sum() > 100

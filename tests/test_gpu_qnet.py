@@ -14,6 +14,7 @@ import numpy as np
 import pytest
 
 import merge_oracle as mo
+from choice_check import ChoiceCheck
 from conftest import ROOT
 
 pytestmark = pytest.mark.gpu
@@ -50,11 +51,8 @@ def _obs_samples(coracle, n=8192, steps=240, seed=3):
     return np.concatenate(out)
 
 
-def _near_tie(q, tol=1e-2):
-    """Top-2 Q gap within what one bf16 rounding of a hidden unit can move (summation order
-    differs between the matrix cores and the CPU emulation)."""
-    s = np.sort(q, axis=1)
-    return (s[:, -1] - s[:, -2]) <= tol * np.maximum(1.0, np.abs(s[:, -1]))
+# excused greedy choices (tests/choice_check.py): bounds per net
+MAX_EXCUSED = {"l1": 1e-4, "l3": 1e-4}  # round 3 measured 0 excused of > 10^6 greedy choices
 
 
 @pytest.mark.parametrize("key", ["l1", "l3"])
@@ -70,8 +68,9 @@ def test_qnet_forward_matches_bf16_reference(torch, coracle, nets, key, swap):
     scale = np.maximum(1.0, np.abs(q_bf).max(axis=1, keepdims=True))
     err = np.abs(q - q_bf) / scale
     assert np.median(err) < 1e-5 and err.max() < 1e-2, (np.median(err), err.max())
-    tie = _near_tie(q_bf)
-    assert (q.argmax(1) == q_bf.argmax(1))[~tie].all()
+    cc = ChoiceCheck(f"forward {key} swap={swap}", max_frac=MAX_EXCUSED[key])
+    cc.check(q.argmax(1), q_bf.argmax(1), np.ones(len(q), bool), q_bf)
+    cc.finish()
     # bf16 vs the reference's fp32 Net: the kernel loses nothing beyond bf16 itself
     agree = (q.argmax(1) == q_32.argmax(1)).mean()
     agree_bf16 = (q_bf.argmax(1) == q_32.argmax(1)).mean()
@@ -104,8 +103,9 @@ def test_qnet_forward_hdqn_nets(torch, coracle, in_dim, out_dim):
     scale = np.maximum(1.0, np.abs(q_bf).max(axis=1, keepdims=True))
     err = np.abs(q - q_bf) / scale
     assert np.median(err) < 1e-5 and err.max() < 1e-2, (np.median(err), err.max())
-    tie = _near_tie(q_bf)
-    assert (q.argmax(1) == q_bf.argmax(1))[~tie].all()
+    cc = ChoiceCheck(f"forward hdqn.py net {in_dim}->{out_dim}", max_frac=1e-4)
+    cc.check(q.argmax(1), q_bf.argmax(1), np.ones(len(q), bool), q_bf)
+    cc.finish()
     with pytest.raises(ValueError):  # the input width is the net's
         qnet.forward(torch.zeros((4, in_dim + 1), device="cuda:0"))
 
@@ -139,13 +139,14 @@ def test_rollout_qnet_policy_and_transitions(torch, coracle, nets, opponent, n):
     traj = env.rollout_qnet(T, qnet, seed, opponent=opp, first_step=k0)
     traj = {k: (v.cpu().numpy() if v is not None else None) for k, v in traj.items()}
     thr = greedy_threshold(0.7)
+    cc1 = ChoiceCheck(f"rollout ego l1 ({opponent}, n={n})", max_frac=MAX_EXCUSED["l1"])
+    cc2 = ChoiceCheck(f"rollout opponent {opp_key} ({opponent}, n={n})", max_frac=MAX_EXCUSED[opp_key])
     for t in range(T):
         u = coracle.philox_batch(n, 0, seed, k0 + t)
         q = mo.qnet_reference(nets["l1"], obs_in, bf16=True)
         greedy = u[:, 0].astype(np.uint64) < thr
         exp1 = np.where(greedy, q.argmax(1), (u[:, 1].astype(np.uint64) * 5) >> 32)
-        ok1 = (traj["a1"][t] == exp1) | (greedy & _near_tie(q))
-        assert ok1.all(), (t, np.nonzero(~ok1)[0][:5])
+        cc1.check(traj["a1"][t], exp1, greedy, q, f"step {t}")
         if opponent == "none":
             assert (traj["a2"][t] == -1).all()
         else:
@@ -155,8 +156,7 @@ def test_rollout_qnet_policy_and_transitions(torch, coracle, nets, opponent, n):
             else:
                 q2 = mo.qnet_reference(nets[opp_key], obs_in, bf16=True, swap=True)
                 g2 = u[:, 2].astype(np.uint64) < thr
-                ok2 = (traj["a2"][t] == np.where(g2, q2.argmax(1), rnd2)) | (g2 & _near_tie(q2))
-                assert ok2.all(), t
+                cc2.check(traj["a2"][t], np.where(g2, q2.argmax(1), rnd2), g2, q2, f"step {t}")
         # the transition, with the actions the kernel took
         o_obs, o_rew, o_done, o_coll, _, o_fobs, err = coracle.step(
             envs, traj["a1"][t], traj["a2"][t], autoreset=True, final_obs=True)
@@ -171,6 +171,9 @@ def test_rollout_qnet_policy_and_transitions(torch, coracle, nets, opponent, n):
     np.testing.assert_array_equal(env.p1.cpu().numpy(), envs["pos1"])
     np.testing.assert_array_equal(env.ret2.cpu().numpy(), envs["r2_acc"])
     assert env._step_idx == k0 + T
+    cc1.finish()
+    if opponent in ("self", "other"):
+        cc2.finish()
 
 
 @pytest.mark.parametrize("opponent", ["none", "self"])
@@ -249,15 +252,9 @@ def test_rollout_qnet_full_size(torch, coracle, nets, opponent):
         env.step_random(seed + 1, step_idx=k)
     idx_np = np.sort(np.random.default_rng(3).choice(n, 2048, replace=False))
     idx = torch.from_numpy(idx_np).cuda()
-    envs = coracle.new_envs(len(idx_np))
-    for name, src in (("pos1", env.p1), ("vel1", env.v1), ("pos2", env.p2), ("vel2", env.v2),
-                      ("r1_acc", env.ret1), ("r2_acc", env.ret2)):
-        envs[name] = src[idx].cpu().numpy()
-    envs["steps"] = env.steps[idx].cpu().numpy()
-    envs["winner"] = env.winner[idx].cpu().numpy()
-    envs["time_stamp"] = np.cumsum(np.full(2700, 0.2))[np.maximum(envs["steps"] - 1, 0)] * (envs["steps"] > 0)
+    envs = mo.oracle_envs_from(coracle, env, idx)  # main.py's running ep_reward from the device's pending value
     obs_in = env.observe()[idx].cpu().numpy().copy()
-    ret_sum0, counts0 = env.ret_sum[idx].cpu().numpy(), env.counts[idx].cpu().numpy().astype(np.uint32)
+    ret_sum0, counts0 = env.returns[idx].cpu().numpy(), env.counts[idx].cpu().numpy().astype(np.uint32)
 
     opp_key = "l3" if opponent == "other" else "l1"
     opp = QNet.from_state_dict(nets["l3"], device="cuda:0") if opponent == "other" else opponent
@@ -279,19 +276,19 @@ def test_rollout_qnet_full_size(torch, coracle, nets, opponent):
            for k, v in traj.items()}
     thr = greedy_threshold(0.7)
     stats = (ret_sum0.copy(), counts0.copy())
+    cc1 = ChoiceCheck(f"full-size ego l1 ({opponent})", max_frac=MAX_EXCUSED["l1"])
+    cc2 = ChoiceCheck(f"full-size opponent {opp_key} ({opponent})", max_frac=MAX_EXCUSED[opp_key])
     for t in range(T):
         u = np.stack([coracle.philox_batch(1, int(gi), seed, k0 + t)[0] for gi in idx_np])
         q = mo.qnet_reference(nets["l1"], obs_in, bf16=True)
         greedy = u[:, 0].astype(np.uint64) < thr
         exp1 = np.where(greedy, q.argmax(1), (u[:, 1].astype(np.uint64) * 5) >> 32)
-        ok1 = (sub["a1"][t] == exp1) | (greedy & _near_tie(q))
-        assert ok1.all(), (t, idx_np[~ok1][:5])
+        cc1.check(sub["a1"][t], exp1, greedy, q, f"step {t}")
         rnd2 = (u[:, 3].astype(np.uint64) * 5) >> 32
         if opponent in ("self", "other"):
             q2 = mo.qnet_reference(nets[opp_key], obs_in, bf16=True, swap=True)
             g2 = u[:, 2].astype(np.uint64) < thr
-            ok2 = (sub["a2"][t] == np.where(g2, q2.argmax(1), rnd2)) | (g2 & _near_tie(q2))
-            assert ok2.all(), t
+            cc2.check(sub["a2"][t], np.where(g2, q2.argmax(1), rnd2), g2, q2, f"step {t}")
         o_obs, o_rew, o_done, o_coll, _, o_fobs, err = coracle.step(
             envs, sub["a1"][t], sub["a2"][t], autoreset=True, final_obs=True, stats=stats)
         assert err == 0
@@ -306,4 +303,8 @@ def test_rollout_qnet_full_size(torch, coracle, nets, opponent):
                       ("r1_acc", env.ret1), ("r2_acc", env.ret2)):
         np.testing.assert_array_equal(src[idx].cpu().numpy(), envs[name], err_msg=name)
     np.testing.assert_array_equal(env.counts[idx].cpu().numpy().astype(np.uint32), stats[1])
-    np.testing.assert_array_equal(env.ret_sum[idx].cpu().numpy(), stats[0])
+    np.testing.assert_array_equal(env.returns[idx].cpu().numpy(), stats[0])
+    assert stats[1][:, 0].sum() > counts0[:, 0].sum()  # episodes ended in the window
+    cc1.finish()
+    if opponent in ("self", "other"):
+        cc2.finish()

@@ -2,8 +2,10 @@
 
 tests/golden/reference_golden.npz was written by tests/golden/gen_golden.py, which runs the
 reference (merging_gym/envs/merging_env.py @ /root/reference) with stand-ins for its absent
-third-party deps. Bar: done / collision / winner / value types exact; floats to 1e-9
-(the QP stand-in and the oracle's QP step differ by fp64 rounding only).
+third-party deps (the QP one restates quadprog's qpgen2 statement by statement, on the matrices
+the reference builds). Bar: done / collision / winner / value types exact; the fp64 state
+(positions, speeds, accelerations, returns) and the rewards BIT-EXACT; observations exact for
+the Python oracle (numpy sin / cos, as the reference) and to 1e-9 for the C oracle (glibc's).
 """
 
 import numpy as np
@@ -44,11 +46,12 @@ def test_python_oracle_replays_reference_trace(golden, trace):
         assert coll == bool(g["coll"][k]), (trace, k)
         assert _winner(env.winner) == g["winner"][k], (trace, k)
         assert _types(obs, rew) == g["types"][k], (trace, k)
-        np.testing.assert_allclose(np.asarray(obs, float), g["obs"][k], rtol=0, atol=FTOL)
-        np.testing.assert_allclose(np.asarray(rew, float), g["rew"][k], rtol=0, atol=FTOL)
-        np.testing.assert_allclose([env.state1["pos"], env.state2["pos"]], g["pos"][k], rtol=0, atol=FTOL)
-        np.testing.assert_allclose([env.state1["vel"], env.state2["vel"]], g["vel"][k], rtol=0, atol=FTOL)
-        np.testing.assert_allclose([env.r1_accumulate, env.r2_accumulate], g["racc"][k], rtol=0, atol=FTOL)
+        np.testing.assert_array_equal(np.asarray(obs, float), g["obs"][k], err_msg=str((trace, k)))
+        np.testing.assert_array_equal(np.asarray(rew, float), g["rew"][k], err_msg=str((trace, k)))
+        np.testing.assert_array_equal([env.state1["pos"], env.state2["pos"]], g["pos"][k])
+        np.testing.assert_array_equal([env.state1["vel"], env.state2["vel"]], g["vel"][k])
+        np.testing.assert_array_equal([env.state1["acc"], env.state2["acc"]], g["acc"][k])
+        np.testing.assert_array_equal([env.r1_accumulate, env.r2_accumulate], g["racc"][k])
         assert env.time_stamp == g["time"][k]
 
 
@@ -73,12 +76,12 @@ def _replay_c(coracle, golden, trace):
         assert bool(done) == bool(g["done"][k]), (trace, k)
         assert bool(coll) == bool(g["coll"][k]), (trace, k)
         assert e["winner"] == g["winner"][k], (trace, k)
-        np.testing.assert_allclose(obs, g["obs"][k], rtol=0, atol=FTOL)
-        np.testing.assert_allclose(rew, g["rew"][k], rtol=0, atol=FTOL)
-        np.testing.assert_allclose([e["pos1"], e["pos2"]], g["pos"][k], rtol=0, atol=FTOL)
-        np.testing.assert_allclose([e["vel1"], e["vel2"]], g["vel"][k], rtol=0, atol=FTOL)
-        np.testing.assert_allclose([e["acc1"], e["acc2"]], g["acc"][k], rtol=0, atol=FTOL)
-        np.testing.assert_allclose([e["r1_acc"], e["r2_acc"]], g["racc"][k], rtol=0, atol=FTOL)
+        np.testing.assert_allclose(obs, g["obs"][k], rtol=0, atol=FTOL)  # glibc vs numpy sin / cos
+        np.testing.assert_array_equal(rew, g["rew"][k], err_msg=str((trace, k)))
+        np.testing.assert_array_equal([e["pos1"], e["pos2"]], g["pos"][k], err_msg=str((trace, k)))
+        np.testing.assert_array_equal([e["vel1"], e["vel2"]], g["vel"][k], err_msg=str((trace, k)))
+        np.testing.assert_array_equal([e["acc1"], e["acc2"]], g["acc"][k], err_msg=str((trace, k)))
+        np.testing.assert_array_equal([e["r1_acc"], e["r2_acc"]], g["racc"][k], err_msg=str((trace, k)))
         assert e["time_stamp"] == g["time"][k]
 
 
@@ -133,10 +136,10 @@ def test_one_step_rows(coracle, golden):
     np.testing.assert_array_equal(coll.astype(bool), golden["one_coll"])
     np.testing.assert_array_equal(envs["winner"], golden["one_winner_out"])
     np.testing.assert_allclose(obs, golden["one_obs"], rtol=0, atol=FTOL)
-    np.testing.assert_allclose(rew, golden["one_rew"], rtol=0, atol=FTOL)
-    np.testing.assert_allclose(np.stack([envs["pos1"], envs["pos2"]], 1), golden["one_pos"], rtol=0, atol=FTOL)
-    np.testing.assert_allclose(np.stack([envs["r1_acc"], envs["r2_acc"]], 1), golden["one_racc_out"],
-                               rtol=0, atol=FTOL)
+    np.testing.assert_array_equal(rew, golden["one_rew"])
+    np.testing.assert_array_equal(np.stack([envs["pos1"], envs["pos2"]], 1), golden["one_pos"])
+    np.testing.assert_array_equal(np.stack([envs["vel1"], envs["vel2"]], 1), golden["one_vel"])
+    np.testing.assert_array_equal(np.stack([envs["r1_acc"], envs["r2_acc"]], 1), golden["one_racc_out"])
     assert np.array_equal(envs["time_stamp"], golden["one_time"])
 
 
@@ -147,10 +150,16 @@ def test_reset_obs_and_spaces(golden):
     assert _types(obs, [0.0, 0.0]) == golden["reset_types"]
 
 
-def test_mpc_closed_form(golden):
-    """mpc_1d's first acceleration equals (vt - v0) / t up to fp64 rounding."""
+def test_mpc_closed_form(coracle, golden):
+    """mpc_1d's first acceleration (helper.py:152-191 run by the reference itself, solve_qp being
+    the qpgen2 stand-in) equals the oracles' bit for bit, and (vt - v0) / t up to fp64 rounding
+    (SURVEY 8(a) a2)."""
     acc = np.array([mo.first_accel(x0, v0, x0 + vt * 3.0, vt, 3.0)
                     for x0, v0, vt in zip(golden["mpc_x0"], golden["mpc_v0"], golden["mpc_vt"])])
-    np.testing.assert_allclose(acc, golden["mpc_acc"], rtol=0, atol=1e-12)
+    np.testing.assert_array_equal(acc, golden["mpc_acc"])
+    acc_c = np.array([coracle.mpc_first_accel(x0, v0, x0 + vt * 3.0, vt, 3.0)
+                      for x0, v0, vt in zip(golden["mpc_x0"], golden["mpc_v0"], golden["mpc_vt"])])
+    np.testing.assert_array_equal(acc_c, golden["mpc_acc"])
+    np.testing.assert_array_equal(np.signbit(acc), np.signbit(golden["mpc_acc"]))  # -0.0 where vt == v0
     np.testing.assert_allclose((golden["mpc_vt"] - golden["mpc_v0"]) / 3.0, golden["mpc_acc"],
                                rtol=0, atol=1e-12)

@@ -27,7 +27,7 @@ def test_numpy_batch_equals_c_oracle(coracle):
     nb = mn.NumpyMergeBatch(n)
     envs = coracle.new_envs(n)
     coracle.reset(envs)
-    ret_sum, counts = np.zeros((n, 2)), np.zeros((n, 4), np.uint32)
+    ret_sum, counts = np.zeros((n, 3)), np.zeros((n, 6), np.uint32)
     for k in range(steps):
         a1, a2 = mn.random_actions(nb.gidx, seed, k, opponent_random=k % 3 != 0)
         obs, rew, done, coll = nb.step(a1, a2)
