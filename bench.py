@@ -77,6 +77,11 @@ def parse():
     ap.add_argument("--size2-envs", type=int, default=1 << 22,
                     help="envs of the post-Infinity-Cache leg (N = 1 only); 0 disables it")
     ap.add_argument("--size2-steps", type=int, default=100)
+    ap.add_argument("--size2-when", choices=("first", "last"), default="first",
+                    help="run the 2^22 leg right after the step leg (default) or after every other leg")
+    ap.add_argument("--size2-prealloc", action="store_true",
+                    help="allocate the 2^22 leg's env before the other legs, whenever it runs (A/B of where "
+                         "its memory lands)")
     ap.add_argument("--gather", choices=("summary", "per-env"), default="summary",
                     help="statistics collective: 72-byte totals per rank, or every env's row")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="per CPU-baseline leg")
@@ -185,15 +190,21 @@ def capture_steps(step, first: int, count: int, torch):
     return g
 
 
-def size2_leg(args, torch):
-    """The step kernel past the Infinity Cache: --size2-envs envs (638 MB of state and outputs per
-    step at 2^22 > 256 MiB), burned in to the steady state, --size2-steps launches timed with HIP
-    events on the launch stream."""
+def size2_env(args, torch):
     from merging_gym import MergeVecEnv
 
+    return MergeVecEnv(args.size2_envs, device=torch.device("cuda", torch.cuda.current_device()), autoreset=True,
+                       final_observation=True, episode_stats=True)
+
+
+def size2_leg(args, torch, env=None):
+    """The step kernel past the Infinity Cache: --size2-envs envs (638 MB of state and outputs per
+    step at 2^22 > 256 MiB), burned in to the steady state, --size2-steps launches timed with HIP
+    events on the launch stream. env: one allocated earlier (--size2-prealloc)."""
     E = args.size2_envs
-    env = MergeVecEnv(E, device=torch.device("cuda", torch.cuda.current_device()), autoreset=True,
-                      final_observation=True, episode_stats=True)
+    prealloc = env is not None
+    if env is None:
+        env = size2_env(args, torch)
     k = burn_in(env, args.burn_in, args.seed, 0)
     for _ in range(max(5, args.burn_in_launches)):
         env.step_random(args.seed, step_idx=k)
@@ -213,6 +224,7 @@ def size2_leg(args, torch):
     del env
     torch.cuda.empty_cache()
     return {"envs": E, "steps": args.size2_steps, "burn_in_steps": args.burn_in + max(5, args.burn_in_launches),
+            "when": args.size2_when, "preallocated": prealloc,
             "kernel_ms": kernel_ms,
             "value": E / (kernel_ms * 1e-3), "unit": "env-steps/s", "achieved": achieved, "peak": HBM_PEAK_GBPS,
             "unit_bw": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "frac_8d": frac_8d, "traffic": load_pmc(E),
@@ -689,8 +701,11 @@ def main():
     # after the Q-net and h-DQN legs (gigabytes of trajectory buffers and rings, some freed) the
     # same 2^22-env batch measured 2.2x slower, with no clock effect (tools/throttle_probe.py)
     size2 = None
-    if world == 1 and args.size2_envs > 0 and args.size2_envs != E:
-        size2 = size2_leg(args, torch)
+    do_size2 = world == 1 and args.size2_envs > 0 and args.size2_envs != E
+    env2 = size2_env(args, torch) if do_size2 and args.size2_prealloc else None
+    if do_size2 and args.size2_when == "first":
+        size2 = size2_leg(args, torch, env2)
+        env2 = None
 
     rollout = None
     if args.rollout_steps > 0:
@@ -706,6 +721,10 @@ def main():
     hdqn = None
     if args.qnet_launches > 0 and args.rollout_steps > 0:
         hdqn = hdqn_leg(env, args, world, dist, torch)
+
+    if do_size2 and args.size2_when == "last":
+        size2 = size2_leg(args, torch, env2)
+        env2 = None
 
     total_env_steps = world * E * args.steps
     value = total_env_steps / elapsed

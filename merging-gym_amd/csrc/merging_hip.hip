@@ -349,12 +349,22 @@ __device__ __forceinline__ void move_car(const mg_params& P, double acc, double&
 __device__ __forceinline__ void score_step(const mg_params& P, Env& e, double x1, double y1,
                                            double x2, double y2, StepOut& r, bool frozen = false);
 
+// main.py:225's win test, state[8] > state[3] = END_POINT - p2 > END_POINT - p1, on the state a step
+// acts on, evaluated before the move: left to the compiler it sinks into the rare finishing branch
+// and keeps the pre-step positions live across the step (66 instead of 61 VGPRs in the step
+// kernel: 7 waves per SIMD, a third round of blocks at 2^20 envs).
+__device__ __forceinline__ bool win_test_early(const mg_params& P, const Env& e) {
+  int w = (P.end_point - e.p2) > (P.end_point - e.p1) ? 1 : 0;
+  asm volatile("" : "+v"(w));
+  return w != 0;
+}
+
 // MergeEnv.step (merging_env.py:138-195) for one env held in registers. CHECKED = false: the
 // caller guarantees a1 in 0..4 and a2 in -1..4 (device-drawn actions), so the KeyError path and
 // its zeroed outputs are not compiled in.
 template <bool CHECKED = true>
 __device__ __forceinline__ void env_step(const mg_params& P, Env& e, int a1, int a2, StepOut& r) {
-  r.win_pre = (P.end_point - e.p2) > (P.end_point - e.p1);  // main.py:225 on the state acted on
+  r.win_pre = win_test_early(P, e);
   r.first1 = false;
   r.dx1 = 0.0;
   env_clock(P, e);
@@ -401,7 +411,7 @@ __device__ __forceinline__ void env_step_lockstep(const mg_params& P, Env (&e)[N
     bad[j] = bad1 || bad2;
     r[j].bad = (bad1 ? 1 : 0) | (bad2 ? 2 : 0);
     r[j].r1_int = r[j].r2_int = false;
-    r[j].win_pre = (P.end_point - e[j].p2) > (P.end_point - e[j].p1);
+    r[j].win_pre = win_test_early(P, e[j]);
     r[j].first1 = false;
     env_clock(P, e[j]);
     const double acc1 = mpc_acc(P, bad1 ? 0 : a1[j], e[j].v1);

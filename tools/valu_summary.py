@@ -19,10 +19,21 @@ STEPS = {"step_kernel": 1, "rollout_kernel": 16, "qnet_rollout": 16, "hdqn_rollo
 
 
 def kernel_key(name):
+    """qnet_rollout / hdqn_rollout for the opponent-mode-0 instances (the names earlier rounds
+    used), qnet_rollout<2> etc. for the others; step_kernel / rollout_kernel."""
+    import re
+
     for k in ("hdqn_rollout", "qnet_rollout", "step_kernel", "rollout_kernel"):  # most specific first
         if k in name:
+            m = re.search(k + r"\w*<(\d)>", name)
+            if k in ("hdqn_rollout", "qnet_rollout") and m and m.group(1) != "0":
+                return f"{k}<{m.group(1)}>"
             return k
     return None
+
+
+def base_key(k):
+    return k.split("<")[0]
 
 
 def main():
@@ -42,8 +53,8 @@ def main():
     out = {}
     for k, cs in vals.items():
         mean = {c: sum(v) / len(v) for c, v in cs.items()}
-        wave_steps = ENVS / 64 * STEPS[k]
-        row = {"per_dispatch": mean, "env_steps_per_dispatch": ENVS * STEPS[k]}
+        wave_steps = ENVS / 64 * STEPS[base_key(k)]
+        row = {"per_dispatch": mean, "env_steps_per_dispatch": ENVS * STEPS[base_key(k)]}
         for c in ("VALUBusy", "SALUBusy"):
             if c in mean:
                 row[c] = mean[c]
@@ -52,6 +63,9 @@ def main():
         f64 = sum(per_ws.get(c, 0.0) for c in ("valu_fma_f64", "valu_mul_f64", "valu_add_f64", "valu_trans_f64"))
         if "valu" in per_ws:
             row["fp64_share_of_valu"] = f64 / per_ws["valu"]
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in mean and "GRBM_GUI_ACTIVE" in mean and "CU_NUM" in mean:
+            # MFMA-pipe busy cycles of every SIMD over the kernel's GPU-active cycles x SIMDs
+            row["mfma_busy_frac"] = mean["SQ_VALU_MFMA_BUSY_CYCLES"] / (mean["GRBM_GUI_ACTIVE"] * mean["CU_NUM"] * 4)
         if "SQ_WAVE_CYCLES" in mean:
             row["wave_time_split"] = {"wait_any": mean.get("SQ_WAIT_ANY", 0) / mean["SQ_WAVE_CYCLES"],
                                       "wait_inst_any": mean.get("SQ_WAIT_INST_ANY", 0) / mean["SQ_WAVE_CYCLES"],
