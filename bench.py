@@ -166,6 +166,11 @@ def load_valu():
                   "valu_insts_per_lane_step": ins.get("valu", 0.0),  # wave instructions per 64 env-steps
                   "fp64_share_of_valu": v.get("fp64_share_of_valu"),
                   "source": "profiles/valu_busy.json (rocprofv3 --pmc VALUBusy + SQ_INSTS_VALU*, 2^20 envs)"}
+        if "mfma_busy_frac" in v:  # rocprofv3's MfmaUtil: matrix-pipe busy cycles / (GPU cycles x SIMDs)
+            out[k]["mfma_busy_frac"] = v["mfma_busy_frac"]
+            out[k]["mfma_bf16_flops_per_env_step"] = v.get("mfma_bf16_flops_per_env_step")
+            out[k]["lds_bank_conflict_frac"] = v.get("lds_bank_conflict_frac")
+            out[k]["source"] += " + MfmaUtil, SQ_INSTS_VALU_MFMA_MOPS_BF16, SQ_LDS_BANK_CONFLICT"
     return out
 
 
@@ -210,22 +215,48 @@ def size2_leg(args, torch, env=None):
         env.step_random(args.seed, step_idx=k)
         k += 1
     env.clear_statistics()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # One event pair per window of 20 launches, averaged over all of them, with the host's enqueue
+    # time of each window beside it. Placed after the Q-net / h-DQN legs, the first timed window
+    # once measured 453 us per launch and the next four 107-114 (r03e): a one-time stall of ~7 ms
+    # at the first window, not a slow placement (the same arena is 107 us from the second window
+    # on, and eight arenas allocated side by side all time 101-112 us, tools/placement_probe.py).
+    # Hence, as in the main timed loop: the collector off and one rehearsal window first.
+    win = 20
+    nwin = max(1, args.size2_steps // win)
+    gc.disable()
     torch.cuda.synchronize()
-    ev0.record()
-    for j in range(args.size2_steps):
+    r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    r0.record()
+    for j in range(win):
         env.step_random(args.seed, step_idx=k + j)
-    ev1.record()
+    r1.record()
     torch.cuda.synchronize()
-    kernel_ms = ev0.elapsed_time(ev1) / args.size2_steps
+    rehearsal_us = round(r0.elapsed_time(r1) / win * 1e3, 1)
+    k += win
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(nwin + 1)]
+    host = []
+    torch.cuda.synchronize()
+    evs[0].record()
+    for w in range(nwin):
+        h0 = time.perf_counter()
+        for j in range(win):
+            env.step_random(args.seed, step_idx=k + w * win + j)
+        evs[w + 1].record()
+        host.append(round((time.perf_counter() - h0) * 1e3, 3))
+    torch.cuda.synchronize()
+    gc.enable()
+    win_us = [round(evs[w].elapsed_time(evs[w + 1]) / win * 1e3, 1) for w in range(nwin)]
+    kernel_ms = evs[0].elapsed_time(evs[-1]) / (nwin * win)
+    arena = env._arena.data_ptr() if env._arena is not None else env.p1.data_ptr()
     achieved = BYTES_PER_ENV_STEP * E / (kernel_ms * 1e-3) / 1e9
     frac_8d = BYTES_PER_ENV_STEP_8D * E / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS
     completed = int(env.counts[:, 0].sum())
     del env
     torch.cuda.empty_cache()
-    return {"envs": E, "steps": args.size2_steps, "burn_in_steps": args.burn_in + max(5, args.burn_in_launches),
+    return {"envs": E, "steps": nwin * win, "burn_in_steps": args.burn_in + max(5, args.burn_in_launches),
             "when": args.size2_when, "preallocated": prealloc,
-            "kernel_ms": kernel_ms,
+            "kernel_ms": kernel_ms, "window_us": win_us, "window_host_enqueue_ms": host,
+            "rehearsal_window_us": rehearsal_us, "arena_addr": hex(arena),
             "value": E / (kernel_ms * 1e-3), "unit": "env-steps/s", "achieved": achieved, "peak": HBM_PEAK_GBPS,
             "unit_bw": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "frac_8d": frac_8d, "traffic": load_pmc(E),
             "episodes_completed": completed}
@@ -781,9 +812,14 @@ def main():
         if hdqn is not None:
             if "hdqn_rollout" in valu:
                 hdqn["valu"] = valu["hdqn_rollout"]
+            for key, sub in (("hdqn_rollout<2>", "selfplay"), ("hdqn_rollout<3>", "other_checkpoint")):
+                if key in valu and isinstance(hdqn.get(sub), dict):
+                    hdqn[sub]["valu"] = valu[key]
             line["hdqn_policy"] = hdqn
-        if qnet is not None and "qnet_rollout" in valu:
-            qnet[0]["valu"] = valu["qnet_rollout"]
+        if qnet is not None:  # opponents none / self / other: kernel instances 0 / 2 / 3
+            for leg, key in zip(qnet, ("qnet_rollout", "qnet_rollout<2>", "qnet_rollout<3>")):
+                if key in valu:
+                    leg["valu"] = valu[key]
         if size2 is not None:
             line["size_2p22"] = size2
         if world == 1 and not args.no_cpu_baseline:

@@ -1325,6 +1325,130 @@ __device__ __forceinline__ void qnet_mlp_swp(const uint8_t* net, bf16x8 xb0, bf1
   qnet_gather_q(acc3_0, acc3_1, h, q);
 }
 
+// qnet_mlp_swp for a packed net in GLOBAL memory (the h-DQN kernel's opponent from another
+// checkpoint: four nets exceed one CU's LDS, so the opponent's two are read from L2). The same
+// MFMA / ReLU schedule, but its 66 weight fragments come through a buffer resource with a
+// prefetch ring kQGlobalAhead fragments deep across the whole forward: one lane offset per row
+// pattern (five VGPRs) and the per-fragment constant in an SGPR, instead of a 64-bit address per
+// fragment and one fragment ahead (which left each MFMA pair waiting on an L2 round trip).
+// Fragments in the order the MFMAs consume them: W1(0); for tile mt = 0..5 W1(mt + 1) then
+// W2(mt, j = 0..7); the last tile's W2(6, 0 / 2 / 4 / 6); then W3(0..6).
+constexpr int kQGlobalAhead = 3;
+constexpr int kQFrags = 66;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t qnet_rsrc(const uint8_t* net) {
+  // gfx9 buffer descriptor word 3 (raw untyped dword access), num_records = the packed net
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(net), static_cast<short>(0), kQNetBytes,
+                                           0x00020000);
+}
+
+__device__ __forceinline__ bf16x8 qnet_frag_global(__amdgpu_buffer_rsrc_t rs, int s, int r, int h) {
+  int lane_b, const_b;
+  auto w1 = [&](int mt) {
+    if (32 * mt + 31 < kQR1) {
+      lane_b = (r * kQS1 + 8 * h) * 2;
+      const_b = 32 * mt * kQS1 * 2;
+    } else {
+      lane_b = (qrow1(32 * mt + r) * kQS1 + 8 * h) * 2;
+      const_b = 0;
+    }
+  };
+  auto w2 = [&](int mt, int j) {
+    const int m2 = j >> 1, kb = 2 * mt + (j & 1);
+    if (32 * m2 + 31 < kQR2) {
+      lane_b = (r * kQS2 + 8 * h) * 2;
+      const_b = kQOffW2 + 32 * m2 * kQS2 * 2 + 32 * kb;
+    } else {
+      lane_b = (qrow2(32 * m2 + r) * kQS2 + 8 * h) * 2;
+      const_b = kQOffW2 + 32 * kb;
+    }
+  };
+  if (s == 0) {
+    w1(0);
+  } else if (s <= 54) {
+    const int u = s - 1, mt = u / 9, v = u % 9;
+    if (v == 0)
+      w1(mt + 1);
+    else
+      w2(mt, v - 1);
+  } else if (s <= 58) {
+    w2(kQH1 / 32 - 1, 2 * (s - 55));
+  } else {
+    lane_b = (qrow3(r) * kQS3 + 8 * h) * 2;
+    const_b = kQOffW3 + 32 * (s - 59);
+  }
+  return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, lane_b, const_b, 0));
+}
+
+__device__ __forceinline__ void qnet_mlp_global(__amdgpu_buffer_rsrc_t rs, bf16x8 xb0, bf16x8 xb1, float (&q)[8]) {
+  static_assert(kQH1 / 32 == 7 && (kQH2Real + 15) / 16 == 7 && 1 + 6 * 9 + 4 + 7 == kQFrags,
+                "qnet_frag_global's consumption order assumes 7 hidden-1 tiles and 7 layer-3 k-blocks");
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  bf16x8 ring[kQGlobalAhead];
+#pragma unroll
+  for (int s = 0; s < kQGlobalAhead; ++s) ring[s] = qnet_frag_global(rs, s, r, h);
+  auto take = [&](int s) __attribute__((always_inline)) {
+    const bf16x8 f = ring[s % kQGlobalAhead];
+    if (s + kQGlobalAhead < kQFrags) ring[s % kQGlobalAhead] = qnet_frag_global(rs, s + kQGlobalAhead, r, h);
+    return f;
+  };
+  f32x16 acc2a[4] = {}, acc2b[4] = {};
+  const f32x16 zero = {};
+  f32x16 c0, c1;
+  {
+    const bf16x8 a1 = take(0);
+    c0 = mfma32(a1, xb0, zero);
+    c1 = mfma32(a1, xb1, zero);
+  }
+  bf16x8 hb[4] = {relu_bf16(c0, 0), relu_bf16(c0, 1), relu_bf16(c1, 0), relu_bf16(c1, 1)};
+  auto tile_step = [&](int mt, bool more, int nk) __attribute__((always_inline)) {
+    const int s0 = 1 + 9 * mt;  // this tile's first fragment (W1(mt + 1) when more)
+    if (more) {
+      const bf16x8 a1 = take(s0);
+      c0 = mfma32(a1, xb0, zero);
+      c1 = mfma32(a1, xb1, zero);
+    }
+    uint32_t nx[16];
+    int s = more ? s0 + 1 : s0;  // the last tile starts at fragment 55 = 1 + 9 * 6
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int m2 = j >> 1, sk = j & 1;
+      if (sk >= nk) continue;
+      const bf16x8 a2 = take(s++);
+      __builtin_amdgcn_sched_barrier(0);
+      acc2a[m2] = mfma32(a2, hb[sk], acc2a[m2]);
+      acc2b[m2] = mfma32(a2, hb[2 + sk], acc2b[m2]);
+      if (more) {
+#pragma unroll
+        for (int pp = 2 * j; pp < 2 * j + 2; ++pp) {
+          const int f = pp >> 2, b = 8 * (f & 1) + 2 * (pp & 3);
+          const f32x16& c = f < 2 ? c0 : c1;
+          nx[pp] = relu_pair(c[b], c[b + 1]);
+        }
+      }
+    }
+    if (more) {
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+        hb[f] = __builtin_bit_cast(bf16x8, u32x4{nx[4 * f], nx[4 * f + 1], nx[4 * f + 2], nx[4 * f + 3]});
+    }
+  };
+  constexpr int kLast = kQH1 / 32 - 1;
+#pragma unroll
+  for (int mt = 0; mt < kLast; ++mt) tile_step(mt, true, 2);
+  tile_step(kLast, false, 1);
+  f32x16 acc3_0 = {}, acc3_1 = {};
+  constexpr int kK3 = (kQH2Real + 15) / 16;
+#pragma unroll
+  for (int kb = 0; kb < kK3; ++kb) {
+    const int m2 = kb >> 1, sk = kb & 1;
+    const bf16x8 a3 = take(59 + kb);
+    acc3_0 = mfma32(a3, relu_bf16(acc2a[m2], sk), acc3_0);
+    acc3_1 = mfma32(a3, relu_bf16(acc2b[m2], sk), acc3_1);
+  }
+  qnet_gather_q(acc3_0, acc3_1, h, q);
+}
+
 __device__ __forceinline__ int argmax_first(const float (&q)[8], int out_dim) {
   int best = 0;
   float v = q[0];
@@ -1744,7 +1868,7 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
           const bf16x8 x0 = qnet_input(tile + (row0 + r) * kObs, true, h);
           const bf16x8 x1 = qnet_input(tile + (row0 + 32 + r) * kObs, true, h);
           if constexpr (OPP == 3)
-            qnet_mlp_swp(R.meta_op, x0, x1, q);  // the opponent's own Goal_DQN (:267)
+            qnet_mlp_global(qnet_rsrc(R.meta_op), x0, x1, q);  // the opponent's own Goal_DQN (:267)
           else
             qnet_mlp_swp(lds_meta, x0, x1, q);
           gop_star = argmax_first(q, R.num_goals);
@@ -1769,7 +1893,7 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
           const bf16x8 x0 = qnet_input_goal(tile + (row0 + r) * kObs, b_gop[row0 + r], h, true);
           const bf16x8 x1 = qnet_input_goal(tile + (row0 + 32 + r) * kObs, b_gop[row0 + 32 + r], h, true);
           if constexpr (OPP == 3)
-            qnet_mlp_swp(R.lower_op, x0, x1, qo);  // the opponent's own HDQN (:268)
+            qnet_mlp_global(qnet_rsrc(R.lower_op), x0, x1, qo);  // the opponent's own HDQN (:268)
           else
             qnet_mlp_swp(lds_lower, x0, x1, qo);
           b_aop[j] = static_cast<uint8_t>(argmax_first(qo, MG_NUM_ACTIONS));

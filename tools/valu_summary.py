@@ -63,9 +63,14 @@ def main():
         f64 = sum(per_ws.get(c, 0.0) for c in ("valu_fma_f64", "valu_mul_f64", "valu_add_f64", "valu_trans_f64"))
         if "valu" in per_ws:
             row["fp64_share_of_valu"] = f64 / per_ws["valu"]
-        if "SQ_VALU_MFMA_BUSY_CYCLES" in mean and "GRBM_GUI_ACTIVE" in mean and "CU_NUM" in mean:
-            # MFMA-pipe busy cycles of every SIMD over the kernel's GPU-active cycles x SIMDs
-            row["mfma_busy_frac"] = mean["SQ_VALU_MFMA_BUSY_CYCLES"] / (mean["GRBM_GUI_ACTIVE"] * mean["CU_NUM"] * 4)
+        if "MfmaUtil" in mean:
+            # rocprofv3's derived MfmaUtil: MFMA-pipe busy cycles summed over the SIMDs over
+            # (GPU-active cycles x SIMD count), in percent
+            row["mfma_busy_frac"] = mean["MfmaUtil"] / 100.0
+        if "SQ_INSTS_VALU_MFMA_MOPS_BF16" in mean:
+            row["mfma_bf16_flops_per_env_step"] = mean["SQ_INSTS_VALU_MFMA_MOPS_BF16"] * 512 / (wave_steps * 64)
+        if "SQ_LDS_BANK_CONFLICT" in mean and "SQ_LDS_IDX_ACTIVE" in mean and mean["SQ_LDS_IDX_ACTIVE"]:
+            row["lds_bank_conflict_frac"] = mean["SQ_LDS_BANK_CONFLICT"] / mean["SQ_LDS_IDX_ACTIVE"]
         if "SQ_WAVE_CYCLES" in mean:
             row["wave_time_split"] = {"wait_any": mean.get("SQ_WAIT_ANY", 0) / mean["SQ_WAVE_CYCLES"],
                                       "wait_inst_any": mean.get("SQ_WAIT_INST_ANY", 0) / mean["SQ_WAVE_CYCLES"],
