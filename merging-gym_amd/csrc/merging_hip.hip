@@ -1150,16 +1150,23 @@ __device__ __forceinline__ void qnet_to_lds(const uint8_t* net, uint8_t* lds) {
 }
 
 // Rows 0-3 of the env of lane 32t + r sit in registers 0-3 of lane half 0 of column tile t,
-// rows 4-7 in lane half 1: swap halves across the wave.
+// rows 4-7 in lane half 1. One v_permlane32_swap per register pair (gfx950) exchanges tile 0's
+// upper half with tile 1's lower half: afterwards register j of the first operand holds row j and
+// of the second row 4 + j of the lane's own env, in both lane halves (the ds_bpermute round trip
+// plus selects it replaces sat between the forward's last MFMA and the argmax).
 __device__ __forceinline__ void qnet_gather_q(const f32x16& acc3_0, const f32x16& acc3_1, int h,
                                               float (&q)[8]) {
+  (void)h;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const float own = h ? acc3_1[j] : acc3_0[j];
-    const float send = h ? acc3_0[j] : acc3_1[j];
-    const float got = __shfl_xor(send, 32);
-    q[j] = h ? got : own;
-    q[4 + j] = h ? own : got;
+    // operands into locals first and the result read as one 64-bit value: hipcc (ROCm 7.2)
+    // passed element 0 for every j when the builtin's arguments were subscripts, and returned
+    // the first result for both subscripts of its 2-vector
+    const float a = acc3_0[j], b = acc3_1[j];
+    const uint32_t x = __builtin_bit_cast(uint32_t, a), y = __builtin_bit_cast(uint32_t, b);
+    const uint64_t sw = __builtin_bit_cast(uint64_t, __builtin_amdgcn_permlane32_swap(x, y, false, false));
+    q[j] = __builtin_bit_cast(float, static_cast<uint32_t>(sw));
+    q[4 + j] = __builtin_bit_cast(float, static_cast<uint32_t>(sw >> 32));
   }
 }
 
@@ -1307,21 +1314,39 @@ __device__ __forceinline__ void qnet_mlp_swp(const uint8_t* net, bf16x8 xb0, bf1
                 "only the last hidden tile's second k-block is padding");
 #pragma unroll
   for (int mt = 0; mt < kLast; ++mt) tile_step(mt, true, 2);
-  tile_step(kLast, false, 1);
-  // layer 3 over the k-blocks holding real units (96..111 carries units 100..102 = 1.0 too;
-  // 112..127 is padding), its W3 fragments one ahead
+  // The last hidden tile (its k-block 0 only) interleaved with layer 3, over the k-blocks holding
+  // real units (96..111 carries units 100..102 = 1.0 too; 112..127 is padding). acc2a/b[m2] are
+  // final once the tile's pair m2 has issued, so layer 3's k-blocks 2 m2 and 2 m2 + 1 -- their
+  // ReLU and MFMAs, in the same order as before -- follow pair m2 + 1 instead of the whole tile:
+  // the tile's MFMAs had no vector work beside them and layer 3 is mostly vector work. W2 and W3
+  // fragments one ahead.
   f32x16 acc3_0 = {}, acc3_1 = {};
   auto w3frag = [&](int kb) { return *reinterpret_cast<const bf16x8*>(W3 + qrow3(r) * kQS3 + 16 * kb + 8 * h); };
   constexpr int kK3 = (kQH2Real + 15) / 16;
+  static_assert(kK3 == 7 && kQH2 / 32 == 4, "layer 3 k-blocks 2 m2, 2 m2 + 1 follow layer-2 row tile m2");
   bf16x8 a3n = w3frag(0);
+  auto layer3 = [&](int m2) __attribute__((always_inline)) {
 #pragma unroll
-  for (int kb = 0; kb < kK3; ++kb) {
-    const int m2 = kb >> 1, sk = kb & 1;
-    const bf16x8 a3 = a3n;
-    if (kb + 1 < kK3) a3n = w3frag(kb + 1);
-    acc3_0 = mfma32(a3, relu_bf16(acc2a[m2], sk), acc3_0);
-    acc3_1 = mfma32(a3, relu_bf16(acc2b[m2], sk), acc3_1);
+    for (int sk = 0; sk < 2; ++sk) {
+      const int kb = 2 * m2 + sk;
+      if (kb >= kK3) continue;
+      const bf16x8 a3 = a3n;
+      if (kb + 1 < kK3) a3n = w3frag(kb + 1);
+      acc3_0 = mfma32(a3, relu_bf16(acc2a[m2], sk), acc3_0);
+      acc3_1 = mfma32(a3, relu_bf16(acc2b[m2], sk), acc3_1);
+    }
+  };
+  bf16x8 a2n = w2frag(kLast, 0);
+#pragma unroll
+  for (int m2 = 0; m2 < kQH2 / 32; ++m2) {
+    const bf16x8 a2 = a2n;
+    if (m2 + 1 < kQH2 / 32) a2n = w2frag(kLast, 2 * (m2 + 1));
+    __builtin_amdgcn_sched_barrier(0);
+    acc2a[m2] = mfma32(a2, hb[0], acc2a[m2]);
+    acc2b[m2] = mfma32(a2, hb[2], acc2b[m2]);
+    if (m2 > 0) layer3(m2 - 1);
   }
+  layer3(kQH2 / 32 - 1);
   qnet_gather_q(acc3_0, acc3_1, h, q);
 }
 
@@ -1371,11 +1396,18 @@ __device__ __forceinline__ bf16x8 qnet_frag_global(__amdgpu_buffer_rsrc_t rs, in
       w1(mt + 1);
     else
       w2(mt, v - 1);
-  } else if (s <= 58) {
-    w2(kQH1 / 32 - 1, 2 * (s - 55));
   } else {
-    lane_b = (qrow3(r) * kQS3 + 8 * h) * 2;
-    const_b = kQOffW3 + 32 * (s - 59);
+    // the last tile's pairs interleaved with layer 3 (qnet_mlp_swp's tail): W2(6, 0), W2(6, 2),
+    // W3(0), W3(1), W2(6, 4), W3(2), W3(3), W2(6, 6), W3(4), W3(5), W3(6)
+    const int u = s - 55;
+    const int pair = u == 0 ? 0 : u == 1 ? 1 : u == 4 ? 2 : u == 7 ? 3 : -1;
+    if (pair >= 0) {
+      w2(kQH1 / 32 - 1, 2 * pair);
+    } else {
+      const int kb = u == 2 ? 0 : u == 3 ? 1 : u == 5 ? 2 : u == 6 ? 3 : u - 4;
+      lane_b = (qrow3(r) * kQS3 + 8 * h) * 2;
+      const_b = kQOffW3 + 32 * kb;
+    }
   }
   return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, lane_b, const_b, 0));
 }
@@ -1436,16 +1468,28 @@ __device__ __forceinline__ void qnet_mlp_global(__amdgpu_buffer_rsrc_t rs, bf16x
   constexpr int kLast = kQH1 / 32 - 1;
 #pragma unroll
   for (int mt = 0; mt < kLast; ++mt) tile_step(mt, true, 2);
-  tile_step(kLast, false, 1);
+  // the last tile interleaved with layer 3, as in qnet_mlp_swp (fragments 55..65)
   f32x16 acc3_0 = {}, acc3_1 = {};
   constexpr int kK3 = (kQH2Real + 15) / 16;
+  int s = 55;
+  auto layer3 = [&](int m2) __attribute__((always_inline)) {
 #pragma unroll
-  for (int kb = 0; kb < kK3; ++kb) {
-    const int m2 = kb >> 1, sk = kb & 1;
-    const bf16x8 a3 = take(59 + kb);
-    acc3_0 = mfma32(a3, relu_bf16(acc2a[m2], sk), acc3_0);
-    acc3_1 = mfma32(a3, relu_bf16(acc2b[m2], sk), acc3_1);
+    for (int sk = 0; sk < 2; ++sk) {
+      if (2 * m2 + sk >= kK3) continue;
+      const bf16x8 a3 = take(s++);
+      acc3_0 = mfma32(a3, relu_bf16(acc2a[m2], sk), acc3_0);
+      acc3_1 = mfma32(a3, relu_bf16(acc2b[m2], sk), acc3_1);
+    }
+  };
+#pragma unroll
+  for (int m2 = 0; m2 < kQH2 / 32; ++m2) {
+    const bf16x8 a2 = take(s++);
+    __builtin_amdgcn_sched_barrier(0);
+    acc2a[m2] = mfma32(a2, hb[0], acc2a[m2]);
+    acc2b[m2] = mfma32(a2, hb[2], acc2b[m2]);
+    if (m2 > 0) layer3(m2 - 1);
   }
+  layer3(kQH2 / 32 - 1);
   qnet_gather_q(acc3_0, acc3_1, h, q);
 }
 
