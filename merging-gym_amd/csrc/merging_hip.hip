@@ -1367,8 +1367,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t qnet_rsrc(const uint8_t* net) 
                                            0x00020000);
 }
 
-__device__ __forceinline__ bf16x8 qnet_frag_global(__amdgpu_buffer_rsrc_t rs, int s, int r, int h) {
-  int lane_b, const_b;
+// byte offset of fragment s (consumption order) for lane (r, h): a lane part and a constant part
+__device__ __forceinline__ void qnet_frag_offset(int s, int r, int h, int& lane_b, int& const_b) {
   auto w1 = [&](int mt) {
     if (32 * mt + 31 < kQR1) {
       lane_b = (r * kQS1 + 8 * h) * 2;
@@ -1409,19 +1409,34 @@ __device__ __forceinline__ bf16x8 qnet_frag_global(__amdgpu_buffer_rsrc_t rs, in
       const_b = kQOffW3 + 32 * kb;
     }
   }
-  return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, lane_b, const_b, 0));
 }
 
-__device__ __forceinline__ void qnet_mlp_global(__amdgpu_buffer_rsrc_t rs, bf16x8 xb0, bf16x8 xb1, float (&q)[8]) {
+// where qnet_mlp_ring's fragments come from: a buffer resource over a net in global memory, the
+// per-fragment constant in soffset. (The same ring over the LDS nets, 2 to 4 deep, measured
+// within +-1 % of qnet_mlp_swp's one-ahead loads on every Q-net leg, r03: not used there.)
+struct QSrcGlobal {
+  __amdgpu_buffer_rsrc_t rs;
+  __device__ __forceinline__ bf16x8 operator()(int lane_b, int const_b) const {
+    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, lane_b, const_b, 0));
+  }
+};
+
+template <int D, class Src>
+__device__ __forceinline__ void qnet_mlp_ring(const Src& src, bf16x8 xb0, bf16x8 xb1, float (&q)[8]) {
   static_assert(kQH1 / 32 == 7 && (kQH2Real + 15) / 16 == 7 && 1 + 6 * 9 + 4 + 7 == kQFrags,
-                "qnet_frag_global's consumption order assumes 7 hidden-1 tiles and 7 layer-3 k-blocks");
+                "qnet_frag_offset's consumption order assumes 7 hidden-1 tiles and 7 layer-3 k-blocks");
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-  bf16x8 ring[kQGlobalAhead];
+  auto fetch = [&](int s) __attribute__((always_inline)) {
+    int lane_b, const_b;
+    qnet_frag_offset(s, r, h, lane_b, const_b);
+    return src(lane_b, const_b);
+  };
+  bf16x8 ring[D];
 #pragma unroll
-  for (int s = 0; s < kQGlobalAhead; ++s) ring[s] = qnet_frag_global(rs, s, r, h);
+  for (int s = 0; s < D; ++s) ring[s] = fetch(s);
   auto take = [&](int s) __attribute__((always_inline)) {
-    const bf16x8 f = ring[s % kQGlobalAhead];
-    if (s + kQGlobalAhead < kQFrags) ring[s % kQGlobalAhead] = qnet_frag_global(rs, s + kQGlobalAhead, r, h);
+    const bf16x8 f = ring[s % D];
+    if (s + D < kQFrags) ring[s % D] = fetch(s + D);
     return f;
   };
   f32x16 acc2a[4] = {}, acc2b[4] = {};
@@ -1912,7 +1927,7 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
           const bf16x8 x0 = qnet_input(tile + (row0 + r) * kObs, true, h);
           const bf16x8 x1 = qnet_input(tile + (row0 + 32 + r) * kObs, true, h);
           if constexpr (OPP == 3)
-            qnet_mlp_global(qnet_rsrc(R.meta_op), x0, x1, q);  // the opponent's own Goal_DQN (:267)
+            qnet_mlp_ring<kQGlobalAhead>(QSrcGlobal{qnet_rsrc(R.meta_op)}, x0, x1, q);  // the opponent's own Goal_DQN (:267)
           else
             qnet_mlp_swp(lds_meta, x0, x1, q);
           gop_star = argmax_first(q, R.num_goals);
@@ -1937,7 +1952,7 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
           const bf16x8 x0 = qnet_input_goal(tile + (row0 + r) * kObs, b_gop[row0 + r], h, true);
           const bf16x8 x1 = qnet_input_goal(tile + (row0 + 32 + r) * kObs, b_gop[row0 + 32 + r], h, true);
           if constexpr (OPP == 3)
-            qnet_mlp_global(qnet_rsrc(R.lower_op), x0, x1, qo);  // the opponent's own HDQN (:268)
+            qnet_mlp_ring<kQGlobalAhead>(QSrcGlobal{qnet_rsrc(R.lower_op)}, x0, x1, qo);  // the opponent's own HDQN (:268)
           else
             qnet_mlp_swp(lds_lower, x0, x1, qo);
           b_aop[j] = static_cast<uint8_t>(argmax_first(qo, MG_NUM_ACTIONS));
