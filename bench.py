@@ -77,8 +77,8 @@ def parse():
     ap.add_argument("--size2-envs", type=int, default=1 << 22,
                     help="envs of the post-Infinity-Cache leg (N = 1 only); 0 disables it")
     ap.add_argument("--size2-steps", type=int, default=100)
-    ap.add_argument("--size2-when", choices=("first", "last"), default="first",
-                    help="run the 2^22 leg right after the step leg (default) or after every other leg")
+    ap.add_argument("--size2-when", choices=("first", "last"), default="last",
+                    help="run the 2^22 leg after every other leg (default) or right after the step leg")
     ap.add_argument("--size2-prealloc", action="store_true",
                     help="allocate the 2^22 leg's env before the other legs, whenever it runs (A/B of where "
                          "its memory lands)")
@@ -728,9 +728,11 @@ def main():
                                "mean_ep_reward_main / win_rate_main: main.py:209-211, :225 (winner-filtered "
                                "reward, pre-terminal observation); ego_first_rate: winner == 1"))
 
-    # the step kernel past the Infinity Cache first, while device memory is unfragmented: allocated
-    # after the Q-net and h-DQN legs (gigabytes of trajectory buffers and rings, some freed) the
-    # same 2^22-env batch measured 2.2x slower, with no clock effect (tools/throttle_probe.py)
+    # the step kernel past the Infinity Cache, after every other leg by default. Rounds 2-3 saw it
+    # 2.2-2.6x slower there in one 100-launch window; per-window timing (r03e) showed a one-time
+    # ~7 ms stall inside the first 20 launches, the rest at full speed and every arena placement
+    # equal (tools/placement_probe.py): with the collector off and one rehearsal window, first /
+    # last / last with the env allocated before the legs measure 104.9 / 105.0 / 105.2 us (r03h)
     size2 = None
     do_size2 = world == 1 and args.size2_envs > 0 and args.size2_envs != E
     env2 = size2_env(args, torch) if do_size2 and args.size2_prealloc else None
