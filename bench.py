@@ -351,7 +351,7 @@ def qnet_leg(env, args, world, dist, torch, opponent):
     h = torch.relu(x @ w["fc1.weight"].T + w["fc1.bias"])
     h = torch.relu(h @ w["fc2.weight"].T + w["fc2.bias"])
     greedy_cpu = (h @ w["out.weight"].T + w["out.bias"]).argmax(1)
-    return {"kernel": f"qnet_rollout_kernel<{ {'none': 0, 'uniform': 1, 'self': 2, 'other': 3}[label] }>",
+    return {"kernel": f"qnet_rollout_ws_kernel<{ {'none': '0, false', 'uniform': '1, false', 'self': '2, true', 'other': '3, true'}[label] }>",
             "opponent": label if label != "other" else "other net (main.py Strategy_OP L1; checkpoint l3)",
             "steps_per_launch": T, "launches": L, "dtype": "bf16 (fp32 accumulate)",
             "value": world * E * T * L / elapsed, "unit": "env-steps/s",

@@ -398,16 +398,16 @@ __device__ __forceinline__ void env_step(const mg_params& P, Env& e, int a1, int
 // instruction stream. Identical results to N env_step calls, invalid actions included: those
 // are computed with a stand-in action and their effects dropped by selects (the ego keeps its
 // move unless action1 is bad; nothing after the moves happens, as in env_step's early return).
-template <int N>
+template <int N, bool CHECKED = true>
 __device__ __forceinline__ void env_step_lockstep(const mg_params& P, Env (&e)[N], const int (&a1)[N],
                                                   const int (&a2)[N], StepOut (&r)[N]) {
   double ang[2 * N], sn[2 * N], cs[2 * N];
   bool bad[N];
 #pragma unroll
   for (int j = 0; j < N; ++j) {
-    const bool bad1 = !valid_action(a1[j]);
+    const bool bad1 = CHECKED && !valid_action(a1[j]);
     const bool none2 = a2[j] == MG_ACTION_NONE;
-    const bool bad2 = !(none2 || valid_action(a2[j]));
+    const bool bad2 = CHECKED && !(none2 || valid_action(a2[j]));
     bad[j] = bad1 || bad2;
     r[j].bad = (bad1 ? 1 : 0) | (bad2 ? 2 : 0);
     r[j].r1_int = r[j].r2_int = false;
@@ -1570,7 +1570,7 @@ struct QRollout {
 // explore draw, u.y its random action, u.z the opponent's explore draw, u.w its random action. Envs
 // past n (live[j] false) are stepped too but never stored. A greedy action outside 0..4 (a
 // net with out_dim > 5) gets env_step's KeyError semantics (env_step_lockstep).
-template <int OPP, int N>
+template <int OPP, int N, bool CHECKED>
 __device__ __forceinline__ void qnet_policy_step_n(const QRollout& R, Env (&e)[N], StepOut (&r)[N],
                                                    int64_t i0, const bool (&live)[N], int t,
                                                    const int (&greedy1)[N], const int (&greedy2)[N],
@@ -1590,7 +1590,7 @@ __device__ __forceinline__ void qnet_policy_step_n(const QRollout& R, Env (&e)[N
     if constexpr (OPP >= 2)
       a2[j] = (static_cast<uint64_t>(u.z) < R.opp_greedy_thr) ? greedy2[j] : action_from_u32(u.w);
   }
-  env_step_lockstep<N>(R.P, e, a1, a2, r);
+  env_step_lockstep<N, CHECKED>(R.P, e, a1, a2, r);
 #pragma unroll
   for (int j = 0; j < N; ++j) {
     won[j] = false;
@@ -1650,7 +1650,10 @@ constexpr int qws_ilp() { return OPP == 3 ? 1 : kQWsIlp; }
 template <int OPP>
 constexpr int qws_envs() { return 2 * 64 * kQWsEnvWaves * qws_ilp<OPP>(); }
 
-template <int OPP>
+// CHECKED: a greedy action may fall outside action_dict (a net with out_dim > 5): the lockstep step
+// carries the KeyError selects. Every other launch takes CHECKED = false (-2 % on the ego-only
+// leg, r03i; the self-play and other-net instances showed no gain and keep the checked step).
+template <int OPP, bool CHECKED>
 __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws_kernel(const QRollout R) {
   constexpr int kIlp = qws_ilp<OPP>();
   constexpr int kEnvs = qws_envs<OPP>();  // envs per block
@@ -1722,9 +1725,9 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
       bool won[kIlp];
       // wave-uniform branch: each group's envs stay in named registers
       if (g == 0)
-        qnet_policy_step_n<OPP, kIlp>(R, e0, r, base + local0 + lane, live0, t, greedy1, greedy2, won);
+        qnet_policy_step_n<OPP, kIlp, CHECKED>(R, e0, r, base + local0 + lane, live0, t, greedy1, greedy2, won);
       else
-        qnet_policy_step_n<OPP, kIlp>(R, e1, r, base + local0 + lane, live1, t, greedy1, greedy2, won);
+        qnet_policy_step_n<OPP, kIlp, CHECKED>(R, e1, r, base + local0 + lane, live1, t, greedy1, greedy2, won);
       const int64_t wbase = base + local0;
 #pragma unroll
       for (int j = 0; j < kIlp; ++j) {
@@ -2656,6 +2659,15 @@ __global__ __launch_bounds__(kBlock) void goal_status_kernel(const double* dx1, 
 
 }  // namespace
 
+// one config-5 launch (with dispatch-packet events when mg_time_next_launch armed them)
+template <int OPP, bool CHECKED>
+static void launch_qnet(int64_t blocks, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1, const QRollout& R) {
+  if (ev0 || ev1)
+    hipExtLaunchKernelGGL((qnet_rollout_ws_kernel<OPP, CHECKED>), dim3(blocks), dim3(kQWsThreads), 0, st, ev0, ev1, 0, R);
+  else
+    hipLaunchKernelGGL((qnet_rollout_ws_kernel<OPP, CHECKED>), dim3(blocks), dim3(kQWsThreads), 0, st, R);
+}
+
 extern "C" {
 
 int mg_abi_version(void) { return MG_ABI_VERSION; }
@@ -2856,22 +2868,15 @@ int mg_rollout_qnet(const mg_params* params, const mg_state* state, const mg_tra
   hipStream_t st = static_cast<hipStream_t>(stream);
   hipEvent_t ev0 = g_ev_start, ev1 = g_ev_stop;
   g_ev_start = g_ev_stop = nullptr;
-#define MG_LAUNCH_Q(OPPV)                                                                                   \
-  do {                                                                                                      \
-    if (ev0 || ev1)                                                                                         \
-      hipExtLaunchKernelGGL(qnet_rollout_ws_kernel<OPPV>, dim3(blocks), dim3(kQWsThreads), 0, st, ev0, ev1, 0, R); \
-    else                                                                                                    \
-      hipLaunchKernelGGL(qnet_rollout_ws_kernel<OPPV>, dim3(blocks), dim3(kQWsThreads), 0, st, R);         \
-  } while (0)
+  const bool checked = out_dim > MG_NUM_ACTIONS;  // argmax may name an action past action_dict
   if (opponent_mode == 0)
-    MG_LAUNCH_Q(0);
+    checked ? launch_qnet<0, true>(blocks, st, ev0, ev1, R) : launch_qnet<0, false>(blocks, st, ev0, ev1, R);
   else if (opponent_mode == 1)
-    MG_LAUNCH_Q(1);
+    checked ? launch_qnet<1, true>(blocks, st, ev0, ev1, R) : launch_qnet<1, false>(blocks, st, ev0, ev1, R);
   else if (opponent_mode == 2)
-    MG_LAUNCH_Q(2);
+    launch_qnet<2, true>(blocks, st, ev0, ev1, R);
   else
-    MG_LAUNCH_Q(3);
-#undef MG_LAUNCH_Q
+    launch_qnet<3, true>(blocks, st, ev0, ev1, R);
   return finish_launch("mg_rollout_qnet");
 }
 

@@ -25,7 +25,7 @@ def kernel_key(name):
 
     for k in ("hdqn_rollout", "qnet_rollout", "step_kernel", "rollout_kernel"):  # most specific first
         if k in name:
-            m = re.search(k + r"\w*<(\d)>", name)
+            m = re.search(k + r"\w*<(\d)", name)
             if k in ("hdqn_rollout", "qnet_rollout") and m and m.group(1) != "0":
                 return f"{k}<{m.group(1)}>"
             return k
