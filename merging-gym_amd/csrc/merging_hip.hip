@@ -2107,7 +2107,9 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
           pg = b_goal[j];
           pa = a1;
         }
-        env_step(R.P, ev, a1, a2, rv);
+        // every action here is in action_dict: the lower nets' argmax runs over the first
+        // NUM_ACTIONS outputs, the random draws are 0..4, so the step needs no KeyError path
+        env_step<false>(R.P, ev, a1, a2, rv);
         ac += rv.r1;  // :311-313 extrinsic_reward += reward
         if (ring) {
 #pragma unroll

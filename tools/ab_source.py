@@ -1,6 +1,6 @@
 """Build an A/B variant of libmerging_hip.so from an edited copy of the source (the shipped
 source has no compile-time knobs): each argument after the name is `old=>new`, a literal text
-replacement that must match exactly once.
+replacement that must match exactly once (`old=>>new`: every occurrence).
 
     python tools/ab_source.py ahead6 'kQGlobalAhead = 3;=>kQGlobalAhead = 6;'
     -> tools/variants/lib_ahead6.so (same flags as merging_gym/build.py)
@@ -19,9 +19,11 @@ def main(argv):
     name, edits = argv[0], argv[1:]
     src = open(build.SRC).read()
     for e in edits:
-        old, new = e.split("=>", 1)
-        if src.count(old) != 1:
-            raise SystemExit(f"{name}: '{old}' matches {src.count(old)} times")
+        every = "=>>" in e  # `old=>>new`: replace every occurrence (at least one)
+        old, new = e.split("=>>" if every else "=>", 1)
+        n = src.count(old)
+        if n == 0 or (n != 1 and not every):
+            raise SystemExit(f"{name}: '{old}' matches {n} times")
         src = src.replace(old, new)
     os.makedirs(os.path.join(ROOT, "tools", "variants"), exist_ok=True)
     out = os.path.join(ROOT, "tools", "variants", f"lib_{name}.so")
