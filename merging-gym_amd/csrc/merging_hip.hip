@@ -331,10 +331,19 @@ __device__ __forceinline__ void env_clock(const mg_params& P, Env& e) {
 // qpgen2's vsmall counts as already satisfied and leaves the unconstrained minimiser u = -0.0 (dposl
 // of a = -q, q = 0). (Mathematically u0 = b / t, since
 // D.1 = 0; evaluating that closed form instead moves u0 by an ulp in most steps.)
-__device__ __forceinline__ double mpc_acc(const mg_params& P, int a, double v) {
-  const double b = P.action_speed[a] - v;
+__device__ __forceinline__ double mpc_acc_speed(const mg_params& P, double speed, double v) {
+  const double b = speed - v;
   const double u = div_const(b, P.qp_nz, P.qp_inv_nz) * P.qp_z0;
   return fabs(b) < P.qp_vsmall ? -0.0 : u;  // dposl's -0.0 (a = -q = -0.0): nothing violated
+}
+
+__device__ __forceinline__ double mpc_acc(const mg_params& P, int a, double v) {
+  return mpc_acc_speed(P, P.action_speed[a], v);
+}
+
+// action_dict[a] (merging_env.py:101) or 0.0 where a is not in it (the value is then unused)
+__device__ __forceinline__ double action_speed_or0(const mg_params& P, int a) {
+  return valid_action(a) ? P.action_speed[a] : 0.0;
 }
 
 // v = max(0, v + acc*dT) (an int 0 when the max picks 0), p += v*dT  (:149-150, :153-154)
@@ -362,8 +371,11 @@ __device__ __forceinline__ bool win_test_early(const mg_params& P, const Env& e)
 // MergeEnv.step (merging_env.py:138-195) for one env held in registers. CHECKED = false: the
 // caller guarantees a1 in 0..4 and a2 in -1..4 (device-drawn actions), so the KeyError path and
 // its zeroed outputs are not compiled in.
+// sp1 / sp2: action_dict[a1] / [a2], looked up by the caller (action_speed_or0), so it can issue
+// those loads before the state loads (the step kernel; env_step below looks them up itself)
 template <bool CHECKED = true>
-__device__ __forceinline__ void env_step(const mg_params& P, Env& e, int a1, int a2, StepOut& r) {
+__device__ __forceinline__ void env_step_sp(const mg_params& P, Env& e, int a1, int a2, double sp1, double sp2,
+                                            StepOut& r) {
   r.win_pre = win_test_early(P, e);
   r.first1 = false;
   r.dx1 = 0.0;
@@ -376,7 +388,7 @@ __device__ __forceinline__ void env_step(const mg_params& P, Env& e, int a1, int
   r.done = r.coll = r.r1_int = r.r2_int = false;
   r.r1 = r.r2 = 0.0;
   if (!bad1) {
-    r.acc1 = mpc_acc(P, a1, e.v1);
+    r.acc1 = mpc_acc_speed(P, sp1, e.v1);
     move_car(P, r.acc1, e.p1, e.v1, r.v1_int);
   }
   if (r.bad) {  // the reference raises KeyError at action_dict[...] after advancing this far
@@ -385,13 +397,18 @@ __device__ __forceinline__ void env_step(const mg_params& P, Env& e, int a1, int
     return;
   }
   // action2 None -> acc 0 (:152): the "L0" constant-speed opponent
-  if (a2 != MG_ACTION_NONE) r.acc2 = mpc_acc(P, a2, e.v2);
+  if (a2 != MG_ACTION_NONE) r.acc2 = mpc_acc_speed(P, sp2, e.v2);
   move_car(P, r.acc2, e.p2, e.v2, r.v2_int);
 
   double x1, y1, x2, y2;
   lon2coord(P, e.p1, true, x1, y1);
   lon2coord(P, e.p2, false, x2, y2);
   score_step(P, e, x1, y1, x2, y2, r);
+}
+
+template <bool CHECKED = true>
+__device__ __forceinline__ void env_step(const mg_params& P, Env& e, int a1, int a2, StepOut& r) {
+  env_step_sp<CHECKED>(P, e, a1, a2, action_speed_or0(P, a1), action_speed_or0(P, a2), r);
 }
 
 // N envs stepped statement by statement, so their independent fp64 chains interleave in one
@@ -809,8 +826,12 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const Launch L) {
       a1 = L.a1[i];
       a2 = L.a2 ? static_cast<int>(L.a2[i]) : MG_ACTION_NONE;
     }
+    // the two action_dict lookups (vector loads from the launch arguments) issued before the
+    // state loads, so they are in flight together (looked up inside the step, the first one's
+    // wait came after the state had arrived): -1 to -1.5 % per launch (r03q)
+    const double sp1 = action_speed_or0(P, a1), sp2 = action_speed_or0(P, a2);
     Env e = load_env(L.S, i);
-    env_step(P, e, a1, a2, r);
+    env_step_sp(P, e, a1, a2, sp1, sp2, r);
     if (r.bad) {
       if (L.O.error) atomicOr(L.O.error, r.bad);
       store_env(L.S, i, e);  // clock (and the ego for a bad action2) advanced, nothing else
@@ -865,9 +886,15 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const Launch L) {
     if ((tid & 63) == 0 && live) L.O.won_mask[i >> 6] = m;
   }
   if constexpr (!OUT64) {
-    if (L.O.obs) {  // one launch per step: block staging measured as fast as per-wave staging
-      const int64_t rem = L.n - base;
-      store_obs_tile(obs_tile, r.o, L.O.obs + base * kObs, rem < kBlock ? static_cast<int>(rem) : kBlock);
+    // per-wave staging, no block barrier: a wave held up by a finishing lane's statistics
+    // read-modify-write (a DRAM read past the Infinity Cache) no longer holds up the block's
+    // other three at the barrier (2^22 envs: 107.0 -> 104.8 us per launch with the lookups
+    // above, r03q; +-0 at 2^20)
+    if (L.O.obs) {
+      const int64_t wbase = base + (tid & ~63);
+      const int64_t wrem = L.n - wbase;
+      wave_store_obs(obs_tile + (tid & ~63) * kObs, r.o, L.O.obs + wbase * kObs,
+                     wrem <= 0 ? 0 : (wrem < 64 ? static_cast<int>(wrem) : 64));
     }
   }
 }
