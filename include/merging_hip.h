@@ -27,7 +27,8 @@
  *   mg_rollout_hdqn   T steps of hdqn.py's acting loop (meta-net goal, lower net on [goal] + state,
  *                     goal_status intrinsic reward) fused with the env step: replaces
  *                     Goal_DQN.choose_goal / HDQN.choose_action + env.step (hdqn.py:280-323)
- *   mg_qnet_pack / mg_qnet_forward / mg_qnet_packed_bytes: the Q-net Net (main.py:30-47,
+ *   mg_qnet_pack / mg_qnet_forward / mg_qnet_packed_bytes / mg_qnet_fragments /
+ *   mg_qnet_fragment_bytes: the Q-net Net (main.py:30-47,
  *                     hdqn.py:38-55) in the kernel's packed bf16 layout, and its forward pass
  *   mg_abi_version, mg_last_error, mg_params_default, mg_time_next_launch: library plumbing
  *                     and profiling (no reference twin).
@@ -52,7 +53,7 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 17
+#define MG_ABI_VERSION 18
 #define MG_OBS_DIM 10   /* merging_env.py:75 observation_shape = (10) */
 #define MG_NUM_ACTIONS 5 /* merging_env.py:101-102 action_dict / Discrete(5) */
 #define MG_ACTION_NONE (-1) /* action2=None: the constant-speed "L0" opponent, merging_env.py:152 */
@@ -293,6 +294,14 @@ int mg_qnet_pack(const float* fc1_w, const float* fc1_b, const float* fc2_w, con
                  const float* out_w, const float* out_b, int32_t in_dim, int32_t out_dim,
                  void* packed, void* stream);
 
+/* The fragment-major copy of a packed net (ABI 18), mg_qnet_fragment_bytes() = 66 KB: the 66 MFMA
+ * operand fragments of one forward in the order the kernel consumes them, each the 64 lanes' 16
+ * bytes contiguous (1 KB). mg_rollout_hdqn reads an opponent from another checkpoint
+ * (opponent_mode 3) from global memory in this layout: a fragment load then touches 8 cache
+ * lines instead of the 32 rows of the packed layout. fragments: 16-byte aligned device buffer. */
+size_t mg_qnet_fragment_bytes(void);
+int mg_qnet_fragments(const void* packed, void* fragments, void* stream);
+
 /* q[n,8] fp32 = Net(x[n,in_dim]) with bf16 operands and fp32 accumulation (rows >= out_dim are
  * padding; in_dim is the net's, 1..13: 10 for main.py's Net on observations, 11 for hdqn.py's
  * lower-level Net on goal states [goal] + state, :145, :291). swap_halves != 0 (in_dim 10 only)
@@ -354,9 +363,10 @@ typedef struct mg_hdqn_traj {
  * traj as mg_rollout_qnet; opponent_mode 0 (None, Strategy_OP "L0", :261, :294-296), 1 (uniform),
  * 2 (Strategy_OP "selfplay", :262-264: upper_op = upper, lower_op = lower, so the same two
  * nets) or 3 (any other Strategy_OP, :265-268: upper_op / lower_op loaded from another h-DQN
- * checkpoint -- opp_meta_net / opp_lower_net, packed like meta_net / lower_net, 16-byte aligned,
- * ignored by the other modes; ABI 16. Four nets exceed one CU's LDS, so the opponent's two are
- * read from global memory, where they stay L2-resident): the opponent's goal is chosen by its
+ * checkpoint -- opp_meta_net / opp_lower_net, the mg_qnet_fragments copies of its packed nets
+ * (ABI 18; packed nets until ABI 17), 16-byte aligned, ignored by the other modes; ABI 16. Four
+ * nets exceed one CU's LDS, so the opponent's two are read from global memory, where they stay
+ * L2-resident): the opponent's goal is chosen by its
  * meta-net on the swapped state
  * state[5:] + state[:5] at every outer-loop iteration (:285 -- the launch's first step when
  * goal_op[i] < 0, and the step after a break: the ego's goal reached or the episode ended) and

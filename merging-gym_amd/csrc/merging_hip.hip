@@ -651,40 +651,6 @@ __device__ __forceinline__ void after_step(const mg_params& P, Env& e, StepOut& 
   if (finish) finish_episode(P, e, r, St, final_obs_row, i, sreg);
 }
 
-// Write a block's [rows,10] fp32 observation tile through LDS as contiguous 16-byte stores
-// (a wave's 64 rows of 40 B become 160 dwordx4 lanes instead of 640 scattered dwords).
-// Every thread of the block must call it (two barriers).
-__device__ __forceinline__ void store_obs_tile_n(float* tile, const obs_t (&o)[kObs], float* dst,
-                                                 int nrows, int block) {
-  const int tid = threadIdx.x;
-  float2* t2 = reinterpret_cast<float2*>(tile + tid * kObs);
-#pragma unroll
-  for (int k = 0; k < kObs / 2; ++k)
-    t2[k] = make_float2(static_cast<float>(o[2 * k]), static_cast<float>(o[2 * k + 1]));
-  __syncthreads();
-  const int nfl = nrows * kObs;
-  if (dst == nullptr) {
-  } else if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
-    const int n4 = nfl >> 2;
-    f32x4* d4 = reinterpret_cast<f32x4*>(dst);
-    const f32x4* s4 = reinterpret_cast<const f32x4*>(tile);
-    for (int j = tid; j < n4; j += block) st_out(d4 + j, s4[j]);
-    const int tail = nfl - (n4 << 2);  // 0 or 2
-    if (tid < tail) st_out(dst + (n4 << 2) + tid, tile[(n4 << 2) + tid]);
-  } else {  // rows are 8-byte aligned whenever the buffer is
-    const int n2 = nfl >> 1;
-    f32x2* d2 = reinterpret_cast<f32x2*>(dst);
-    const f32x2* s2 = reinterpret_cast<const f32x2*>(tile);
-    for (int j = tid; j < n2; j += block) st_out(d2 + j, s2[j]);
-  }
-  __syncthreads();
-}
-
-__device__ __forceinline__ void store_obs_tile(float* tile, const obs_t (&o)[kObs], float* dst,
-                                               int nrows) {
-  store_obs_tile_n(tile, o, dst, nrows, kBlock);
-}
-
 // Wave-scope ordering of LDS accesses between the lanes of ONE wave (no s_barrier): the LDS
 // executes a wave's accesses in order; this only stops the compiler from moving them.
 __device__ __forceinline__ void wave_lds_sync() {
@@ -693,8 +659,9 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// The same as store_obs_tile for one wave's 64 rows: the wave's tile slice holds the new
-// observations afterwards, and no other wave is waited for.
+// A wave's [rows,10] fp32 observations written through its LDS slice as contiguous 16-byte stores
+// (64 rows of 40 B become 160 dwordx4 lanes instead of 640 scattered dwords): the slice holds the
+// new observations afterwards, and no other wave is waited for (no block barrier).
 __device__ __forceinline__ void wave_copy_rows(const float* wtile, float* dst, int nrows);
 
 __device__ __forceinline__ void wave_store_obs(float* wtile, const obs_t (&o)[kObs], float* dst,
@@ -1377,20 +1344,22 @@ __device__ __forceinline__ void qnet_mlp_swp(const uint8_t* net, bf16x8 xb0, bf1
   qnet_gather_q(acc3_0, acc3_1, h, q);
 }
 
-// qnet_mlp_swp for a packed net in GLOBAL memory (the h-DQN kernel's opponent from another
-// checkpoint: four nets exceed one CU's LDS, so the opponent's two are read from L2). The same
-// MFMA / ReLU schedule, but its 66 weight fragments come through a buffer resource with a
-// prefetch ring kQGlobalAhead fragments deep across the whole forward: one lane offset per row
-// pattern (five VGPRs) and the per-fragment constant in an SGPR, instead of a 64-bit address per
-// fragment and one fragment ahead (which left each MFMA pair waiting on an L2 round trip).
+// qnet_mlp_swp for a net in GLOBAL memory (the h-DQN kernel's opponent from another checkpoint:
+// four nets exceed one CU's LDS, so the opponent's two are read from L2). The same MFMA / ReLU
+// schedule, but its 66 weight fragments come from the net's FRAGMENT-MAJOR copy
+// (mg_qnet_fragments: fragment s = the 64 lanes' 16 bytes, contiguous, 1 KB) through a buffer
+// resource, in a prefetch ring kQGlobalAhead fragments deep across the whole forward. Read in the
+// packed (LDS) layout, a fragment load touched 32 rows 464 B apart -- 32 cache lines per wave
+// instruction, which the vector L1 processes a line at a time; fragment-major it is 8 lines.
 // Fragments in the order the MFMAs consume them: W1(0); for tile mt = 0..5 W1(mt + 1) then
-// W2(mt, j = 0..7); the last tile's W2(6, 0 / 2 / 4 / 6); then W3(0..6).
+// W2(mt, j = 0..7); the last tile's pairs interleaved with layer 3 (qnet_mlp_swp's tail).
 constexpr int kQGlobalAhead = 3;
 constexpr int kQFrags = 66;
+constexpr int kQFragBytes = kQFrags * 1024;  // mg_qnet_fragment_bytes()
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t qnet_rsrc(const uint8_t* net) {
-  // gfx9 buffer descriptor word 3 (raw untyped dword access), num_records = the packed net
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(net), static_cast<short>(0), kQNetBytes,
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t qnet_rsrc(const uint8_t* frags) {
+  // gfx9 buffer descriptor word 3 (raw untyped dword access), num_records = the fragment copy
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(frags), static_cast<short>(0), kQFragBytes,
                                            0x00020000);
 }
 
@@ -1438,26 +1407,30 @@ __device__ __forceinline__ void qnet_frag_offset(int s, int r, int h, int& lane_
   }
 }
 
-// where qnet_mlp_ring's fragments come from: a buffer resource over a net in global memory, the
-// per-fragment constant in soffset. (The same ring over the LDS nets, 2 to 4 deep, measured
-// within +-1 % of qnet_mlp_swp's one-ahead loads on every Q-net leg, r03: not used there.)
-struct QSrcGlobal {
+// fragment s of a fragment-major net for this lane: 16 contiguous bytes per lane, the fragment's
+// 1 KB offset in soffset. (A ring over the LDS nets, 2 to 4 deep, measured within +-1 % of
+// qnet_mlp_swp's one-ahead loads on every Q-net leg, r03: not used there.)
+struct QSrcFrag {
   __amdgpu_buffer_rsrc_t rs;
-  __device__ __forceinline__ bf16x8 operator()(int lane_b, int const_b) const {
-    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, lane_b, const_b, 0));
+  __device__ __forceinline__ bf16x8 operator()(int s, int lane) const {
+    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * lane, 1024 * s, 0));
   }
 };
+
+// the fragment-major copy of a packed net: block s, lane l <- fragment s of lane l
+__global__ __launch_bounds__(64) void qnet_fragments_kernel(const uint8_t* packed, uint8_t* frags) {
+  const int s = blockIdx.x, lane = threadIdx.x;
+  int lane_b, const_b;
+  qnet_frag_offset(s, lane & 31, lane >> 5, lane_b, const_b);
+  reinterpret_cast<u32x4*>(frags + 1024 * s)[lane] = *reinterpret_cast<const u32x4*>(packed + lane_b + const_b);
+}
 
 template <int D, class Src>
 __device__ __forceinline__ void qnet_mlp_ring(const Src& src, bf16x8 xb0, bf16x8 xb1, float (&q)[8]) {
   static_assert(kQH1 / 32 == 7 && (kQH2Real + 15) / 16 == 7 && 1 + 6 * 9 + 4 + 7 == kQFrags,
                 "qnet_frag_offset's consumption order assumes 7 hidden-1 tiles and 7 layer-3 k-blocks");
-  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-  auto fetch = [&](int s) __attribute__((always_inline)) {
-    int lane_b, const_b;
-    qnet_frag_offset(s, r, h, lane_b, const_b);
-    return src(lane_b, const_b);
-  };
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  auto fetch = [&](int s) __attribute__((always_inline)) { return src(s, lane); };
   bf16x8 ring[D];
 #pragma unroll
   for (int s = 0; s < D; ++s) ring[s] = fetch(s);
@@ -1818,7 +1791,7 @@ struct HRollout {
   double* ext_acc;  // [n] in / out, extrinsic reward since the inner loop began (Goal_DQN rows)
   const uint8_t* meta;
   const uint8_t* lower;
-  const uint8_t* meta_op;   // OPP 3: the opponent's own packed nets (read from global memory / L2)
+  const uint8_t* meta_op;   // OPP 3: the opponent's own nets, fragment-major (read from L2)
   const uint8_t* lower_op;
   uint64_t seed;
   uint64_t first_step;
@@ -1957,7 +1930,7 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
           const bf16x8 x0 = qnet_input(tile + (row0 + r) * kObs, true, h);
           const bf16x8 x1 = qnet_input(tile + (row0 + 32 + r) * kObs, true, h);
           if constexpr (OPP == 3)
-            qnet_mlp_ring<kQGlobalAhead>(QSrcGlobal{qnet_rsrc(R.meta_op)}, x0, x1, q);  // the opponent's own Goal_DQN (:267)
+            qnet_mlp_ring<kQGlobalAhead>(QSrcFrag{qnet_rsrc(R.meta_op)}, x0, x1, q);  // the opponent's own Goal_DQN (:267)
           else
             qnet_mlp_swp(lds_meta, x0, x1, q);
           gop_star = argmax_first(q, R.num_goals);
@@ -1982,7 +1955,7 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
           const bf16x8 x0 = qnet_input_goal(tile + (row0 + r) * kObs, b_gop[row0 + r], h, true);
           const bf16x8 x1 = qnet_input_goal(tile + (row0 + 32 + r) * kObs, b_gop[row0 + 32 + r], h, true);
           if constexpr (OPP == 3)
-            qnet_mlp_ring<kQGlobalAhead>(QSrcGlobal{qnet_rsrc(R.lower_op)}, x0, x1, qo);  // the opponent's own HDQN (:268)
+            qnet_mlp_ring<kQGlobalAhead>(QSrcFrag{qnet_rsrc(R.lower_op)}, x0, x1, qo);  // the opponent's own HDQN (:268)
           else
             qnet_mlp_swp(lds_lower, x0, x1, qo);
           b_aop[j] = static_cast<uint8_t>(argmax_first(qo, MG_NUM_ACTIONS));
@@ -2837,6 +2810,17 @@ int mg_qnet_pack(const float* fc1_w, const float* fc1_b, const float* fc2_w, con
   return finish_launch("mg_qnet_pack");
 }
 
+size_t mg_qnet_fragment_bytes(void) { return static_cast<size_t>(kQFragBytes); }
+
+int mg_qnet_fragments(const void* packed, void* fragments, void* stream) {
+  if (!packed || !fragments) return fail(hipErrorInvalidValue, "%s", "mg_qnet_fragments: NULL pointer");
+  if ((reinterpret_cast<uintptr_t>(packed) | reinterpret_cast<uintptr_t>(fragments)) & 15)
+    return fail(hipErrorInvalidValue, "%s", "mg_qnet_fragments: buffers must be 16-byte aligned");
+  hipLaunchKernelGGL(qnet_fragments_kernel, dim3(kQFrags), dim3(64), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const uint8_t*>(packed), static_cast<uint8_t*>(fragments));
+  return finish_launch("mg_qnet_fragments");
+}
+
 int mg_qnet_forward(const void* packed, const float* x, int32_t in_dim, int32_t swap_halves, float* q,
                     int64_t n, void* stream) {
   if (!packed || !x || !q) return fail(hipErrorInvalidValue, "%s", "mg_qnet_forward: NULL pointer");
@@ -2935,7 +2919,8 @@ int mg_rollout_hdqn(const mg_params* params, const mg_state* state, const mg_tra
   if (opponent_mode == 3 &&
       (!opp_meta_net || !opp_lower_net ||
        ((reinterpret_cast<uintptr_t>(opp_meta_net) | reinterpret_cast<uintptr_t>(opp_lower_net)) & 15)))
-    return fail(hipErrorInvalidValue, "%s", "opponent_mode 3 needs 16-byte aligned opp_meta_net / opp_lower_net");
+    return fail(hipErrorInvalidValue, "%s",
+                "opponent_mode 3 needs 16-byte aligned opp_meta_net / opp_lower_net (mg_qnet_fragments copies)");
   if (htraj && (htraj->ext_reward || htraj->no_break) && !ext_acc)
     return fail(hipErrorInvalidValue, "%s", "ext_reward / no_break need ext_acc (an [n] double device array)");
   if (htraj && htraj->no_break && (reinterpret_cast<uintptr_t>(htraj->no_break) & 7))

@@ -15,7 +15,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libmerging_hip.so"
 LIB_PATH = os.environ.get("MERGING_HIP_LIB", os.path.join(_HERE, LIB_NAME))
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 OBS_DIM = 10
 NUM_ACTIONS = 5
@@ -114,6 +114,8 @@ def _load():
     lib.mg_rollout_random.argtypes = [PP, SP, _c.POINTER(Traj), STP, _c.c_int64, _c.c_int64,
                                       _c.c_uint64, _c.c_uint64, _c.c_int32, _c.c_int32, _c.c_uint32, _P]
     lib.mg_qnet_packed_bytes.restype = _c.c_size_t
+    lib.mg_qnet_fragment_bytes.restype = _c.c_size_t
+    lib.mg_qnet_fragments.argtypes = [_P, _P, _P]
     lib.mg_qnet_pack.argtypes = [_P] * 6 + [_c.c_int32, _c.c_int32, _P, _P]
     lib.mg_qnet_forward.argtypes = [_P, _P, _c.c_int32, _c.c_int32, _P, _c.c_int64, _P]
     lib.mg_rollout_qnet.argtypes = [PP, SP, _c.POINTER(Traj), STP, _c.c_int64, _c.c_int64, _c.c_uint64,
@@ -133,7 +135,8 @@ def _load():
                                      _P, _c.c_int64, _P]
     for f in (lib.mg_step, lib.mg_step_random, lib.mg_reset, lib.mg_observe, lib.mg_rollout_random,
               lib.mg_time_next_launch, lib.mg_qnet_pack, lib.mg_qnet_forward, lib.mg_rollout_qnet,
-              lib.mg_rollout_hdqn, lib.mg_replay_store, lib.mg_replay_sample, lib.mg_goal_status):
+              lib.mg_rollout_hdqn, lib.mg_replay_store, lib.mg_replay_sample, lib.mg_goal_status,
+              lib.mg_qnet_fragments):
         f.restype = _c.c_int
     v = lib.mg_abi_version()
     if v != ABI_VERSION:

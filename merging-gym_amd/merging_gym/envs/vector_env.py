@@ -411,8 +411,8 @@ class MergeVecEnv:
             self._st_ref, self.hdqn_goal.data_ptr(), None if gop is None else gop.data_ptr(),
             None if ext is None else ext.data_ptr(), n, self.env_offset, seed & 0xFFFFFFFFFFFFFFFF, k0 & 0xFFFFFFFFFFFFFFFF,
             T, meta.packed.data_ptr(), meta.out_dim, lower.packed.data_ptr(), meta.reset_argmax(),
-            greedy_threshold(episilo), mode, None if opp_meta is None else opp_meta.packed.data_ptr(),
-            None if opp_lower is None else opp_lower.packed.data_ptr(), None if ring is None else ring.memory.data_ptr(),
+            greedy_threshold(episilo), mode, None if opp_meta is None else opp_meta.fragments.data_ptr(),
+            None if opp_lower is None else opp_lower.fragments.data_ptr(), None if ring is None else ring.memory.data_ptr(),
             None if ring is None else ring._counter.data_ptr(), 0 if ring is None else ring.capacity,
             self._flags, self._stream())
         nat.check(rc, "mg_rollout_hdqn")

@@ -65,6 +65,20 @@ class QNet:
         _native.check(_native.lib.mg_qnet_pack(*(t.data_ptr() for t in ts), self.in_dim, self.out_dim,
                                                self.packed.data_ptr(), stream), "mg_qnet_pack")
 
+    @property
+    def fragments(self):
+        """The fragment-major copy of the packed net (mg_qnet_fragments, made once): the layout
+        mg_rollout_hdqn reads an opponent from another checkpoint in from global memory."""
+        if getattr(self, "_fragments", None) is None:
+            import torch
+
+            f = torch.empty(self._nat.lib.mg_qnet_fragment_bytes(), dtype=torch.uint8, device=self.device)
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+            self._nat.check(self._nat.lib.mg_qnet_fragments(self.packed.data_ptr(), f.data_ptr(), stream),
+                            "mg_qnet_fragments")
+            self._fragments = f
+        return self._fragments
+
     def reset_argmax(self) -> int:
         """argmax of this net on the reset observation (merging_env.py:208-230), computed once on
         the device: the greedy goal Goal_DQN picks after every episode end (hdqn.py:278-283),

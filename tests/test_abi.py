@@ -20,7 +20,8 @@ def test_header_declares_the_step_path():
     assert {"mg_step", "mg_step_random", "mg_reset", "mg_observe", "mg_abi_version",
             "mg_last_error", "mg_params_default", "mg_rollout_random", "mg_rollout_qnet",
             "mg_qnet_pack", "mg_qnet_forward", "mg_qnet_packed_bytes", "mg_replay_store",
-            "mg_replay_sample", "mg_replay_scratch_bytes"} <= _declared()
+            "mg_replay_sample", "mg_replay_scratch_bytes", "mg_goal_status", "mg_qnet_fragments",
+            "mg_qnet_fragment_bytes"} <= _declared()
 
 
 def test_library_exports_every_declared_symbol():
@@ -111,6 +112,11 @@ def test_argument_errors_without_gpu():
     assert rc != 0 and b"NULL" in _native.lib.mg_last_error()
     rc = _native.lib.mg_reset(None, None, None, None, 1, None)
     assert rc != 0
+    # the fragment-major copy of a packed net (ABI 18): 66 fragments of 64 lanes x 16 bytes
+    assert _native.lib.mg_qnet_fragment_bytes() == 66 * 1024
+    assert _native.lib.mg_qnet_fragments(None, None, None) != 0 and b"NULL" in _native.lib.mg_last_error()
+    odd = ctypes.c_void_p((1 << 20) + 8)
+    assert _native.lib.mg_qnet_fragments(odd, odd, None) != 0 and b"aligned" in _native.lib.mg_last_error()
     # replay: missing buffers, bad capacity and short scratch are refused before any launch
     tr = _native.Transitions()
     rc = _native.lib.mg_replay_store(None, None, 16, 22, ctypes.byref(tr), 4, 1, 0, None, 0, None)
