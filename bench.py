@@ -302,6 +302,9 @@ def rollout_leg(env, args, world, dist, torch):
 QNET_USEFUL_FLOP = 2 * (10 * 200 + 200 * 100 + 100 * 5)      # one Net forward, main.py:30-47
 QNET_MFMA_FLOP = 132 * 32 * 32 * 16 * 2 // 64  # MFMAs issued per 64 envs (padded tiles, all-padding k-blocks skipped), per env
 MFMA_BF16_PEAK_TFLOPS = 2500.0                                 # MI355X dense bf16
+# what v_mfma_f32_32x32x16_bf16 sustains on all 1,024 SIMDs with nothing else running (register
+# operands; the clock settles near 1.83 GHz): tools/micro/qfwd_probe.hip, profiles/r03/qfwd_probe_r03m.json
+MFMA_BF16_SUSTAINED_TFLOPS = 1920.0
 
 
 def qnet_leg(env, args, world, dist, torch, opponent):
@@ -360,6 +363,8 @@ def qnet_leg(env, args, world, dist, torch, opponent):
             "mfma_tflops": nets * QNET_MFMA_FLOP * per_s / 1e12,
             "peak_tflops": MFMA_BF16_PEAK_TFLOPS,
             "frac_useful": nets * QNET_USEFUL_FLOP * per_s / 1e12 / MFMA_BF16_PEAK_TFLOPS,
+            "sustained_tflops": MFMA_BF16_SUSTAINED_TFLOPS,
+            "mfma_frac_of_sustained": nets * QNET_MFMA_FLOP * per_s / 1e12 / MFMA_BF16_SUSTAINED_TFLOPS,
             "greedy_agreement_vs_fp32_cpu": float((greedy_gpu == greedy_cpu).double().mean()),
             "agreement_sample": int(x.shape[0])}
 
@@ -480,7 +485,7 @@ def hdqn_leg(env, args, world, dist, torch):
             "other_checkpoint": {"kernel": "hdqn_rollout_kernel<3>", "kernel_ms_mean": other_ms,
                                  "env_steps_per_s": other_per_s,
                                  "frac_useful_lower_bound": self_flop * other_per_s / 1e12 / MFMA_BF16_PEAK_TFLOPS,
-                                 "note": "opponent nets read from global memory (L2), not LDS"},
+                                 "note": "opponent nets read from global memory (L2, fragment-major copies), not LDS"},
             "with_goal_ring": {"fused_store_ms_per_launch": fused_ms, "rollout_then_replay_store_ms": separate_ms,
                                "fused_env_steps_per_s": E * T / (fused_ms * 1e-3),
                                "separate_env_steps_per_s": E * T / (separate_ms * 1e-3),
@@ -489,6 +494,8 @@ def hdqn_leg(env, args, world, dist, torch):
             "ms_per_step": elapsed / (L * T) * 1e3, "kernel_ms_mean": kernel_ms,
             "useful_tflops": HDQN_USEFUL_FLOP * per_s / 1e12, "peak_tflops": MFMA_BF16_PEAK_TFLOPS,
             "frac_useful": HDQN_USEFUL_FLOP * per_s / 1e12 / MFMA_BF16_PEAK_TFLOPS,
+            "mfma_tflops": 2 * QNET_MFMA_FLOP * per_s / 1e12, "sustained_tflops": MFMA_BF16_SUSTAINED_TFLOPS,
+            "mfma_frac_of_sustained": 2 * QNET_MFMA_FLOP * per_s / 1e12 / MFMA_BF16_SUSTAINED_TFLOPS,
             "nets": "seeded, torch.nn.Linear default init U(-1/sqrt(in), 1/sqrt(in)) (signed)",
             "goal_break_rate_per_step": break_rate, "next_goal_share": greedy_goal_spread}
 
