@@ -15,6 +15,11 @@ from __future__ import annotations
 import numpy as np
 
 
+# every finished check's line, printed again at the end of the session by tests/conftest.py
+# (pytest_terminal_summary), so the fractions are in the log even when output is captured (-q)
+SUMMARY: list[str] = []
+
+
 class ChoiceCheck:
     def __init__(self, name: str, tol: float = 1e-2, max_frac: float | None = None):
         self.name, self.tol, self.max_frac = name, tol, max_frac
@@ -50,8 +55,10 @@ class ChoiceCheck:
         return self.excused / max(1, self.greedy)
 
     def finish(self) -> float:
-        print(f"[near-tie] {self.name}: {self.excused} of {self.greedy} greedy choices excused "
-              f"({100 * self.frac:.3f} %, bound {'-' if self.max_frac is None else f'{100 * self.max_frac:.2f} %'})")
+        line = (f"[near-tie] {self.name}: {self.excused} of {self.greedy} greedy choices excused "
+                f"({100 * self.frac:.3f} %, bound {'-' if self.max_frac is None else f'{100 * self.max_frac:.2f} %'})")
+        print(line)
+        SUMMARY.append(line)
         if self.max_frac is not None:
             assert self.frac <= self.max_frac, (self.name, self.excused, self.greedy)
         return self.frac

@@ -47,3 +47,25 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+def pytest_terminal_summary(terminalreporter):
+    """The near-tie excusals of the Q-net / h-DQN greedy checks (tests/choice_check.py), one line
+    per check, printed whether or not output was captured."""
+    try:
+        from choice_check import SUMMARY
+    except ImportError:
+        return
+    if SUMMARY:
+        terminalreporter.section("near-tie excusals (bf16 kernel vs bf16-emulated reference)")
+        excused = greedy = 0
+        for line in SUMMARY:
+            terminalreporter.write_line(line)
+        import re
+
+        for line in SUMMARY:
+            m = re.search(r": (\d+) of (\d+) greedy", line)
+            if m:
+                excused += int(m.group(1))
+                greedy += int(m.group(2))
+        terminalreporter.write_line(f"[near-tie] total: {excused} of {greedy} greedy choices excused")
