@@ -56,7 +56,33 @@ __global__ __launch_bounds__(64 * WAVES) void mfma_only_probe(const uint8_t* net
   (void)net;
 }
 
-template <int WAVES, bool MFMA_ONLY = false>
+// the same matrix-pipe work (132 x 32x32x16 = 264 x 16x16x32 FLOPs) as 16x16x32 MFMAs, 8 independent
+// accumulators: does the smaller shape sustain a higher rate (clock) on all SIMDs?
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+template <int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void mfma16_only_probe(const uint8_t* net, int iters, unsigned long long* cyc,
+                                                                float* out) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  bf16x8 a, b;
+  for (int j = 0; j < 8; ++j) {
+    a[j] = static_cast<__bf16>(0.001f * (lane + j));
+    b[j] = static_cast<__bf16>(0.002f * (lane - j));
+  }
+  f32x4v c[8] = {};
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int k = 0; k < 264; ++k) c[k & 7] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c[k & 7], 0, 0, 0);
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  float acc = 0.f;
+  for (int k = 0; k < 8; ++k) acc += c[k][lane & 3];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+  if (lane == 0) cyc[blockIdx.x * WAVES + wave] = t1 - t0;
+  (void)net;
+}
+
+template <int WAVES, int MODE = 0>  // MODE 0: qnet_forward_swp, 1: 32x32x16 only, 2: 16x16x32 only
 void run(const uint8_t* dnet, int blocks, int iters) {
   unsigned long long* dcyc;
   float* dout;
@@ -67,8 +93,10 @@ void run(const uint8_t* dnet, int blocks, int iters) {
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     (void)hipEventRecord(e0, 0);
-    if (MFMA_ONLY)
+    if (MODE == 1)
       hipLaunchKernelGGL(mfma_only_probe<WAVES>, dim3(blocks), dim3(64 * WAVES), 0, 0, dnet, iters, dcyc, dout);
+    else if (MODE == 2)
+      hipLaunchKernelGGL(mfma16_only_probe<WAVES>, dim3(blocks), dim3(64 * WAVES), 0, 0, dnet, iters, dcyc, dout);
     else
       hipLaunchKernelGGL(qfwd_probe<WAVES>, dim3(blocks), dim3(64 * WAVES), 0, 0, dnet, iters, dcyc, dout);
     (void)hipEventRecord(e1, 0);
@@ -84,7 +112,8 @@ void run(const uint8_t* dnet, int blocks, int iters) {
     std::printf("{\"kernel\": \"%s\", \"waves_per_block\": %d, \"blocks\": %d, \"iters\": %d, "
                 "\"cycles_per_forward\": %.0f, \"mfma_cycles_per_forward\": 4224, \"wall_ms\": %.3f, "
                 "\"mfma_tflops\": %.1f, \"clock_ghz\": %.2f}\n",
-                MFMA_ONLY ? "mfma_only" : "qnet_forward_swp", WAVES, blocks, iters, mean / iters, ms,
+                MODE == 1 ? "mfma_32x32x16_only" : MODE == 2 ? "mfma_16x16x32_only" : "qnet_forward_swp", WAVES, blocks,
+                iters, mean / iters, ms,
                 flops / (ms * 1e-3) / 1e12, mean / (ms * 1e-3) / 1e9);
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
@@ -103,8 +132,10 @@ int main() {
   run<4>(dnet, 256, 2000);  // one Q-net wave per SIMD, one block per CU
   run<8>(dnet, 256, 2000);  // two per SIMD
   run<4>(dnet, 512, 2000);  // one per SIMD, two blocks per CU if they fit
-  run<4, true>(dnet, 256, 2000);  // MFMAs alone, one wave per SIMD
-  run<8, true>(dnet, 256, 2000);  // two per SIMD
+  run<4, 1>(dnet, 256, 2000);  // MFMAs alone, one wave per SIMD
+  run<8, 1>(dnet, 256, 2000);  // two per SIMD
+  run<4, 2>(dnet, 256, 2000);  // the same FLOPs as 16x16x32 MFMAs
+  run<8, 2>(dnet, 256, 2000);
   (void)hipFree(dnet);
   return 0;
 }
