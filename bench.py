@@ -300,11 +300,20 @@ def rollout_leg(env, args, world, dist, torch):
 
 
 QNET_USEFUL_FLOP = 2 * (10 * 200 + 200 * 100 + 100 * 5)      # one Net forward, main.py:30-47
-QNET_MFMA_FLOP = 132 * 32 * 32 * 16 * 2 // 64  # MFMAs issued per 64 envs (padded tiles, all-padding k-blocks skipped), per env
+# MFMAs issued per 64-env forward (ABI 19). The 16x16 forward (self-play / other-net opponents,
+# h-DQN): layer 1 14 x 32x32x16, layers 2 and 3 (196 + 16) x 16x16x32. The 32x32 forward (config 5
+# without a net opponent): 132 x 32x32x16 (padded tiles, all-padding k-blocks skipped).
+QNET_MFMA32_FLOP = 14 * 32 * 32 * 16 * 2
+QNET_MFMA16_FLOP = 212 * 16 * 16 * 32 * 2
+QNET_MFMA_FLOP = (QNET_MFMA32_FLOP + QNET_MFMA16_FLOP) // 64  # per env, 16x16 forward
+QNET32_MFMA_FLOP = 132 * 32 * 32 * 16 * 2 // 64              # per env, 32x32 forward
 MFMA_BF16_PEAK_TFLOPS = 2500.0                                 # MI355X dense bf16
-# what v_mfma_f32_32x32x16_bf16 sustains on all 1,024 SIMDs with nothing else running (register
-# operands; the clock settles near 1.83 GHz): tools/micro/qfwd_probe.hip, profiles/r03/qfwd_probe_r03m.json
-MFMA_BF16_SUSTAINED_TFLOPS = 1920.0
+# what the matrix pipe sustains on all 1,024 SIMDs, one wave per SIMD, nothing else running
+# (register operands, tools/micro/qfwd_probe.hip, profiles/r03/qfwd_probe_16x16.txt): 32x32x16
+# 2.07 PF, 16x16x32 2.33 PF; the 16x16 forward's mix of the two at those rates
+MFMA32_BF16_SUSTAINED_TFLOPS = 2068.0
+MFMA_BF16_SUSTAINED_TFLOPS = round((QNET_MFMA32_FLOP + QNET_MFMA16_FLOP) /
+                                   (QNET_MFMA32_FLOP / MFMA32_BF16_SUSTAINED_TFLOPS + QNET_MFMA16_FLOP / 2330.0), 1)
 
 
 def qnet_leg(env, args, world, dist, torch, opponent):
@@ -344,6 +353,9 @@ def qnet_leg(env, args, world, dist, torch, opponent):
     elapsed = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / L
     nets = 2 if label in ("self", "other") else 1
+    # the instances without a net opponent run the 32x32 forward (qnet32_mlp), the others the 16x16 one
+    mfma_flop, sustained = ((QNET32_MFMA_FLOP, MFMA32_BF16_SUSTAINED_TFLOPS) if nets == 1
+                            else (QNET_MFMA_FLOP, MFMA_BF16_SUSTAINED_TFLOPS))
     per_s = E * T / (kernel_ms * 1e-3)
     # BASELINE config 5: greedy-action agreement with the reference's fp32 Net on the CPU
     # (main.py:30-47, re-declared here with torch) over the envs' current observations
@@ -360,11 +372,12 @@ def qnet_leg(env, args, world, dist, torch, opponent):
             "value": world * E * T * L / elapsed, "unit": "env-steps/s",
             "ms_per_step": elapsed / (L * T) * 1e3, "kernel_ms_mean": kernel_ms,
             "useful_tflops": nets * QNET_USEFUL_FLOP * per_s / 1e12,
-            "mfma_tflops": nets * QNET_MFMA_FLOP * per_s / 1e12,
+            "forward": "32x32" if nets == 1 else "16x16",
+            "mfma_tflops": nets * mfma_flop * per_s / 1e12,
             "peak_tflops": MFMA_BF16_PEAK_TFLOPS,
             "frac_useful": nets * QNET_USEFUL_FLOP * per_s / 1e12 / MFMA_BF16_PEAK_TFLOPS,
-            "sustained_tflops": MFMA_BF16_SUSTAINED_TFLOPS,
-            "mfma_frac_of_sustained": nets * QNET_MFMA_FLOP * per_s / 1e12 / MFMA_BF16_SUSTAINED_TFLOPS,
+            "sustained_tflops": sustained,
+            "mfma_frac_of_sustained": nets * mfma_flop * per_s / 1e12 / sustained,
             "greedy_agreement_vs_fp32_cpu": float((greedy_gpu == greedy_cpu).double().mean()),
             "agreement_sample": int(x.shape[0])}
 

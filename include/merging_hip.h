@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 18
+#define MG_ABI_VERSION 19
 #define MG_OBS_DIM 10   /* merging_env.py:75 observation_shape = (10) */
 #define MG_NUM_ACTIONS 5 /* merging_env.py:101-102 action_dict / Discrete(5) */
 #define MG_ACTION_NONE (-1) /* action2=None: the constant-speed "L0" opponent, merging_env.py:152 */
@@ -288,17 +288,22 @@ int mg_rollout_random(const mg_params* params, const mg_state* state, const mg_t
  * [100,200], fc2.bias [100], out.weight [out,100], out.bias [out] (device pointers, row-major).
  * Weights are stored as bf16; each fp32 bias as three bf16 parts (hi + mid + lo == bias exactly)
  * in padded K slots whose inputs are 1.0, so the matrix cores add it inside the K sum; hidden
- * sizes are the reference's 200 and 100; 1 <= in_dim <= 13, 1 <= out_dim <= 8. */
+ * sizes are the reference's 200 and 100; 1 <= in_dim <= 13, 1 <= out_dim <= 8. ABI 19: the buffer
+ * holds two layouts of the same bf16 values -- first the operand fragments of the 16x16x32 forward
+ * (self-play / other-net opponents, h-DQN, mg_qnet_forward), then the 32x32x16 layout of the
+ * config-5 instances without a net opponent. */
 size_t mg_qnet_packed_bytes(void);
 int mg_qnet_pack(const float* fc1_w, const float* fc1_b, const float* fc2_w, const float* fc2_b,
                  const float* out_w, const float* out_b, int32_t in_dim, int32_t out_dim,
                  void* packed, void* stream);
 
-/* The fragment-major copy of a packed net (ABI 18), mg_qnet_fragment_bytes() = 66 KB: the 66 MFMA
- * operand fragments of one forward in the order the kernel consumes them, each the 64 lanes' 16
- * bytes contiguous (1 KB). mg_rollout_hdqn reads an opponent from another checkpoint
- * (opponent_mode 3) from global memory in this layout: a fragment load then touches 8 cache
- * lines instead of the 32 rows of the packed layout. fragments: 16-byte aligned device buffer. */
+/* The fragment-major copy of a packed net, mg_qnet_fragment_bytes() = mg_qnet_packed_bytes(). Since
+ * ABI 19 the packed layout itself is fragment-major -- the MFMA operand fragments of one forward in
+ * the order the kernel consumes them, each the 64 lanes' 16 bytes contiguous (1 KB; the four
+ * layer-3 fragments 512 B) -- so this is a plain copy, kept for ABI-18 callers (ABI 18: a
+ * separate 66-KB layout). mg_rollout_hdqn reads an opponent from another checkpoint
+ * (opponent_mode 3) from global memory in this layout: a fragment load touches 8 cache lines.
+ * fragments: 16-byte aligned device buffer. */
 size_t mg_qnet_fragment_bytes(void);
 int mg_qnet_fragments(const void* packed, void* fragments, void* stream);
 

@@ -961,27 +961,36 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(const Rollout R) {
 // The reference's DQN Net (scripts/main.py:30-47, scripts/hdqn.py:38-55): Linear(in,200) ->
 // ReLU -> Linear(200,100) -> ReLU -> Linear(100,out), and its epsilon-greedy choose_action
 // (main.py:99-112: greedy argmax when np.random.randn() <= EPISILO, else uniform). Computed
-// in bf16 on the matrix cores with fp32 accumulation (v_mfma_f32_32x32x16_bf16), one wave per
-// 64 envs, in the TRANSPOSED form  H1' = W1 X',  H2' = W2 H1',  Q' = W3 H2'  (hidden units
-// on the 32 rows of a tile, envs on its 32 columns = lanes). A 32x32 accumulator keeps its
-// rows in registers, so it feeds the next MFMA directly as the B operand (k = hidden unit):
-// registers 8s..8s+7 of lane half h hold rows 16s + 8(j>>2) + 4h + (j&3), j = 0..7, and the
-// packed weights store each 16-column block with that k order (mg_qnet_pack), so no lane
-// moves and no LDS round trip between layers.
+// in bf16 on the matrix cores with fp32 accumulation, one wave per 64 envs, in the TRANSPOSED
+// form  H1' = W1 X',  H2' = W2 H1',  Q' = W3 H2'  (hidden units on tile rows, envs on lanes):
+//  * layer 1 (K = 16: up to 13 inputs and the 3 bias slots) on v_mfma_f32_32x32x16_bf16, 7 row
+//    tiles of 32 units x 2 column tiles of 32 envs;
+//  * layers 2 and 3 on v_mfma_f32_16x16x32_bf16: H2' in 7 row tiles of 16 units x 4 column tiles
+//    of 16 envs over 7 k-blocks of 32 hidden-1 units, Q' in one row tile over 4 k-blocks of 32
+//    hidden-2 units. Under load the chip holds a higher clock for the 16x16 shape at equal cycles
+//    per FLOP (tools/micro/qfwd_probe.hip: 2.33-2.47 PF against 2.07 PF for 32x32x16, r03ab), and
+//    16-row tiles pad hidden-2 to 112 units instead of 128: 14 x 32 + (196 + 16) x 16 = 3,840
+//    matrix cycles per 64-env forward (round 3's all-32x32 forward: 132 x 32 = 4,224).
+// No layer's output goes through LDS:
+//  * a 32x32 layer-1 accumulator holds its 32 envs (lane & 31) in both lane halves. After ReLU +
+//    bf16 packing, one v_permlane16_swap per pair of packed registers leaves envs 0..15 in every
+//    16-lane row of the first register and envs 16..31 in the second: each is then the B operand
+//    of a 16x16x32 MFMA (lane l: env column l & 15, k = 8 (l >> 4) + j), in the k order
+//    qnet_unit1, which mg_qnet_pack gives W2's columns;
+//  * a 16x16 accumulator holds rows 4 (l >> 4) .. + 3 of column l & 15, so two row tiles side by
+//    side are the B operand of a layer-3 k-block (k order qnet_unit2, W3's columns);
+//  * the Q tiles of the four column tiles reach one env per lane through two v_permlane32_swap and
+//    one v_permlane16_swap per register (qnet_gather_q).
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short i16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
-constexpr int kQH1 = 224, kQH2 = 128;                              // padded 200, 100
-constexpr int kQH1Real = 200, kQH2Real = 100;                      // main.py:30-47 Net widths
-constexpr int kQS1 = 24, kQS2 = 232, kQS3 = 136;                   // row strides (bf16): every
-// Stored rows: only up to the last row that can be non-zero plus one zero row (W1: units
-// 0..202 + zero row 203; W2: 0..102 + zero row 103; W3: outputs 0..7 + zero row 8). A lane
-// whose tile row lies past them reads the zero row instead (qrow*), so two packed nets fit one
-// CU's LDS beside the observation tiles (the h-DQN kernel).
-constexpr int kQR1 = 204, kQR2 = 104, kQR3 = 9;                    // stored rows per matrix
-constexpr int kQOffW2 = kQR1 * kQS1 * 2;                           // ds_read_b128 lane group hits
-constexpr int kQOffW3 = kQOffW2 + kQR2 * kQS2 * 2;                 // 16 distinct 4-bank slots
-constexpr int kQNetBytes = kQOffW3 + kQR3 * kQS3 * 2;              // 60,496 B
+constexpr int kQH1Real = 200, kQH2Real = 100;  // main.py:30-47 Net widths
+constexpr int kQT1 = 7;  // layer-1 row tiles of 32 units = layer-2 k-blocks (224 >= 203)
+constexpr int kQT2 = 7;  // layer-2 row tiles of 16 units (112 >= 103)
+constexpr int kQK3 = 4;  // layer-3 k-blocks of 32 hidden-2 units (two row tiles each)
 // Biases are folded into the padded K slots: each bias b is split into three bf16 parts
 // hi + mid + lo == b exactly (8 significant bits each, 24 = fp32's), stored as three weight
 // columns whose inputs are 1.0 -- layer-1 inputs 13..15, hidden-1 units 200..202 and hidden-2
@@ -993,6 +1002,9 @@ constexpr int kQBiasIn = 13;       // first of the three layer-1 input slots hol
 constexpr int kQOne1 = 200;        // hidden-1 units 200..202 = 1.0
 constexpr int kQOne2 = 100;        // hidden-2 units 100..102 = 1.0
 constexpr int kQMaxIn = kQBiasIn;  // widest net input: 13
+static_assert(32 * kQT1 >= kQOne1 + 3 && 32 * (kQT1 - 1) < kQH1Real && 16 * kQT2 >= kQOne2 + 3 &&
+                  16 * (kQT2 - 1) < kQH2Real && 32 * kQK3 >= 16 * kQT2,
+              "tile counts cover the hidden units and their 1.0 units, no tile is all padding");
 // specialised kernel: 4 Q-net waves + kQWsEnvWaves env waves (8 env waves -- 3 waves per SIMD,
 // a Q-net wave within 168 VGPRs -- measured 19 % slower); each env lane steps kQWsIlp envs per
 // phase, in lockstep (independent fp64 chains interleaved in one instruction stream), so a group
@@ -1001,39 +1013,63 @@ constexpr int kQWsEnvWaves = 4;
 constexpr int kQWsIlp = 2;
 constexpr int kQWsThreads = 64 * (4 + kQWsEnvWaves);
 constexpr int kQWsWavesPerSimd = (4 + kQWsEnvWaves) / 4;
-static_assert(kQOffW2 % 16 == 0 && kQOffW3 % 16 == 0 && kQNetBytes % 16 == 0,
-              "packed Q-net sections must stay 16-byte aligned");
 
-__device__ __forceinline__ int qrow1(int m) { return m < kQR1 ? m : kQR1 - 1; }
-__device__ __forceinline__ int qrow2(int m) { return m < kQR2 ? m : kQR2 - 1; }
-__device__ __forceinline__ int qrow3(int m) { return m < kQR3 ? m : kQR3 - 1; }
+// The packed net (mg_qnet_pack) is the forward's MFMA A operands in the order it consumes them,
+// each fragment the 64 lanes' 16 bytes contiguous, so a wave's ds_read_b128 (LDS nets) or
+// buffer_load_dwordx4 (nets read from L2) covers 1 KB of consecutive bytes: conflict-free in LDS,
+// 8 cache lines from L2. Consumption order:
+//   s = 0: W1(0); for k-block kb = 0..5: W1(kb + 1), then W2(t, kb) for row tiles t = 0..6;
+//   kb = 6 interleaved with layer 3:  W2(0,6) W2(1,6) W2(2,6) W3(0) W2(3,6) W2(4,6) W3(1)
+//                                     W2(5,6) W2(6,6) W3(2) W3(3)
+// W1(m): lane l = 32 h + r holds W1[32 m + r][8 h .. 8 h + 7] (inputs in natural order, b1's parts
+// at 13..15). W2(t, kb): lane l holds row 16 t + (l & 15), hidden-1 units qnet_unit1(kb, l >> 4,
+// j = 0..7). W3(kb): 512 B -- output rows 0..7 only; lane l reads row l & 7, so rows 8..15 of the
+// Q tile repeat rows 0..7 and are never read.
+struct QFrag {
+  int kind, tile, kb;  // kind 0: W1(tile), 1: W2(tile, kb), 2: W3(kb)
+};
+constexpr int kQFrags = 1 + 6 * 8 + 11;
+// Closed forms (no loops or tables), so that every fragment offset of the unrolled forward folds
+// to a constant. Last k-block: entry u = s - 49 is W3 at u = 3, 6, 9, 10, else W2 row tile u - u / 3.
+__host__ __device__ constexpr QFrag qfrag(int s) {
+  if (s == 0) return QFrag{0, 0, 0};
+  if (s < 49) {
+    const int u = s - 1, kb = u / 8, v = u % 8;
+    return v == 0 ? QFrag{0, kb + 1, 0} : QFrag{1, v - 1, kb};
+  }
+  const int u = s - 49;
+  if (u == 10) return QFrag{2, 0, 3};
+  return u % 3 == 0 && u > 0 ? QFrag{2, 0, u / 3 - 1} : QFrag{1, u - u / 3, kQT1 - 1};
+}
+__host__ __device__ constexpr int qfrag_off(int s) {
+  if (s <= 49) return 1024 * s;
+  const int u = s - 49;
+  return 1024 * s - 512 * ((u > 3) + (u > 6) + (u > 9) + (u > 10));
+}
+constexpr int kQNetBytes = qfrag_off(kQFrags);  // 59,392 B
+static_assert(kQNetBytes == 56 * 1024 + 4 * 512, "7 W1 + 49 W2 fragments of 1 KB, 4 W3 of 512 B");
 
-// hardware k (0..15) within a 16-block -> hidden unit within that block (see above)
-__host__ __device__ constexpr int qnet_krow(int kk) {
-  return 8 * ((kk & 7) >> 2) + 4 * (kk >> 3) + (kk & 3);
+// hidden-1 unit at k = 8 g + j of layer-2 k-block kb: 32x32 accumulator register i = 2 q + e of
+// lane half h holds row (i & 3) + 8 (i >> 2) + 4 h; after the swap, lane row g holds packed
+// register q + 4 (g & 1) of half g >> 1 as its dword q
+__host__ __device__ constexpr int qnet_unit1(int kb, int g, int j) {
+  return 32 * kb + (j & 3) + 8 * (j >> 2) + 16 * (g & 1) + 4 * (g >> 1);
+}
+// hidden-2 unit at k = 8 g + j of layer-3 k-block kb: rows 4 g .. 4 g + 3 of row tiles 2 kb
+// (j < 4) and 2 kb + 1 (j >= 4)
+__host__ __device__ constexpr int qnet_unit2(int kb, int g, int j) {
+  return 32 * kb + 16 * (j >> 2) + 4 * g + (j & 3);
 }
 
-// ReLU + round to bf16 of accumulator registers 8s..8s+7 -> one B fragment. Rounded first,
-// then max(x, 0) on the packed bf16 pairs as signed 16-bit integers: a bf16 with its sign
-// bit set is a negative int16 (and -0.0 becomes +0.0), so max_i16(x, 0) is exactly ReLU --
-// 4 v_cvt_pk_bf16_f32 + 4 v_pk_max_i16 instead of 8 v_max_f32 + 4 converts.
-typedef short i16x2 __attribute__((ext_vector_type(2)));
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-
 // ReLU + bf16 pack of two accumulator values: one v_cvt_pk_bf16_f32 + one v_pk_max_i16
-// (a 2-wide fptrunc selects ONE convert; scalar casts cost 2 converts + a perm).
+// (a 2-wide fptrunc selects ONE convert; scalar casts cost 2 converts + a perm). Rounded first,
+// then max(x, 0) on the packed bf16 pairs as signed 16-bit integers: a bf16 with its sign bit set
+// is a negative int16 (and -0.0 becomes +0.0), so max_i16(x, 0) is exactly ReLU.
 __device__ __forceinline__ uint32_t relu_pair(float x, float y) {
   i16x2 v = __builtin_bit_cast(i16x2, __builtin_convertvector(f32x2{x, y}, bf16x2));
   const i16x2 zero = {0, 0};
   v = __builtin_elementwise_max(v, zero);
   return __builtin_bit_cast(uint32_t, v);
-}
-
-__device__ __forceinline__ bf16x8 relu_bf16(const f32x16& c, int s) {
-  const int b = 8 * s;
-  return __builtin_bit_cast(bf16x8, u32x4{relu_pair(c[b], c[b + 1]), relu_pair(c[b + 2], c[b + 3]),
-                                          relu_pair(c[b + 4], c[b + 5]), relu_pair(c[b + 6], c[b + 7])});
 }
 
 // Layer-1 B fragment of one env: features k = 8h .. 8h+7 of its observation row, in the
@@ -1076,15 +1112,19 @@ __device__ __forceinline__ bf16x8 qnet_input_wide(const float* row16, int h) {
 __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
 
-// Packs fp32 torch Linear weights (row-major [out][in]) and biases into the kernel layout.
+// Packs fp32 torch Linear weights (row-major [out][in]) and biases into the fragment layout above:
+// one thread per (fragment, lane, element).
 __global__ void qnet_pack_kernel(const float* w1, const float* b1, const float* w2, const float* b2,
                                  const float* w3, const float* b3, int in_dim, int out_dim,
                                  uint8_t* packed) {
-  int e = blockIdx.x * blockDim.x + threadIdx.x;
-  __bf16* pw1 = reinterpret_cast<__bf16*>(packed);
-  __bf16* pw2 = reinterpret_cast<__bf16*>(packed + kQOffW2);
-  __bf16* pw3 = reinterpret_cast<__bf16*>(packed + kQOffW3);
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= kQFrags * 64 * 8) return;
+  const int s = e >> 9, lane = (e >> 3) & 63, j = e & 7;
+  const QFrag f = qfrag(s);
   // part p (0 hi, 1 mid, 2 lo) of the three-way bf16 split of b (hi + mid + lo == b)
   auto part = [](float b, int p) {
     const float hi = static_cast<float>(static_cast<__bf16>(b));
@@ -1092,39 +1132,26 @@ __global__ void qnet_pack_kernel(const float* w1, const float* b1, const float* 
     const float mid = static_cast<float>(static_cast<__bf16>(r));
     return p == 0 ? hi : p == 1 ? mid : r - mid;
   };
-  if (e < kQR1 * kQS1) {  // W1[m][k]: natural k order (the input features), then b1's parts
-    const int m = e / kQS1, k = e % kQS1;
-    float v = 0.f;
+  float v = 0.f;
+  int off = qfrag_off(s) + 16 * lane;
+  if (f.kind == 0) {  // W1[m][k]: the input features, then b1's parts; hidden-1 units 200..202 = 1.0
+    const int m = 32 * f.tile + (lane & 31), k = 8 * (lane >> 5) + j;
     if (m < kQH1Real && k < in_dim) v = w1[m * in_dim + k];
     else if (m < kQH1Real && k >= kQBiasIn && k < kQBiasIn + 3) v = part(b1[m], k - kQBiasIn);
-    else if (m >= kQOne1 && m < kQOne1 + 3 && k == kQBiasIn) v = 1.f;  // hidden-1 units = 1.0
-    pw1[e] = static_cast<__bf16>(v);
-    return;
+    else if (m >= kQOne1 && m < kQOne1 + 3 && k == kQBiasIn) v = 1.f;
+  } else if (f.kind == 1) {  // W2[m][u], u = qnet_unit1: then b2's parts; hidden-2 units 100..102 = 1.0
+    const int m = 16 * f.tile + (lane & 15), u = qnet_unit1(f.kb, lane >> 4, j);
+    if (m < kQH2Real && u < kQH1Real) v = w2[m * kQH1Real + u];
+    else if (m < kQH2Real && u >= kQOne1 && u < kQOne1 + 3) v = part(b2[m], u - kQOne1);
+    else if (m >= kQOne2 && m < kQOne2 + 3 && u == kQOne1) v = 1.f;
+  } else {  // W3[m][u], u = qnet_unit2, then b3's parts; rows 0..7 of 16
+    if ((lane & 15) >= 8) return;
+    const int m = lane & 7, u = qnet_unit2(f.kb, lane >> 4, j);
+    if (m < out_dim && u < kQH2Real) v = w3[m * kQH2Real + u];
+    else if (m < out_dim && u >= kQOne2 && u < kQOne2 + 3) v = part(b3[m], u - kQOne2);
+    off = qfrag_off(s) + 16 * (8 * (lane >> 4) + m);
   }
-  e -= kQR1 * kQS1;
-  if (e < kQR2 * kQS2) {  // W2[m][c]: columns in the accumulator's k order, then b2's parts
-    const int m = e / kQS2, c = e % kQS2;
-    const int src = 16 * (c / 16) + qnet_krow(c % 16);
-    float v = 0.f;
-    if (c < kQH1) {
-      if (m < kQH2Real && src < kQH1Real) v = w2[m * kQH1Real + src];
-      else if (m < kQH2Real && src >= kQOne1 && src < kQOne1 + 3) v = part(b2[m], src - kQOne1);
-      else if (m >= kQOne2 && m < kQOne2 + 3 && src == kQOne1) v = 1.f;  // hidden-2 units = 1.0
-    }
-    pw2[e] = static_cast<__bf16>(v);
-    return;
-  }
-  e -= kQR2 * kQS2;
-  if (e < kQR3 * kQS3) {  // W3[m][c], then b3's parts
-    const int m = e / kQS3, c = e % kQS3;
-    const int src = 16 * (c / 16) + qnet_krow(c % 16);
-    float v = 0.f;
-    if (m < out_dim && c < kQH2) {
-      if (src < kQH2Real) v = w3[m * kQH2Real + src];
-      else if (src >= kQOne2 && src < kQOne2 + 3) v = part(b3[m], src - kQOne2);
-    }
-    pw3[e] = static_cast<__bf16>(v);
-  }
+  reinterpret_cast<__bf16*>(packed + off)[j] = static_cast<__bf16>(v);
 }
 
 // A zero the compiler cannot see through. Added to the LDS addresses of loop-invariant
@@ -1143,12 +1170,325 @@ __device__ __forceinline__ void qnet_to_lds(const uint8_t* net, uint8_t* lds) {
   for (int j = threadIdx.x; j < kQNetBytes / 16; j += blockDim.x) dst[j] = src[j];
 }
 
+// Fragment s of a packed net for this lane: a net in LDS ...
+struct QSrcLds {
+  const uint8_t* net;  // + opaque zero: the loads stay where they are used
+  int lo, lo3;         // lane byte offsets within a W1 / W2 fragment and within a W3 fragment
+  __device__ __forceinline__ bf16x8 operator()(int s) const {
+    return *reinterpret_cast<const bf16x8*>(net + qfrag_off(s) + (qfrag(s).kind == 2 ? lo3 : lo));
+  }
+};
+// ... or in global memory (the h-DQN kernel's opponent from another checkpoint: four nets exceed
+// one CU's LDS, so the opponent's two are read from L2), through a buffer resource: the lane offset
+// in a VGPR, the fragment's offset a constant
+struct QSrcGlobal {
+  __amdgpu_buffer_rsrc_t rs;
+  int lo, lo3;
+  __device__ __forceinline__ bf16x8 operator()(int s) const {
+    return __builtin_bit_cast(
+        bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, qfrag(s).kind == 2 ? lo3 : lo, qfrag_off(s), 0));
+  }
+};
+__device__ __forceinline__ int qnet_lane_off() { return 16 * (threadIdx.x & 63); }
+__device__ __forceinline__ int qnet_lane_off3() {
+  const int lane = threadIdx.x & 63;
+  return 16 * (8 * (lane >> 4) + (lane & 7));
+}
+__device__ __forceinline__ QSrcLds qnet_lds(const uint8_t* net) {
+  return QSrcLds{net + opaque_zero(), qnet_lane_off(), qnet_lane_off3()};
+}
+__device__ __forceinline__ QSrcGlobal qnet_global(const uint8_t* net) {
+  // gfx9 buffer descriptor word 3 (raw untyped dword access), num_records = the packed net
+  return QSrcGlobal{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(net), static_cast<short>(0), kQNetBytes,
+                                                      0x00020000),
+                    qnet_lane_off(), qnet_lane_off3()};
+}
+constexpr int kQLdsAhead = 2;     // fragments in flight, LDS nets
+constexpr int kQGlobalAhead = 3;  // fragments in flight, nets read from L2 (five measured the same, r03e)
+
+// (x, y) -> (x with y's lane rows swapped in as documented for the instruction, y likewise).
+// Operands into locals and the result read as one 64-bit value: hipcc (ROCm 7.2) passed element 0
+// for every j when the builtin's arguments were subscripts, and returned the first result for
+// both subscripts of its 2-vector.
+__device__ __forceinline__ void permlane16_swap(uint32_t& x, uint32_t& y) {
+  const uint32_t a = x, b = y;
+  const uint64_t sw = __builtin_bit_cast(uint64_t, __builtin_amdgcn_permlane16_swap(a, b, false, false));
+  x = static_cast<uint32_t>(sw);
+  y = static_cast<uint32_t>(sw >> 32);
+}
+
+// Q tile of column tile t: lane row g holds rows 4 g + i of env 16 t + (l & 15) in register i.
+// Transposed over (g, t) so that lane l = 16 g + c ends with rows 0..7 of env 16 g + c = l:
+// permlane32_swap of tiles (0, 2) and (1, 3) leaves rows 0-3 / 4-7 of tiles 0 and 2 (resp. 1, 3)
+// in lane rows 0, 1, 2, 3 of the first register; permlane16_swap of those two registers then gives
+// rows 0-3 of tile g in lane row g of the first and rows 4-7 in the second.
+__device__ __forceinline__ void qnet_gather_q(const f32x4 (&acc3)[4], float (&q)[8]) {
+  // Inline asm: with the builtins, hipcc (ROCm 7.2) computed register 0's swaps only and returned
+  // them for all four registers. The compiler does not pad hazards inside inline asm, and the
+  // operands come straight from the last layer-3 MFMAs (VGPR accumulators in the rollout kernels):
+  // 16 wait states first cover the XDL-write -> VALU-read distance of a 16x16x32 result (and the
+  // two a VALU write needs before a swap reads it), two more after the block.
+  float x0[4], y0[4], x1[4], y1[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    x0[i] = acc3[0][i];
+    y0[i] = acc3[2][i];
+    x1[i] = acc3[1][i];
+    y1[i] = acc3[3][i];
+  }
+  asm volatile(
+      "s_nop 7\n\ts_nop 7\n\t"
+      "v_permlane32_swap_b32 %0, %4\n\tv_permlane32_swap_b32 %8, %12\n\t"
+      "v_permlane32_swap_b32 %1, %5\n\tv_permlane32_swap_b32 %9, %13\n\t"
+      "v_permlane32_swap_b32 %2, %6\n\tv_permlane32_swap_b32 %10, %14\n\t"
+      "v_permlane32_swap_b32 %3, %7\n\tv_permlane32_swap_b32 %11, %15\n\t"
+      "s_nop 1\n\t"
+      "v_permlane16_swap_b32 %0, %8\n\tv_permlane16_swap_b32 %1, %9\n\t"
+      "v_permlane16_swap_b32 %2, %10\n\tv_permlane16_swap_b32 %3, %11\n\t"
+      "s_nop 1"
+      : "+v"(x0[0]), "+v"(x0[1]), "+v"(x0[2]), "+v"(x0[3]), "+v"(y0[0]), "+v"(y0[1]), "+v"(y0[2]), "+v"(y0[3]),
+        "+v"(x1[0]), "+v"(x1[1]), "+v"(x1[2]), "+v"(x1[3]), "+v"(y1[0]), "+v"(y1[1]), "+v"(y1[2]), "+v"(y1[3]));
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    q[i] = x0[i];
+    q[4 + i] = x1[i];
+  }
+}
+
+// Q-values of this lane's env row0 + lane (rows 0..7) from the layer-1 B fragments of the wave's
+// two 32-env column tiles (xb0: envs row0 + r, xb1: envs row0 + 32 + r, k-half h = lane >> 5),
+// with the weight fragments from src, D in flight. Every lane of the wave must call it.
+// Software-pipelined and fully unrolled: layer 1 of k-block kb + 1 is issued ahead of layer 2 of
+// k-block kb, and its ReLU, packing and swaps are computed in pieces between kb's layer-2 MFMAs
+// (each W2 fragment feeds the four column tiles' MFMAs); layer 3's k-blocks follow the last
+// k-block's layer-2 row tiles they read. Unrolled, the first MFMA into each accumulator takes an
+// inline zero and the next k-block's operands land in their final registers.
+template <int D, class Src>
+__device__ __forceinline__ void qnet_mlp(const Src& src, bf16x8 xb0, bf16x8 xb1, float (&q)[8]) {
+  static_assert(kQT1 == 7 && kQT2 == 7 && kQK3 == 4 && kQFrags == 60,
+                "qfrag's consumption order assumes 7 k-blocks, 7 layer-2 row tiles and 4 layer-3 k-blocks");
+  bf16x8 ring[D];
+#pragma unroll
+  for (int s = 0; s < D; ++s) ring[s] = src(s);
+  auto take = [&](int s) __attribute__((always_inline)) {
+    const bf16x8 f = ring[s % D];
+    if (s + D < kQFrags) ring[s % D] = src(s + D);
+    return f;
+  };
+  const f32x16 z16 = {};
+  const f32x4 z4 = {};
+  f32x16 c0, c1;
+  auto layer1 = [&](int s) __attribute__((always_inline)) {
+    const bf16x8 a1 = take(s);
+    c0 = mfma32(a1, xb0, z16);
+    c1 = mfma32(a1, xb1, z16);
+  };
+  // packed ReLU pairs of c0 (d = 0..7) and c1 (d = 8..15)
+  auto relu_d = [&](int d) __attribute__((always_inline)) {
+    const f32x16& c = d < 8 ? c0 : c1;
+    const int b = 2 * (d & 7);
+    return relu_pair(c[b], c[b + 1]);
+  };
+  uint32_t nx[16];
+  // swaps of column tile u's packed registers: afterwards nx[8u + q] is dword q of the B operand
+  // of env tile 2u, nx[8u + 4 + q] that of env tile 2u + 1
+  auto swap_u = [&](int u) __attribute__((always_inline)) {
+#pragma unroll
+    for (int qd = 0; qd < 4; ++qd) permlane16_swap(nx[8 * u + qd], nx[8 * u + 4 + qd]);
+  };
+  auto operands = [&](bf16x8 (&hb)[4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) hb[t] = __builtin_bit_cast(bf16x8, u32x4{nx[4 * t], nx[4 * t + 1], nx[4 * t + 2], nx[4 * t + 3]});
+  };
+  layer1(0);
+#pragma unroll
+  for (int d = 0; d < 16; ++d) nx[d] = relu_d(d);
+  swap_u(0);
+  swap_u(1);
+  bf16x8 hb[4];
+  operands(hb);
+  f32x4 acc2[kQT2][4];
+  // One MFMA per slot and the vector work placed behind it, in source order (sched_barrier): a
+  // 16x16x32 MFMA occupies the matrix pipe 16 cycles, room for one ReLU pair (v_cvt_pk + v_pk_max)
+  // or one swap of the wave's own instruction stream; left to the scheduler, the four MFMAs of a
+  // row tile went out back to back and the vector work behind them held the next row tile.
+  auto slot = [&](f32x4& acc, const bf16x8& a, const bf16x8& b, bool zero) __attribute__((always_inline)) {
+    __builtin_amdgcn_sched_barrier(0);
+    acc = mfma16(a, b, zero ? z4 : acc);
+  };
+  int s = 1;
+#pragma unroll
+  for (int kb = 0; kb < kQT1 - 1; ++kb) {
+    layer1(s++);
+#pragma unroll
+    for (int t2 = 0; t2 < kQT2; ++t2) {
+      const bf16x8 a2 = take(s++);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        slot(acc2[t2][t], a2, hb[t], kb == 0);
+        // the next k-block's operands: ReLU pairs behind row tiles 1..4, swaps behind 5 and 6
+        if (t2 >= 1 && t2 <= 4) nx[4 * (t2 - 1) + t] = relu_d(4 * (t2 - 1) + t);
+        if (t2 == 5) permlane16_swap(nx[t], nx[4 + t]);
+        if (t2 == 6) permlane16_swap(nx[8 + t], nx[12 + t]);
+      }
+    }
+    operands(hb);
+  }
+  // The last k-block with layer 3 interleaved. Layer-3 k-block k3 reads row tiles 2 k3 and 2 k3 + 1;
+  // the ReLU pairs of its B operands are built in the slots after each row tile's MFMAs have issued
+  // (two pairs per slot), into two buffers used alternately.
+  f32x4 acc3[4];
+  uint32_t b3[2][4][4];
+  auto pairs3 = [&](int t2, int t) __attribute__((always_inline)) {  // row tile t2 of env tile t
+    const int buf = (t2 >> 1) & 1, d = 2 * (t2 & 1);
+    b3[buf][t][d] = relu_pair(acc2[t2][t][0], acc2[t2][t][1]);
+    b3[buf][t][d + 1] = relu_pair(acc2[t2][t][2], acc2[t2][t][3]);
+  };
+  // slots of layer-2 row tile t2, each followed by the pairs of row tile p (p < 0: none)
+  auto layer2 = [&](int t2, int p) __attribute__((always_inline)) {
+    const bf16x8 a2 = take(s++);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      slot(acc2[t2][t], a2, hb[t], false);
+      if (p >= 0) pairs3(p, t);
+    }
+  };
+  auto layer3 = [&](int k3, int p) __attribute__((always_inline)) {
+    const bf16x8 a3 = take(s++);
+    const int buf = k3 & 1;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (2 * k3 + 1 >= kQT2) b3[buf][t][2] = b3[buf][t][3] = 0u;  // row tile 7 does not exist
+      const bf16x8 b = __builtin_bit_cast(bf16x8, u32x4{b3[buf][t][0], b3[buf][t][1], b3[buf][t][2], b3[buf][t][3]});
+      slot(acc3[t], a3, b, k3 == 0);
+      if (p >= 0) pairs3(p, t);
+    }
+  };
+  static_assert(kQT2 == 7 && kQK3 == 4, "the tail below is written for 7 row tiles, 4 layer-3 k-blocks");
+  layer2(0, -1);
+  layer2(1, 0);
+  layer2(2, 1);
+  layer3(0, 2);
+  layer2(3, -1);
+  layer2(4, 3);
+  layer3(1, 4);
+  layer2(5, -1);
+  layer2(6, 5);
+  layer3(2, 6);
+  layer3(3, -1);
+  qnet_gather_q(acc3, q);
+}
+
+// the forward of a net in LDS
+__device__ __forceinline__ void qnet_mlp_swp(const uint8_t* net, bf16x8 xb0, bf16x8 xb1, float (&q)[8]) {
+  qnet_mlp<kQLdsAhead>(qnet_lds(net), xb0, xb1, q);
+}
+
+// Q-values of this lane's env (rows 0..7) from the block's f32 observation tile in LDS.
+// row0 = tile row of this wave's lane 0. swap = the opponent's view state[5:] + state[:5]
+// (scripts/main.py:199, human_player.py:40-41). Every lane of the wave must call it.
+__device__ __forceinline__ void qnet_forward_swp(const uint8_t* net, const float* tile, int row0,
+                                                 bool swap, float (&q)[8]) {
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  qnet_mlp_swp(net, qnet_input(tile + (row0 + r) * kObs, swap, h),
+               qnet_input(tile + (row0 + 32 + r) * kObs, swap, h), q);
+}
+
+// ---------------------------------------------------------------------------- 32x32 forward
+// The all-32x32x16 forward (rounds 1-3), kept for the config-5 instances without a net opponent
+// (qnet_rollout_ws_kernel<0 / 1>). There the Q-net wave shares its SIMD's vector issue with an
+// env wave that needs as much of it, and an MFMA holds the issue 8 cycles whatever its shape
+// (MI355X_MICROARCH.md): 132 MFMAs per forward hold it 1,056 cycles, the 16x16 forward's 226 hold
+// it 1,808. A/B at 2^20 envs, same process (profiles/r03/ab/qnet_16x16_ab_r03af.txt): ego-only
+// 49.6 us/step with this forward, 53.2 with the 16x16 one; self-play 91.5 against 85.4.
+// Its packed layout follows the 16x16 fragments in the same buffer (mg_qnet_pack writes both):
+// W1 [204 x 24], W2 [104 x 232], W3 [9 x 136] bf16 rows (strides conflict-free for
+// ds_read_b128), transposed as above with hidden units on the 32 rows of a tile; registers
+// 8s..8s+7 of lane half h of a 32x32 accumulator hold rows 16s + 8(j>>2) + 4h + (j&3), and W2 / W3
+// store each 16-column block in that k order, so an accumulator feeds the next MFMA directly.
+constexpr int kQ32H1 = 224, kQ32H2 = 128;  // padded 200, 100
+constexpr int kQ32S1 = 24, kQ32S2 = 232, kQ32S3 = 136;  // row strides (bf16)
+// Stored rows: only up to the last row that can be non-zero plus one zero row (W1: units
+// 0..202 + zero row 203; W2: 0..102 + zero row 103; W3: outputs 0..7 + zero row 8). A lane
+// whose tile row lies past them reads the zero row instead (q32row*).
+constexpr int kQ32R1 = 204, kQ32R2 = 104, kQ32R3 = 9;                    // stored rows per matrix
+constexpr int kQ32OffW2 = kQ32R1 * kQ32S1 * 2;                           // ds_read_b128 lane group hits
+constexpr int kQ32OffW3 = kQ32OffW2 + kQ32R2 * kQ32S2 * 2;                 // 16 distinct 4-bank slots
+constexpr int kQ32NetBytes = kQ32OffW3 + kQ32R3 * kQ32S3 * 2;              // 60,496 B
+static_assert(kQ32OffW2 % 16 == 0 && kQ32OffW3 % 16 == 0 && kQ32NetBytes % 16 == 0 && kQNetBytes % 16 == 0,
+              "packed Q-net sections must stay 16-byte aligned");
+
+__device__ __forceinline__ int q32row1(int m) { return m < kQ32R1 ? m : kQ32R1 - 1; }
+__device__ __forceinline__ int q32row2(int m) { return m < kQ32R2 ? m : kQ32R2 - 1; }
+__device__ __forceinline__ int q32row3(int m) { return m < kQ32R3 ? m : kQ32R3 - 1; }
+
+// hardware k (0..15) within a 16-block -> hidden unit within that block (see above)
+__host__ __device__ constexpr int q32_krow(int kk) {
+  return 8 * ((kk & 7) >> 2) + 4 * (kk >> 3) + (kk & 3);
+}
+
+__device__ __forceinline__ bf16x8 relu_bf16(const f32x16& c, int s) {
+  const int b = 8 * s;
+  return __builtin_bit_cast(bf16x8, u32x4{relu_pair(c[b], c[b + 1]), relu_pair(c[b + 2], c[b + 3]),
+                                          relu_pair(c[b + 4], c[b + 5]), relu_pair(c[b + 6], c[b + 7])});
+}
+
+// Packs fp32 torch Linear weights (row-major [out][in]) and biases into the kernel layout.
+__global__ void qnet32_pack_kernel(const float* w1, const float* b1, const float* w2, const float* b2,
+                                 const float* w3, const float* b3, int in_dim, int out_dim,
+                                 uint8_t* packed) {
+  int e = blockIdx.x * blockDim.x + threadIdx.x;
+  __bf16* pw1 = reinterpret_cast<__bf16*>(packed);
+  __bf16* pw2 = reinterpret_cast<__bf16*>(packed + kQ32OffW2);
+  __bf16* pw3 = reinterpret_cast<__bf16*>(packed + kQ32OffW3);
+  // part p (0 hi, 1 mid, 2 lo) of the three-way bf16 split of b (hi + mid + lo == b)
+  auto part = [](float b, int p) {
+    const float hi = static_cast<float>(static_cast<__bf16>(b));
+    const float r = b - hi;
+    const float mid = static_cast<float>(static_cast<__bf16>(r));
+    return p == 0 ? hi : p == 1 ? mid : r - mid;
+  };
+  if (e < kQ32R1 * kQ32S1) {  // W1[m][k]: natural k order (the input features), then b1's parts
+    const int m = e / kQ32S1, k = e % kQ32S1;
+    float v = 0.f;
+    if (m < kQH1Real && k < in_dim) v = w1[m * in_dim + k];
+    else if (m < kQH1Real && k >= kQBiasIn && k < kQBiasIn + 3) v = part(b1[m], k - kQBiasIn);
+    else if (m >= kQOne1 && m < kQOne1 + 3 && k == kQBiasIn) v = 1.f;  // hidden-1 units = 1.0
+    pw1[e] = static_cast<__bf16>(v);
+    return;
+  }
+  e -= kQ32R1 * kQ32S1;
+  if (e < kQ32R2 * kQ32S2) {  // W2[m][c]: columns in the accumulator's k order, then b2's parts
+    const int m = e / kQ32S2, c = e % kQ32S2;
+    const int src = 16 * (c / 16) + q32_krow(c % 16);
+    float v = 0.f;
+    if (c < kQ32H1) {
+      if (m < kQH2Real && src < kQH1Real) v = w2[m * kQH1Real + src];
+      else if (m < kQH2Real && src >= kQOne1 && src < kQOne1 + 3) v = part(b2[m], src - kQOne1);
+      else if (m >= kQOne2 && m < kQOne2 + 3 && src == kQOne1) v = 1.f;  // hidden-2 units = 1.0
+    }
+    pw2[e] = static_cast<__bf16>(v);
+    return;
+  }
+  e -= kQ32R2 * kQ32S2;
+  if (e < kQ32R3 * kQ32S3) {  // W3[m][c], then b3's parts
+    const int m = e / kQ32S3, c = e % kQ32S3;
+    const int src = 16 * (c / 16) + q32_krow(c % 16);
+    float v = 0.f;
+    if (m < out_dim && c < kQ32H2) {
+      if (src < kQH2Real) v = w3[m * kQH2Real + src];
+      else if (src >= kQOne2 && src < kQOne2 + 3) v = part(b3[m], src - kQOne2);
+    }
+    pw3[e] = static_cast<__bf16>(v);
+  }
+}
+
 // Rows 0-3 of the env of lane 32t + r sit in registers 0-3 of lane half 0 of column tile t,
 // rows 4-7 in lane half 1. One v_permlane32_swap per register pair (gfx950) exchanges tile 0's
 // upper half with tile 1's lower half: afterwards register j of the first operand holds row j and
 // of the second row 4 + j of the lane's own env, in both lane halves (the ds_bpermute round trip
 // plus selects it replaces sat between the forward's last MFMA and the argmax).
-__device__ __forceinline__ void qnet_gather_q(const f32x16& acc3_0, const f32x16& acc3_1, int h,
+__device__ __forceinline__ void qnet32_gather_q(const f32x16& acc3_0, const f32x16& acc3_1, int h,
                                               float (&q)[8]) {
   (void)h;
 #pragma unroll
@@ -1164,102 +1504,16 @@ __device__ __forceinline__ void qnet_gather_q(const f32x16& acc3_0, const f32x16
   }
 }
 
-// Q-values of this lane's env (rows 0..7) from the block's f32 observation tile in LDS.
-// row0 = tile row of this wave's lane 0. swap = the opponent's view state[5:] + state[:5]
-// (scripts/main.py:199, human_player.py:40-41). Every lane of the wave must call it.
-// WIDE: tile rows are 16 floats (qnet_input_wide) instead of the 10-float observations.
-// Compact form (the hidden-tile loop not unrolled) for the uniform kernel and the standalone
-// forward; the specialised kernel's Q-net waves run qnet_forward_swp.
-template <bool WIDE = false>
-__device__ __forceinline__ void qnet_forward(const uint8_t* net, const float* tile, int row0,
-                                             bool swap, float (&q)[8]) {
-  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-  // Both N-tiles in the same hidden-tile iteration: two independent MFMA -> VALU -> MFMA
-  // chains per wave and one W2 fragment load per pair of MFMAs (one N-tile at a time, with 4
-  // accumulators instead of 8, measured 7-12 % slower).
-  f32x16 acc3_0 = {}, acc3_1 = {};
-  {
-    const int z = opaque_zero();
-    const __bf16* W1 = reinterpret_cast<const __bf16*>(net) + z;
-    const __bf16* W2 = reinterpret_cast<const __bf16*>(net + kQOffW2) + z;
-    const __bf16* W3 = reinterpret_cast<const __bf16*>(net + kQOffW3) + z;
-    const bf16x8 xb0 = WIDE ? qnet_input_wide(tile + (row0 + r) * 16, h)
-                            : qnet_input(tile + (row0 + r) * kObs, swap, h);
-    const bf16x8 xb1 = WIDE ? qnet_input_wide(tile + (row0 + 32 + r) * 16, h)
-                            : qnet_input(tile + (row0 + 32 + r) * kObs, swap, h);
-    f32x16 acc2a[4] = {}, acc2b[4] = {};
-#pragma unroll 1
-    for (int mt = 0; mt < kQH1 / 32; ++mt) {
-      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(W1 + qrow1(32 * mt + r) * kQS1 + 8 * h);
-      auto w2frag = [&](int m2, int sk) {
-        return *reinterpret_cast<const bf16x8*>(W2 + qrow2(32 * m2 + r) * kQS2 + 16 * (2 * mt + sk) +
-                                                8 * h);
-      };
-      bf16x8 a2cur = w2frag(0, 0);
-      const f32x16 zero = {};
-      const f32x16 c0 = mfma32(a1, xb0, zero);
-      const f32x16 c1 = mfma32(a1, xb1, zero);
-      const bf16x8 ha[2] = {relu_bf16(c0, 0), relu_bf16(c0, 1)};
-      const bf16x8 hb[2] = {relu_bf16(c1, 0), relu_bf16(c1, 1)};
-#pragma unroll
-      for (int m2 = 0; m2 < kQH2 / 32; ++m2) {
-#pragma unroll
-        for (int sk = 0; sk < 2; ++sk) {
-          // one fragment ahead: the next load is in flight under this pair of MFMAs (loaded at
-          // its use, each pair waited on LDS; all eight up front spilled: +17 %)
-          const bf16x8 a2 = a2cur;
-          if (2 * m2 + sk + 1 < kQH2 / 16) a2cur = w2frag((2 * m2 + sk + 1) >> 1, (sk + 1) & 1);
-          __builtin_amdgcn_sched_barrier(0);
-          acc2a[m2] = mfma32(a2, ha[sk], acc2a[m2]);
-          acc2b[m2] = mfma32(a2, hb[sk], acc2b[m2]);
-        }
-      }
-    }
-#pragma unroll
-    for (int m2 = 0; m2 < kQH2 / 32; ++m2) {
-      const bf16x8 ha[2] = {relu_bf16(acc2a[m2], 0), relu_bf16(acc2a[m2], 1)};
-      const bf16x8 hb[2] = {relu_bf16(acc2b[m2], 0), relu_bf16(acc2b[m2], 1)};
-#pragma unroll
-      for (int sk = 0; sk < 2; ++sk) {
-        const bf16x8 a3 =
-            *reinterpret_cast<const bf16x8*>(W3 + qrow3(r) * kQS3 + 16 * (2 * m2 + sk) + 8 * h);
-        acc3_0 = mfma32(a3, ha[sk], acc3_0);
-        acc3_1 = mfma32(a3, hb[sk], acc3_1);
-      }
-    }
-  }
-  qnet_gather_q(acc3_0, acc3_1, h, q);
-}
-
-// qnet_forward (pair mode) software-pipelined over the hidden tiles and fully unrolled, for a
-// wave that runs only the Q-net (qnet_rollout_ws_kernel has the registers for it): layer 1 of
-// hidden tile mt + 1 is issued ahead of layer 2 of tile mt, and its ReLU is computed in pieces
-// between tile mt's layer-2 MFMAs, so the vector work runs while the matrix pipe is busy
-// instead of between dependent MFMAs. Unrolled, the first MFMA into each layer-2 accumulator
-// takes an inline zero and the fragments built for the next tile land in their final
-// registers (rolled, 128 zeroing moves per forward plus ~14 rotation moves per tile: -5..7 %).
-// The forward from the layer-1 B fragments of the wave's two 32-env column tiles (xb0: envs
-// row0 + r, xb1: envs row0 + 32 + r, k-half h = lane >> 5), for callers that build the input
-// themselves (the h-DQN kernel's goal states and terminal observations).
-__device__ __forceinline__ void qnet_mlp_swp(const uint8_t* net, bf16x8 xb0, bf16x8 xb1, float (&q)[8]);
-
-__device__ __forceinline__ void qnet_forward_swp(const uint8_t* net, const float* tile, int row0,
-                                                 bool swap, float (&q)[8]) {
-  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-  qnet_mlp_swp(net, qnet_input(tile + (row0 + r) * kObs, swap, h),
-               qnet_input(tile + (row0 + 32 + r) * kObs, swap, h), q);
-}
-
-__device__ __forceinline__ void qnet_mlp_swp(const uint8_t* net, bf16x8 xb0, bf16x8 xb1, float (&q)[8]) {
+__device__ __forceinline__ void qnet32_mlp(const uint8_t* net, bf16x8 xb0, bf16x8 xb1, float (&q)[8]) {
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int z = opaque_zero();
   const __bf16* W1 = reinterpret_cast<const __bf16*>(net) + z;
-  const __bf16* W2 = reinterpret_cast<const __bf16*>(net + kQOffW2) + z;
-  const __bf16* W3 = reinterpret_cast<const __bf16*>(net + kQOffW3) + z;
+  const __bf16* W2 = reinterpret_cast<const __bf16*>(net + kQ32OffW2) + z;
+  const __bf16* W3 = reinterpret_cast<const __bf16*>(net + kQ32OffW3) + z;
   f32x16 acc2a[4] = {}, acc2b[4] = {};
   const f32x16 zero = {};
   auto layer1 = [&](int mt, f32x16& c0, f32x16& c1) {
-    const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(W1 + qrow1(32 * mt + r) * kQS1 + 8 * h);
+    const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(W1 + q32row1(32 * mt + r) * kQ32S1 + 8 * h);
     c0 = mfma32(a1, xb0, zero);
     c1 = mfma32(a1, xb1, zero);
   };
@@ -1268,7 +1522,7 @@ __device__ __forceinline__ void qnet_mlp_swp(const uint8_t* net, bf16x8 xb0, bf1
   // hb[f]: f = 0, 1 -> column tile 0 k-steps 0, 1; f = 2, 3 -> column tile 1
   bf16x8 hb[4] = {relu_bf16(c0, 0), relu_bf16(c0, 1), relu_bf16(c1, 0), relu_bf16(c1, 1)};
   auto w2frag = [&](int mt, int j) {
-    return *reinterpret_cast<const bf16x8*>(W2 + qrow2(32 * (j >> 1) + r) * kQS2 + 16 * (2 * mt + (j & 1)) + 8 * h);
+    return *reinterpret_cast<const bf16x8*>(W2 + q32row2(32 * (j >> 1) + r) * kQ32S2 + 16 * (2 * mt + (j & 1)) + 8 * h);
   };
   // one hidden tile: its layer 2, with the next tile's layer 1 + ReLU folded in when `more`
   // (a constant at every call site). nk: 16-unit k-blocks of the tile that hold real units --
@@ -1303,7 +1557,7 @@ __device__ __forceinline__ void qnet_mlp_swp(const uint8_t* net, bf16x8 xb0, bf1
         hb[f] = __builtin_bit_cast(bf16x8, u32x4{nx[4 * f], nx[4 * f + 1], nx[4 * f + 2], nx[4 * f + 3]});
     }
   };
-  constexpr int kLast = kQH1 / 32 - 1;
+  constexpr int kLast = kQ32H1 / 32 - 1;
   static_assert(16 * (2 * kLast + 1) >= kQH1Real && 32 * kLast < kQH1Real,
                 "only the last hidden tile's second k-block is padding");
 #pragma unroll
@@ -1315,9 +1569,9 @@ __device__ __forceinline__ void qnet_mlp_swp(const uint8_t* net, bf16x8 xb0, bf1
   // the tile's MFMAs had no vector work beside them and layer 3 is mostly vector work. W2 and W3
   // fragments one ahead.
   f32x16 acc3_0 = {}, acc3_1 = {};
-  auto w3frag = [&](int kb) { return *reinterpret_cast<const bf16x8*>(W3 + qrow3(r) * kQS3 + 16 * kb + 8 * h); };
+  auto w3frag = [&](int kb) { return *reinterpret_cast<const bf16x8*>(W3 + q32row3(r) * kQ32S3 + 16 * kb + 8 * h); };
   constexpr int kK3 = (kQH2Real + 15) / 16;
-  static_assert(kK3 == 7 && kQH2 / 32 == 4, "layer 3 k-blocks 2 m2, 2 m2 + 1 follow layer-2 row tile m2");
+  static_assert(kK3 == 7 && kQ32H2 / 32 == 4, "layer 3 k-blocks 2 m2, 2 m2 + 1 follow layer-2 row tile m2");
   bf16x8 a3n = w3frag(0);
   auto layer3 = [&](int m2) __attribute__((always_inline)) {
 #pragma unroll
@@ -1332,180 +1586,30 @@ __device__ __forceinline__ void qnet_mlp_swp(const uint8_t* net, bf16x8 xb0, bf1
   };
   bf16x8 a2n = w2frag(kLast, 0);
 #pragma unroll
-  for (int m2 = 0; m2 < kQH2 / 32; ++m2) {
+  for (int m2 = 0; m2 < kQ32H2 / 32; ++m2) {
     const bf16x8 a2 = a2n;
-    if (m2 + 1 < kQH2 / 32) a2n = w2frag(kLast, 2 * (m2 + 1));
+    if (m2 + 1 < kQ32H2 / 32) a2n = w2frag(kLast, 2 * (m2 + 1));
     __builtin_amdgcn_sched_barrier(0);
     acc2a[m2] = mfma32(a2, hb[0], acc2a[m2]);
     acc2b[m2] = mfma32(a2, hb[2], acc2b[m2]);
     if (m2 > 0) layer3(m2 - 1);
   }
-  layer3(kQH2 / 32 - 1);
-  qnet_gather_q(acc3_0, acc3_1, h, q);
+  layer3(kQ32H2 / 32 - 1);
+  qnet32_gather_q(acc3_0, acc3_1, h, q);
 }
 
-// qnet_mlp_swp for a net in GLOBAL memory (the h-DQN kernel's opponent from another checkpoint:
-// four nets exceed one CU's LDS, so the opponent's two are read from L2). The same MFMA / ReLU
-// schedule, but its 66 weight fragments come from the net's FRAGMENT-MAJOR copy
-// (mg_qnet_fragments: fragment s = the 64 lanes' 16 bytes, contiguous, 1 KB) through a buffer
-// resource, in a prefetch ring kQGlobalAhead fragments deep across the whole forward. Read in the
-// packed (LDS) layout, a fragment load touched 32 rows 464 B apart -- 32 cache lines per wave
-// instruction, which the vector L1 processes a line at a time; fragment-major it is 8 lines.
-// Fragments in the order the MFMAs consume them: W1(0); for tile mt = 0..5 W1(mt + 1) then
-// W2(mt, j = 0..7); the last tile's pairs interleaved with layer 3 (qnet_mlp_swp's tail).
-constexpr int kQGlobalAhead = 3;
-constexpr int kQFrags = 66;
-constexpr int kQFragBytes = kQFrags * 1024;  // mg_qnet_fragment_bytes()
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t qnet_rsrc(const uint8_t* frags) {
-  // gfx9 buffer descriptor word 3 (raw untyped dword access), num_records = the fragment copy
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(frags), static_cast<short>(0), kQFragBytes,
-                                           0x00020000);
+// the 32x32 forward of a net whose 32x32 layout is in LDS, from the block's observation tile
+__device__ __forceinline__ void qnet32_forward(const uint8_t* net32, const float* tile, int row0, bool swap,
+                                               float (&q)[8]) {
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  qnet32_mlp(net32, qnet_input(tile + (row0 + r) * kObs, swap, h), qnet_input(tile + (row0 + 32 + r) * kObs, swap, h), q);
 }
 
-// byte offset of fragment s (consumption order) for lane (r, h): a lane part and a constant part
-__device__ __forceinline__ void qnet_frag_offset(int s, int r, int h, int& lane_b, int& const_b) {
-  auto w1 = [&](int mt) {
-    if (32 * mt + 31 < kQR1) {
-      lane_b = (r * kQS1 + 8 * h) * 2;
-      const_b = 32 * mt * kQS1 * 2;
-    } else {
-      lane_b = (qrow1(32 * mt + r) * kQS1 + 8 * h) * 2;
-      const_b = 0;
-    }
-  };
-  auto w2 = [&](int mt, int j) {
-    const int m2 = j >> 1, kb = 2 * mt + (j & 1);
-    if (32 * m2 + 31 < kQR2) {
-      lane_b = (r * kQS2 + 8 * h) * 2;
-      const_b = kQOffW2 + 32 * m2 * kQS2 * 2 + 32 * kb;
-    } else {
-      lane_b = (qrow2(32 * m2 + r) * kQS2 + 8 * h) * 2;
-      const_b = kQOffW2 + 32 * kb;
-    }
-  };
-  if (s == 0) {
-    w1(0);
-  } else if (s <= 54) {
-    const int u = s - 1, mt = u / 9, v = u % 9;
-    if (v == 0)
-      w1(mt + 1);
-    else
-      w2(mt, v - 1);
-  } else {
-    // the last tile's pairs interleaved with layer 3 (qnet_mlp_swp's tail): W2(6, 0), W2(6, 2),
-    // W3(0), W3(1), W2(6, 4), W3(2), W3(3), W2(6, 6), W3(4), W3(5), W3(6)
-    const int u = s - 55;
-    const int pair = u == 0 ? 0 : u == 1 ? 1 : u == 4 ? 2 : u == 7 ? 3 : -1;
-    if (pair >= 0) {
-      w2(kQH1 / 32 - 1, 2 * pair);
-    } else {
-      const int kb = u == 2 ? 0 : u == 3 ? 1 : u == 5 ? 2 : u == 6 ? 3 : u - 4;
-      lane_b = (qrow3(r) * kQS3 + 8 * h) * 2;
-      const_b = kQOffW3 + 32 * kb;
-    }
-  }
-}
-
-// fragment s of a fragment-major net for this lane: 16 contiguous bytes per lane, the fragment's
-// 1 KB offset in soffset. (A ring over the LDS nets, 2 to 4 deep, measured within +-1 % of
-// qnet_mlp_swp's one-ahead loads on every Q-net leg, r03: not used there.)
-struct QSrcFrag {
-  __amdgpu_buffer_rsrc_t rs;
-  __device__ __forceinline__ bf16x8 operator()(int s, int lane) const {
-    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * lane, 1024 * s, 0));
-  }
-};
-
-// the fragment-major copy of a packed net: block s, lane l <- fragment s of lane l
+// mg_qnet_fragments: the packed layout is fragment-major itself since ABI 19, so the "fragment
+// copy" the h-DQN opponent is read from is a plain copy (kept so the ABI-18 callers run unchanged)
 __global__ __launch_bounds__(64) void qnet_fragments_kernel(const uint8_t* packed, uint8_t* frags) {
-  const int s = blockIdx.x, lane = threadIdx.x;
-  int lane_b, const_b;
-  qnet_frag_offset(s, lane & 31, lane >> 5, lane_b, const_b);
-  reinterpret_cast<u32x4*>(frags + 1024 * s)[lane] = *reinterpret_cast<const u32x4*>(packed + lane_b + const_b);
-}
-
-template <int D, class Src>
-__device__ __forceinline__ void qnet_mlp_ring(const Src& src, bf16x8 xb0, bf16x8 xb1, float (&q)[8]) {
-  static_assert(kQH1 / 32 == 7 && (kQH2Real + 15) / 16 == 7 && 1 + 6 * 9 + 4 + 7 == kQFrags,
-                "qnet_frag_offset's consumption order assumes 7 hidden-1 tiles and 7 layer-3 k-blocks");
-  const int lane = threadIdx.x & 63, h = lane >> 5;
-  auto fetch = [&](int s) __attribute__((always_inline)) { return src(s, lane); };
-  bf16x8 ring[D];
-#pragma unroll
-  for (int s = 0; s < D; ++s) ring[s] = fetch(s);
-  auto take = [&](int s) __attribute__((always_inline)) {
-    const bf16x8 f = ring[s % D];
-    if (s + D < kQFrags) ring[s % D] = fetch(s + D);
-    return f;
-  };
-  f32x16 acc2a[4] = {}, acc2b[4] = {};
-  const f32x16 zero = {};
-  f32x16 c0, c1;
-  {
-    const bf16x8 a1 = take(0);
-    c0 = mfma32(a1, xb0, zero);
-    c1 = mfma32(a1, xb1, zero);
-  }
-  bf16x8 hb[4] = {relu_bf16(c0, 0), relu_bf16(c0, 1), relu_bf16(c1, 0), relu_bf16(c1, 1)};
-  auto tile_step = [&](int mt, bool more, int nk) __attribute__((always_inline)) {
-    const int s0 = 1 + 9 * mt;  // this tile's first fragment (W1(mt + 1) when more)
-    if (more) {
-      const bf16x8 a1 = take(s0);
-      c0 = mfma32(a1, xb0, zero);
-      c1 = mfma32(a1, xb1, zero);
-    }
-    uint32_t nx[16];
-    int s = more ? s0 + 1 : s0;  // the last tile starts at fragment 55 = 1 + 9 * 6
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int m2 = j >> 1, sk = j & 1;
-      if (sk >= nk) continue;
-      const bf16x8 a2 = take(s++);
-      __builtin_amdgcn_sched_barrier(0);
-      acc2a[m2] = mfma32(a2, hb[sk], acc2a[m2]);
-      acc2b[m2] = mfma32(a2, hb[2 + sk], acc2b[m2]);
-      if (more) {
-#pragma unroll
-        for (int pp = 2 * j; pp < 2 * j + 2; ++pp) {
-          const int f = pp >> 2, b = 8 * (f & 1) + 2 * (pp & 3);
-          const f32x16& c = f < 2 ? c0 : c1;
-          nx[pp] = relu_pair(c[b], c[b + 1]);
-        }
-      }
-    }
-    if (more) {
-#pragma unroll
-      for (int f = 0; f < 4; ++f)
-        hb[f] = __builtin_bit_cast(bf16x8, u32x4{nx[4 * f], nx[4 * f + 1], nx[4 * f + 2], nx[4 * f + 3]});
-    }
-  };
-  constexpr int kLast = kQH1 / 32 - 1;
-#pragma unroll
-  for (int mt = 0; mt < kLast; ++mt) tile_step(mt, true, 2);
-  // the last tile interleaved with layer 3, as in qnet_mlp_swp (fragments 55..65)
-  f32x16 acc3_0 = {}, acc3_1 = {};
-  constexpr int kK3 = (kQH2Real + 15) / 16;
-  int s = 55;
-  auto layer3 = [&](int m2) __attribute__((always_inline)) {
-#pragma unroll
-    for (int sk = 0; sk < 2; ++sk) {
-      if (2 * m2 + sk >= kK3) continue;
-      const bf16x8 a3 = take(s++);
-      acc3_0 = mfma32(a3, relu_bf16(acc2a[m2], sk), acc3_0);
-      acc3_1 = mfma32(a3, relu_bf16(acc2b[m2], sk), acc3_1);
-    }
-  };
-#pragma unroll
-  for (int m2 = 0; m2 < kQH2 / 32; ++m2) {
-    const bf16x8 a2 = take(s++);
-    __builtin_amdgcn_sched_barrier(0);
-    acc2a[m2] = mfma32(a2, hb[0], acc2a[m2]);
-    acc2b[m2] = mfma32(a2, hb[2], acc2b[m2]);
-    if (m2 > 0) layer3(m2 - 1);
-  }
-  layer3(kQH2 / 32 - 1);
-  qnet_gather_q(acc3_0, acc3_1, h, q);
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i < kQNetBytes / 16) reinterpret_cast<u32x4*>(frags)[i] = reinterpret_cast<const u32x4*>(packed)[i];
 }
 
 __device__ __forceinline__ int argmax_first(const float (&q)[8], int out_dim) {
@@ -1538,7 +1642,11 @@ __global__ __launch_bounds__(kBlock) void qnet_forward_kernel(const uint8_t* net
   }
   __syncthreads();
   float q[8];
-  qnet_forward<true>(lds_net, tile, (threadIdx.x >> 6) * 64, false, q);
+  {
+    const int lane = threadIdx.x & 63, row0 = (threadIdx.x >> 6) * 64;
+    qnet_mlp_swp(lds_net, qnet_input_wide(tile + (row0 + (lane & 31)) * 16, lane >> 5),
+                 qnet_input_wide(tile + (row0 + 32 + (lane & 31)) * 16, lane >> 5), q);
+  }
   const int64_t i = base + threadIdx.x;
   if (i < n) {
 #pragma unroll
@@ -1662,7 +1770,9 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
   constexpr int kEnvWaves = kQWsEnvWaves;
   static_assert(kTiles >= 1 && kHalf == 64 * kEnvWaves * kIlp && kHalf % 256 == 0,
                 "group = 4 Q-net waves x kTiles x 64 envs = env waves x ILP x 64 envs");
-  __shared__ __attribute__((aligned(16))) uint8_t lds_net[kQNetBytes];
+  // OPP 0 / 1: the 32x32 layout (second part of the packed buffer) and forward, see qnet32_mlp
+  constexpr bool kNet32 = OPP < 2;
+  __shared__ __attribute__((aligned(16))) uint8_t lds_net[kNet32 ? kQ32NetBytes : kQNetBytes];
   __shared__ __attribute__((aligned(16))) uint8_t lds_net2[OPP == 3 ? kQNetBytes : 16];
   __shared__ __attribute__((aligned(16))) float tile[kEnvs * kObs];
   __shared__ uint8_t greedy[2][kEnvs];
@@ -1672,7 +1782,12 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
   const bool qwave = wave < 4;
   const int ew = wave - 4;
 
-  qnet_to_lds(R.net, lds_net);
+  if constexpr (kNet32) {
+    const f32x4* src = reinterpret_cast<const f32x4*>(R.net + kQNetBytes);
+    for (int j = tid; j < kQ32NetBytes / 16; j += blockDim.x) reinterpret_cast<f32x4*>(lds_net)[j] = src[j];
+  } else {
+    qnet_to_lds(R.net, lds_net);
+  }
   if constexpr (OPP == 3) qnet_to_lds(R.opp_net, lds_net2);
   const int phases = 2 * R.num_steps + 1;
   if (qwave) {
@@ -1686,7 +1801,10 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
         for (int tt = 0; tt < kTiles; ++tt) {
           const int row0 = (p & 1) * kHalf + (4 * tt + wave) * 64;
           float q[8];
-          qnet_forward_swp(lds_net, tile, row0, false, q);
+          if constexpr (kNet32)
+            qnet32_forward(lds_net, tile, row0, false, q);
+          else
+            qnet_forward_swp(lds_net, tile, row0, false, q);
           greedy[0][row0 + lane] = static_cast<uint8_t>(argmax_first(q, R.out_dim));
           if constexpr (OPP >= 2) {  // the opponent's view state[5:] + state[:5] (main.py:199)
             qnet_forward_swp(OPP == 3 ? lds_net2 : lds_net, tile, row0, true, q);
@@ -1930,7 +2048,7 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
           const bf16x8 x0 = qnet_input(tile + (row0 + r) * kObs, true, h);
           const bf16x8 x1 = qnet_input(tile + (row0 + 32 + r) * kObs, true, h);
           if constexpr (OPP == 3)
-            qnet_mlp_ring<kQGlobalAhead>(QSrcFrag{qnet_rsrc(R.meta_op)}, x0, x1, q);  // the opponent's own Goal_DQN (:267)
+            qnet_mlp<kQGlobalAhead>(qnet_global(R.meta_op), x0, x1, q);  // the opponent's own Goal_DQN (:267)
           else
             qnet_mlp_swp(lds_meta, x0, x1, q);
           gop_star = argmax_first(q, R.num_goals);
@@ -1955,7 +2073,7 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
           const bf16x8 x0 = qnet_input_goal(tile + (row0 + r) * kObs, b_gop[row0 + r], h, true);
           const bf16x8 x1 = qnet_input_goal(tile + (row0 + 32 + r) * kObs, b_gop[row0 + 32 + r], h, true);
           if constexpr (OPP == 3)
-            qnet_mlp_ring<kQGlobalAhead>(QSrcFrag{qnet_rsrc(R.lower_op)}, x0, x1, qo);  // the opponent's own HDQN (:268)
+            qnet_mlp<kQGlobalAhead>(qnet_global(R.lower_op), x0, x1, qo);  // the opponent's own HDQN (:268)
           else
             qnet_mlp_swp(lds_lower, x0, x1, qo);
           b_aop[j] = static_cast<uint8_t>(argmax_first(qo, MG_NUM_ACTIONS));
@@ -2792,7 +2910,7 @@ int mg_rollout_random(const mg_params* params, const mg_state* state, const mg_t
   return launch_rollout(R, static_cast<hipStream_t>(stream));
 }
 
-size_t mg_qnet_packed_bytes(void) { return static_cast<size_t>(kQNetBytes); }
+size_t mg_qnet_packed_bytes(void) { return static_cast<size_t>(kQNetBytes + kQ32NetBytes); }
 
 int mg_qnet_pack(const float* fc1_w, const float* fc1_b, const float* fc2_w, const float* fc2_b,
                  const float* out_w, const float* out_b, int32_t in_dim, int32_t out_dim,
@@ -2803,20 +2921,25 @@ int mg_qnet_pack(const float* fc1_w, const float* fc1_b, const float* fc2_w, con
     return fail(hipErrorInvalidValue, "%s", "mg_qnet_pack: need 1 <= in_dim <= 13, 1 <= out_dim <= 8");
   if (reinterpret_cast<uintptr_t>(packed) & 15)
     return fail(hipErrorInvalidValue, "%s", "mg_qnet_pack: packed buffer must be 16-byte aligned");
-  const int total = kQR1 * kQS1 + kQR2 * kQS2 + kQR3 * kQS3;
+  const int total = kQFrags * 64 * 8;  // one thread per (fragment, lane, element)
   hipLaunchKernelGGL(qnet_pack_kernel, dim3((total + 255) / 256), dim3(256), 0,
                      static_cast<hipStream_t>(stream), fc1_w, fc1_b, fc2_w, fc2_b, out_w, out_b,
                      in_dim, out_dim, static_cast<uint8_t*>(packed));
+  // the 32x32 layout behind it (qnet32_mlp: the config-5 kernel without a net opponent)
+  const int total32 = kQ32R1 * kQ32S1 + kQ32R2 * kQ32S2 + kQ32R3 * kQ32S3;
+  hipLaunchKernelGGL(qnet32_pack_kernel, dim3((total32 + 255) / 256), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), fc1_w, fc1_b, fc2_w, fc2_b, out_w, out_b,
+                     in_dim, out_dim, static_cast<uint8_t*>(packed) + kQNetBytes);
   return finish_launch("mg_qnet_pack");
 }
 
-size_t mg_qnet_fragment_bytes(void) { return static_cast<size_t>(kQFragBytes); }
+size_t mg_qnet_fragment_bytes(void) { return static_cast<size_t>(kQNetBytes); }
 
 int mg_qnet_fragments(const void* packed, void* fragments, void* stream) {
   if (!packed || !fragments) return fail(hipErrorInvalidValue, "%s", "mg_qnet_fragments: NULL pointer");
   if ((reinterpret_cast<uintptr_t>(packed) | reinterpret_cast<uintptr_t>(fragments)) & 15)
     return fail(hipErrorInvalidValue, "%s", "mg_qnet_fragments: buffers must be 16-byte aligned");
-  hipLaunchKernelGGL(qnet_fragments_kernel, dim3(kQFrags), dim3(64), 0, static_cast<hipStream_t>(stream),
+  hipLaunchKernelGGL(qnet_fragments_kernel, dim3(kQNetBytes / 1024), dim3(64), 0, static_cast<hipStream_t>(stream),
                      static_cast<const uint8_t*>(packed), static_cast<uint8_t*>(fragments));
   return finish_launch("mg_qnet_fragments");
 }

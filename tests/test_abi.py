@@ -112,8 +112,11 @@ def test_argument_errors_without_gpu():
     assert rc != 0 and b"NULL" in _native.lib.mg_last_error()
     rc = _native.lib.mg_reset(None, None, None, None, 1, None)
     assert rc != 0
-    # the fragment-major copy of a packed net (ABI 18): 66 fragments of 64 lanes x 16 bytes
-    assert _native.lib.mg_qnet_fragment_bytes() == 66 * 1024
+    # a packed net (ABI 19): the 16x16 forward's fragments (56 of 64 lanes x 16 bytes + 4 of 512 B),
+    # then the 32x32 layout (W1 [204 x 24], W2 [104 x 232], W3 [9 x 136] bf16); the fragment copy
+    # is the first part
+    assert _native.lib.mg_qnet_fragment_bytes() == 56 * 1024 + 4 * 512
+    assert _native.lib.mg_qnet_packed_bytes() == 56 * 1024 + 4 * 512 + 2 * (204 * 24 + 104 * 232 + 9 * 136)
     assert _native.lib.mg_qnet_fragments(None, None, None) != 0 and b"NULL" in _native.lib.mg_last_error()
     odd = ctypes.c_void_p((1 << 20) + 8)
     assert _native.lib.mg_qnet_fragments(odd, odd, None) != 0 and b"aligned" in _native.lib.mg_last_error()

@@ -1,18 +1,14 @@
-"""mg_qnet_fragments (ABI 18): the fragment-major copy of a packed Q-net that mg_rollout_hdqn reads
-an opponent from another checkpoint in (hdqn.py:265-268). Fragment s is the 64 lanes' 16 bytes of
-the s-th MFMA operand of one forward, in the order the kernel consumes them; lane l = 32 h + r
-reads row r (clamped to the last stored row) of the row tile, columns 8 h .. 8 h + 7 of the
-16-column k-block. Restated here from the packed layout (include/merging_hip.h: W1 [204 x 24],
-W2 [104 x 232], W3 [9 x 136] bf16 rows) and compared byte for byte with the device copy."""
+"""mg_qnet_pack (ABI 19): the packed Q-net starts with the 16x16 forward's MFMA operand fragments in
+the order the kernel consumes them, each the 64 lanes' 16 bytes contiguous (include/merging_hip.h). Restated here
+in numpy from the fp32 torch weights of scripts/main.py:30-47's Net -- bf16 rounding, the three-way
+bf16 split of every bias, the 1.0 units and the k orders of the layer-2 / layer-3 operands -- and
+compared byte for byte with the device's packed net and with its fragment copy (mg_qnet_fragments,
+which the h-DQN kernel reads an opponent from another checkpoint in, hdqn.py:265-268)."""
 
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
-
-R1, S1, R2, S2, R3, S3 = 204, 24, 104, 232, 9, 136
-OFF_W2 = R1 * S1 * 2
-OFF_W3 = OFF_W2 + R2 * S2 * 2
 
 
 @pytest.fixture(scope="module")
@@ -23,38 +19,72 @@ def torch():
 
 
 def _order():
-    """(matrix, row tile or None, k-block) of fragment s = 0..65 in consumption order: W1(0);
-    per hidden tile mt = 0..5: W1(mt + 1), then W2 pairs j = 0..7 (row tile j >> 1, k-block
-    2 mt + (j & 1)); the last tile's pairs interleaved with layer 3:
-    W2(6, 0), W2(6, 2), W3(0), W3(1), W2(6, 4), W3(2), W3(3), W2(6, 6), W3(4), W3(5), W3(6)."""
+    """(kind, tile, k-block) of fragment s = 0..59: W1(0); per k-block kb = 0..5: W1(kb + 1), W2(t, kb)
+    for t = 0..6; the last k-block with layer 3: W2(0..2, 6), W3(0), W2(3..4, 6), W3(1), W2(5..6, 6),
+    W3(2), W3(3)."""
     out = [("w1", 0, 0)]
-    for mt in range(6):
-        out.append(("w1", mt + 1, 0))
-        out += [("w2", j >> 1, 2 * mt + (j & 1)) for j in range(8)]
-    tail = [("w2", 0, 12), ("w2", 1, 12), ("w3", None, 0), ("w3", None, 1), ("w2", 2, 12), ("w3", None, 2),
-            ("w3", None, 3), ("w2", 3, 12), ("w3", None, 4), ("w3", None, 5), ("w3", None, 6)]
-    return out + tail
+    for kb in range(6):
+        out.append(("w1", kb + 1, 0))
+        out += [("w2", t, kb) for t in range(7)]
+    out += [("w2", 0, 6), ("w2", 1, 6), ("w2", 2, 6), ("w3", 0, 0), ("w2", 3, 6), ("w2", 4, 6), ("w3", 0, 1),
+            ("w2", 5, 6), ("w2", 6, 6), ("w3", 0, 2), ("w3", 0, 3)]
+    return out
 
 
-def _expected(packed):
-    b = np.asarray(packed, np.uint8)
-    frags = np.zeros((66, 64, 16), np.uint8)
-    for s, (m, tile, kb) in enumerate(_order()):
-        for lane in range(64):
-            r, h = lane & 31, lane >> 5
-            if m == "w1":
-                row, base, stride, col = min(32 * tile + r, R1 - 1), 0, S1, 8 * h
-            elif m == "w2":
-                row, base, stride, col = min(32 * tile + r, R2 - 1), OFF_W2, S2, 16 * kb + 8 * h
-            else:
-                row, base, stride, col = min(r, R3 - 1), OFF_W3, S3, 16 * kb + 8 * h
-            o = base + 2 * (row * stride + col)
-            frags[s, lane] = b[o:o + 16]
-    return frags.reshape(-1)
+def _bf16_bits(x):
+    """fp32 -> bf16 bit patterns, round to nearest even (as the device's conversion)."""
+    u = np.asarray(x, np.float32).view(np.uint32).astype(np.uint64)
+    r = (u + 0x7FFF + ((u >> 16) & 1)) >> 16
+    return r.astype(np.uint16)
 
 
-@pytest.mark.parametrize("in_dim,out_dim", [(10, 3), (11, 5)])
-def test_fragment_copy_matches_the_packed_layout(torch, in_dim, out_dim):
+def _bf16(x):
+    return (_bf16_bits(x).astype(np.uint32) << 16).view(np.float32)
+
+
+def _parts(b):
+    """hi + mid + lo == b, each a bf16 value (mg_qnet_pack's bias split)."""
+    b = np.asarray(b, np.float32)
+    hi = _bf16(b)
+    r = (b - hi).astype(np.float32)
+    mid = _bf16(r)
+    return hi, mid, (r - mid).astype(np.float32)
+
+
+def _expected(sd, in_dim, out_dim):
+    w1, b1 = sd["fc1.weight"], sd["fc1.bias"]
+    w2, b2 = sd["fc2.weight"], sd["fc2.bias"]
+    w3, b3 = sd["out.weight"], sd["out.bias"]
+    W1 = np.zeros((224, 16), np.float32)  # [hidden-1 unit, input slot]
+    W1[:200, :in_dim] = w1
+    W1[:200, 13:16] = np.stack(_parts(b1), 1)
+    W1[200:203, 13] = 1.0
+    W2 = np.zeros((112, 224), np.float32)  # [hidden-2 unit, hidden-1 unit]
+    W2[:100, :200] = w2
+    W2[:100, 200:203] = np.stack(_parts(b2), 1)
+    W2[100:103, 200] = 1.0
+    W3 = np.zeros((8, 128), np.float32)  # [output, hidden-2 unit]
+    W3[:out_dim, :100] = w3
+    W3[:out_dim, 100:103] = np.stack(_parts(b3), 1)
+    lane = np.arange(64)[:, None]
+    j = np.arange(8)[None, :]
+    g = lane >> 4
+    frags = []
+    for kind, tile, kb in _order():
+        if kind == "w1":
+            vals = W1[32 * tile + (lane & 31), 8 * (lane >> 5) + j]
+        elif kind == "w2":
+            unit = 32 * kb + (j & 3) + 8 * (j >> 2) + 16 * (g & 1) + 4 * (g >> 1)
+            vals = W2[16 * tile + (lane & 15), unit]
+        else:  # rows 0..7 only: 512 B, row-group g at 128 g
+            unit = 32 * kb + 16 * (j >> 2) + 4 * g + (j & 3)
+            vals = W3[lane & 7, unit].reshape(4, 16, 8)[:, :8].reshape(32, 8)
+        frags.append(_bf16_bits(vals).reshape(-1))
+    return np.concatenate(frags).view(np.uint8)
+
+
+@pytest.mark.parametrize("in_dim,out_dim", [(10, 3), (11, 5), (10, 8), (13, 1)])
+def test_packed_layout_restated_from_the_weights(torch, in_dim, out_dim):
     from merging_gym.policy import QNet
 
     rng = np.random.default_rng(in_dim * 7 + out_dim)
@@ -63,6 +93,8 @@ def test_fragment_copy_matches_the_packed_layout(torch, in_dim, out_dim):
         sd[f"{name}.weight"] = rng.uniform(-i ** -0.5, i ** -0.5, (o, i)).astype(np.float32)
         sd[f"{name}.bias"] = rng.uniform(-i ** -0.5, i ** -0.5, o).astype(np.float32)
     net = QNet.from_state_dict(sd, device="cuda:0")
-    frags = net.fragments.cpu().numpy()
-    assert frags.shape == (66 * 1024,)
-    np.testing.assert_array_equal(frags, _expected(net.packed.cpu().numpy()))
+    packed = net.packed.cpu().numpy()
+    n16 = 56 * 1024 + 4 * 512  # then the 32x32 layout of the ego-only config-5 instances
+    assert packed.shape == (n16 + 2 * (204 * 24 + 104 * 232 + 9 * 136),)
+    np.testing.assert_array_equal(packed[:n16], _expected(sd, in_dim, out_dim))
+    np.testing.assert_array_equal(net.fragments.cpu().numpy(), packed[:n16])

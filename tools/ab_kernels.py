@@ -58,7 +58,7 @@ class Bed:
         self.coll = torch.empty(n, dtype=torch.uint8, device=dev)
         self.fobs = torch.empty((n, 10), device=dev)
         self.a = torch.empty((2, n), dtype=torch.int8, device=dev)
-        self.ep_stats = torch.zeros((n, 4), dtype=torch.float64, device=dev)  # mg_episode_stats [n]
+        self.ep_stats = torch.zeros((n, 8), dtype=torch.float64, device=dev)  # mg_episode_stats [n], 64 B each
         self.tobs = torch.empty((T, n, 10), device=dev)
         self.trew = torch.empty((T, n, 2), device=dev)
         self.tdone = torch.empty((T, n), dtype=torch.uint8, device=dev)
@@ -92,12 +92,13 @@ class Bed:
         assert rc == 0
         self.k += 1
 
-    def pack_net(self, weights):
+    def pack_net(self, weights, attr="net"):
         ts = [torch.as_tensor(weights[k]).cuda().contiguous() for k in
               ("fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias", "out.weight", "out.bias")]
-        self.net_src = ts
-        self.net = torch.empty(self.lib.mg_qnet_packed_bytes(), dtype=torch.uint8, device="cuda")
-        assert self.lib.mg_qnet_pack(*(t.data_ptr() for t in ts), 10, 5, self.net.data_ptr(), None) == 0
+        setattr(self, attr + "_src", ts)
+        net = torch.empty(self.lib.mg_qnet_packed_bytes(), dtype=torch.uint8, device="cuda")
+        assert self.lib.mg_qnet_pack(*(t.data_ptr() for t in ts), 10, 5, net.data_ptr(), None) == 0
+        setattr(self, attr, net)
 
     def qrollout(self, opp, ev=None):
         if ev:
@@ -105,7 +106,8 @@ class Bed:
         thr = 3255688812  # round(Phi(0.7) * 2^32)
         rc = self.lib.mg_rollout_qnet(ctypes.byref(self.params), ctypes.byref(self.state), ctypes.byref(self.traj),
                                       ctypes.byref(self.stats), self.n, 0, 5, self.k, self.T, self.net.data_ptr(), 5,
-                                      thr, opp, thr, None, 1, torch.cuda.current_stream().cuda_stream)
+                                      thr, opp, thr, self.opp_net.data_ptr() if opp == 3 else None, 1,
+                                      torch.cuda.current_stream().cuda_stream)
         assert rc == 0
         self.k += self.T
 
@@ -208,26 +210,29 @@ def main_qnet(a):
 
     f = np.load(os.path.join(ROOT, "tests", "golden", "dqn_checkpoints.npz"))
     w = {k.split("/", 1)[1]: f[k] for k in f.files if k.startswith("l1/")}
+    w3 = {k.split("/", 1)[1]: f[k] for k in f.files if k.startswith("l3/")}  # main.py Strategy_OP "L1"
     beds = {os.path.basename(p): Bed(bind(p), a.envs, a.T) for p in a.libs}
     for b in beds.values():
         b.pack_net(w)
+        b.pack_net(w3, "opp_net")
         for _ in range(a.warm):
             b.step()
     ev = Events(a.rollouts)
-    res = {k: {0: [], 2: []} for k in beds}
+    res = {k: {0: [], 2: [], 3: []} for k in beds}
     torch.cuda.synchronize()
     for r in range(a.rounds):
         order = list(beds) if r % 2 == 0 else list(reversed(beds))
         for name in order:
             b = beds[name]
-            for opp in (0, 2):
+            for opp in (0, 2, 3):
                 for j in range(a.rollouts):
                     b.qrollout(opp, ev.ev[j])
                 torch.cuda.synchronize()
                 res[name][opp] += [ev.ms(j) / a.T for j in range(a.rollouts)]
     for name, d in res.items():
         print(f"{name:24s} qnet(none) {1e3 * statistics.median(d[0]):7.2f} us/step   "
-              f"qnet(self) {1e3 * statistics.median(d[2]):7.2f} us/step", flush=True)
+              f"qnet(self) {1e3 * statistics.median(d[2]):7.2f} us/step   "
+              f"qnet(other) {1e3 * statistics.median(d[3]):7.2f} us/step", flush=True)
 
 
 def main_replay(a):
