@@ -92,14 +92,15 @@ class NativeError(RuntimeError):
     pass
 
 
-def _load():
-    if not os.path.exists(LIB_PATH):
+def _load(path=LIB_PATH):
+    """Bind libmerging_hip.so (or, for tools/ab_*.py, a variant build of the same ABI at `path`)."""
+    if not os.path.exists(path):
         raise ImportError(
-            f"{LIB_PATH} not found. Build the HIP library first: "
+            f"{path} not found. Build the HIP library first: "
             "python -c 'import __graft_entry__ as g; g.build()' (hipcc --offload-arch=gfx950)")
     import torch  # noqa: F401  -- load torch's libamdhip64 first so the library binds to it
 
-    lib = _c.CDLL(LIB_PATH)
+    lib = _c.CDLL(path)
     lib.mg_abi_version.restype = _c.c_int
     lib.mg_last_error.restype = _c.c_char_p
     lib.mg_params_default.argtypes = [_c.POINTER(Params)]
@@ -140,7 +141,7 @@ def _load():
         f.restype = _c.c_int
     v = lib.mg_abi_version()
     if v != ABI_VERSION:
-        raise ImportError(f"{LIB_PATH}: ABI version {v}, expected {ABI_VERSION} (stale build?)")
+        raise ImportError(f"{path}: ABI version {v}, expected {ABI_VERSION} (stale build?)")
     return lib
 
 

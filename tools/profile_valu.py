@@ -33,21 +33,23 @@ for j in range(8):
 rng = np.random.default_rng(0)
 
 
-def net(i, o):
+def signed(i, o):
+    """bench.py's h-DQN nets: torch.nn.Linear's signed default initialisation (hdqn.py:41-47's
+    uniform(0, 1) weights pick one action for > 90 % of inputs, tests/test_hdqn_test_nets.py)"""
     sd = {}
     for name, (a, b) in zip(("fc1", "fc2", "out"), [(200, i), (100, 200), (o, 100)]):
-        sd[f"{name}.weight"] = rng.uniform(0, 1, (a, b)).astype(np.float32)
+        sd[f"{name}.weight"] = rng.uniform(-b ** -0.5, b ** -0.5, (a, b)).astype(np.float32)
         sd[f"{name}.bias"] = rng.uniform(-b ** -0.5, b ** -0.5, a).astype(np.float32)
     return QNet.from_state_dict(sd, device="cuda:0")
 
 
-meta, lower = net(10, 3), net(11, 5)
+meta, lower = signed(10, 3), signed(11, 5)
 for j in range(8):
     env.rollout_hdqn(16, meta, lower, 7, first_step=k, final_observation=False)
     k += 16
 # round 3: the other opponents of both fused policies (8 launches each): config 5 with the same net
 # on the swapped observation and with another checkpoint (l3); h-DQN self-play and another
-# checkpoint's nets (signed draws, bench.py's nets)
+# checkpoint's nets
 if os.environ.get("MG_PROFILE_ALL_OPPONENTS", "1") != "0":
     qnet3 = QNet.from_state_dict({kk.split("/", 1)[1]: f[kk] for kk in f.files if kk.startswith("l3/")}, device="cuda:0")
     for opp in ("self", qnet3):
@@ -55,14 +57,6 @@ if os.environ.get("MG_PROFILE_ALL_OPPONENTS", "1") != "0":
             env.rollout_qnet(16, qnet, 7, opponent=opp, first_step=k, final_observation=False, won_mask=False)
             k += 16
 
-    def signed(i, o):
-        sd = {}
-        for name, (a, b) in zip(("fc1", "fc2", "out"), [(200, i), (100, 200), (o, 100)]):
-            sd[f"{name}.weight"] = rng.uniform(-b ** -0.5, b ** -0.5, (a, b)).astype(np.float32)
-            sd[f"{name}.bias"] = rng.uniform(-b ** -0.5, b ** -0.5, a).astype(np.float32)
-        return QNet.from_state_dict(sd, device="cuda:0")
-
-    meta, lower = signed(10, 3), signed(11, 5)
     for opp in ("self", (signed(10, 3), signed(11, 5))):
         env.hdqn_goal_op = None
         for j in range(8):
