@@ -78,6 +78,60 @@ __global__ __launch_bounds__(kBlock) void twin(Arrays A, int64_t n, uint32_t k) 
   for (int j = tid; j < n4; j += kBlock) st<NT>(d4 + j, s4[j]);
 }
 
+// twin_aos: the same bytes with the six f64 state values of an env as one 48-byte record
+// (p1, v1, p2, v2, r1, r2), read and written by each wave as 3 KB of consecutive bytes: lane l
+// moves 16-byte piece l + 64 j (j = 0..2) of the wave's 64 records through LDS (3 dwordx4 loads
+// and stores per lane, one sequential stream instead of six strided ones). tf stays a u16 array.
+template <bool NT>
+__global__ __launch_bounds__(kBlock) void twin_aos(double* rec, Arrays A, int64_t n, uint32_t k) {
+  __shared__ __attribute__((aligned(16))) float tile[kBlock * kObs];
+  __shared__ __attribute__((aligned(16))) double srec[kBlock * 6];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kBlock, i = base + tid;
+  const int64_t wbase = base + 64 * w;
+  f32x4* g4 = reinterpret_cast<f32x4*>(rec + wbase * 6);
+  f32x4* l4 = reinterpret_cast<f32x4*>(srec + 64 * w * 6);
+  const bool full = wbase + 64 <= n;
+  if (full) {
+    const f32x4 x0 = g4[lane], x1 = g4[lane + 64], x2 = g4[lane + 128];
+    l4[lane] = x0; l4[lane + 64] = x1; l4[lane + 128] = x2;
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  float o[kObs];
+  double* r = srec + tid * 6;
+  double p1 = r[0], v1 = r[1], p2 = r[2], v2 = r[3], r1 = r[4], r2 = r[5];
+  uint16_t tf = i < n ? A.tf[i] : 0;
+  const uint32_t h = (static_cast<uint32_t>(i) * 2654435761u) ^ k;
+  const int a1 = h % 5, a2 = (h >> 8) % 5;
+  v1 += 0.2 * a1; v2 += 0.2 * a2; p1 += v1; p2 += v2; r1 += 0.5; r2 -= 0.5;
+  const bool done = (tf & 0x1FFF) > 2500;
+  tf = done ? 0 : static_cast<uint16_t>(tf + 1);
+  for (int j = 0; j < kObs; ++j) o[j] = static_cast<float>(j & 1 ? p1 - p2 : v1 + j);
+  if (i < n) {
+    st<NT>(reinterpret_cast<f32x2*>(A.rew) + i, f32x2{static_cast<float>(r1), static_cast<float>(r2)});
+    st<NT>(reinterpret_cast<uint32_t*>(A.a1) + i, static_cast<uint32_t>(a1) | (a2 << 8) |
+                                                      (static_cast<uint32_t>(done) << 16) |
+                                                      (static_cast<uint32_t>(p1 == p2) << 24));
+    A.tf[i] = tf;
+  }
+  r[0] = p1; r[1] = v1; r[2] = p2; r[3] = v2; r[4] = r1; r[5] = r2;
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  if (full) {
+    g4[lane] = l4[lane]; g4[lane + 64] = l4[lane + 64]; g4[lane + 128] = l4[lane + 128];
+  }
+  float2* t2 = reinterpret_cast<float2*>(tile + tid * kObs);
+  for (int j = 0; j < kObs / 2; ++j) t2[j] = make_float2(o[2 * j], o[2 * j + 1]);
+  __syncthreads();
+  const int64_t rem = n - base;
+  const int nrows = rem < kBlock ? static_cast<int>(rem) : kBlock;
+  const int n4 = nrows * kObs / 4;
+  f32x4* d4 = reinterpret_cast<f32x4*>(A.obs + base * kObs);
+  const f32x4* s4 = reinterpret_cast<const f32x4*>(tile);
+  for (int j = tid; j < n4; j += kBlock) st<NT>(d4 + j, s4[j]);
+}
+
 // Reads nr float4 and writes nw float4 per "unit"; units spread over a grid-stride loop.
 __global__ __launch_bounds__(256) void mix(const f32x4* __restrict__ src, f32x4* __restrict__ dst,
                                            int64_t nr4, int64_t nw4) {
@@ -117,6 +171,8 @@ int main(int argc, char** argv) {
   alloc(A.p1, n * 8); alloc(A.v1, n * 8); alloc(A.p2, n * 8); alloc(A.v2, n * 8);
   alloc(A.r1, n * 8); alloc(A.r2, n * 8); alloc(A.tf, n * 2); alloc(A.a1, n * 4); alloc(A.a2, n);
   alloc(A.rew, n * 8); alloc(A.done, n); alloc(A.coll, n); alloc(A.obs, n * 40);
+  double* rec;
+  alloc(rec, n * 48);
   const double bytes = 152.0 * n;
   const unsigned grid = static_cast<unsigned>((n + kBlock - 1) / kBlock);
   for (int rep = 0; rep < 2; ++rep) {
@@ -126,6 +182,8 @@ int main(int argc, char** argv) {
     std::printf("twin_p (NT, packed u32 bytes): %8.2f us  %6.3f TB/s\n", us, bytes / us / 1e6);
     us = time_us([&](int r) { hipLaunchKernelGGL((twin<false, false>), dim3(grid), dim3(kBlock), 0, 0, A, n, r); }, reps);
     std::printf("twin_s (plain)               : %8.2f us  %6.3f TB/s\n", us, bytes / us / 1e6);
+    us = time_us([&](int r) { hipLaunchKernelGGL((twin_aos<true>), dim3(grid), dim3(kBlock), 0, 0, rec, A, n, r); }, reps);
+    std::printf("twin_aos (48-B state records): %8.2f us  %6.3f TB/s\n", us, bytes / us / 1e6);
   }
   float us;
 
