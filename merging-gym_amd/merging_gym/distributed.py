@@ -49,19 +49,27 @@ def gather_episode_stats(returns, counts, group=None):
     import torch.distributed as dist
 
     packed = pack_stats(returns, counts)
-    world = dist.get_world_size(group)
-    if world == 1:
+    if dist.get_world_size(group) == 1:
         return unpack_stats(packed, returns.shape[1])
+    return unpack_stats(all_gather_rows(packed, group).to(packed.device), returns.shape[1])
+
+
+def all_gather_rows(rows, group=None):
+    """[k, w] int64 on every rank -> [world * k, w] in rank order: one all_gather_into_tensor of the
+    device tensor over RCCL (backend "nccl"), or gloo's list form on host memory. Used at any
+    world size (tests run it on a one-rank RCCL group: the device branch a sharded run takes)."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
     if dist.get_backend(group) == "nccl":
-        out = torch.empty((world * packed.shape[0], packed.shape[1]), dtype=packed.dtype,
-                          device=packed.device)
-        dist.all_gather_into_tensor(out, packed, group=group)
-    else:  # gloo: list form, on host memory
-        host = packed.cpu()
-        parts = [torch.empty_like(host) for _ in range(world)]
-        dist.all_gather(parts, host, group=group)
-        out = torch.cat(parts).to(packed.device)
-    return unpack_stats(out, returns.shape[1])
+        out = torch.empty((world * rows.shape[0], rows.shape[1]), dtype=rows.dtype, device=rows.device)
+        dist.all_gather_into_tensor(out, rows.contiguous(), group=group)
+        return out
+    host = rows.cpu()
+    parts = [torch.empty_like(host) for _ in range(world)]
+    dist.all_gather(parts, host, group=group)
+    return torch.cat(parts)
 
 
 NUM_RETURNS, NUM_COUNTS = 3, 6
@@ -124,14 +132,7 @@ def gather_episode_summary(returns, counts, group=None, timings=None):
         timings["allgather_ms"] = None
     if world == 1:
         return summarize_partials(part)
-    if dist.get_backend(group) == "nccl":
-        out = torch.empty((world, part.numel()), dtype=torch.int64, device=part.device)
-        dist.all_gather_into_tensor(out, part, group=group)
-    else:  # gloo: host tensors
-        host = part.cpu()
-        rows = [torch.empty_like(host) for _ in range(world)]
-        dist.all_gather(rows, host, group=group)
-        out = torch.stack(rows)
+    out = all_gather_rows(part.reshape(1, -1), group)
     sync()
     if timings is not None:
         timings["allgather_ms"] = (time.perf_counter() - t1) * 1e3

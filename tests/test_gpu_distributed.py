@@ -56,3 +56,23 @@ def test_two_rank_shards_equal_unsharded_run(tmp_path):
     assert exp["completed"] > 0 and got["summary"]["completed"] == exp["completed"]
     for key, v in exp.items():
         assert abs(got["summary"][key] - v) <= 1e-12 * max(1.0, abs(v)), key
+
+
+def test_rccl_device_gather(tmp_path):
+    """The RCCL branch of the statistics gather (distributed.all_gather_rows, backend "nccl"):
+    all_gather_into_tensor of the 72-byte partial totals and of the per-env rows, on device
+    tensors, in a one-rank RCCL group on the test box's one GPU (RCCL refuses two ranks on one
+    device; the 8-GPU runs are the driver's). What comes back must equal what went in, bit for bit."""
+    import torch
+
+    out = str(tmp_path / "rccl.pt")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "tests", "dist_rccl_worker.py"), "4099", "160", "17", out]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    run = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert run.returncode == 0, run.stderr[-3000:]
+    got = torch.load(out, weights_only=True)
+    assert got["got_part"].shape == (1, 9) and torch.equal(got["got_part"][0], got["part"])
+    assert torch.equal(got["got_rows"], got["rows"]) and got["rows"].shape == (4099, 6)
+    assert int(got["part"][3]) > 0  # episodes completed inside the run
