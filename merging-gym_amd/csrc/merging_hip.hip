@@ -1751,10 +1751,11 @@ __device__ __forceinline__ bool qnet_load_env(const QRollout& R, int64_t i, Env&
 // Greedy actions go to the env waves through LDS; the new observations come back through the
 // tile rows. Each env-wave lane holds the two envs (one per group) it steps.
 // OPP 3 (main.py's default Strategy_OP "L1", :161-168: the opponent is another trained DQN)
-// keeps a second packed net in LDS; the two nets and a 1,024-env tile would pass the CU's 160 KB,
-// so that instance runs ILP 1: 512-env blocks, one env per env-wave lane.
+// keeps a second net in LDS: with the 16x16 layouts (2 x 59,392 B, ABI 19) the two nets, the
+// 1,024-env tile and the greedy bytes take 161,792 B, so it runs ILP 2 like the others (the
+// 32x32 layouts, 2 x 60,496 B, did not fit and ran ILP 1 on 512-env blocks: 1 % slower).
 template <int OPP>
-constexpr int qws_ilp() { return OPP == 3 ? 1 : kQWsIlp; }
+constexpr int qws_ilp() { return kQWsIlp; }
 template <int OPP>
 constexpr int qws_envs() { return 2 * 64 * kQWsEnvWaves * qws_ilp<OPP>(); }
 
