@@ -2,7 +2,7 @@
 the order the kernel consumes them, each the 64 lanes' 16 bytes contiguous (include/merging_hip.h). Restated here
 in numpy from the fp32 torch weights of scripts/main.py:30-47's Net -- bf16 rounding, the three-way
 bf16 split of every bias, the 1.0 units and the k orders of the layer-2 / layer-3 operands -- and
-compared byte for byte with the device's packed net and with its fragment copy (mg_qnet_fragments,
+compared byte for byte with the device's packed net (both layouts) and with its fragment copy (mg_qnet_fragments,
 which the h-DQN kernel reads an opponent from another checkpoint in, hdqn.py:265-268)."""
 
 import numpy as np
@@ -83,6 +83,36 @@ def _expected(sd, in_dim, out_dim):
     return np.concatenate(frags).view(np.uint8)
 
 
+def _expected32(sd, in_dim, out_dim):
+    """The 32x32 layout after the fragments (the ego-only config-5 instances): W1 [204 x 24], W2
+    [104 x 232], W3 [9 x 136] bf16 rows; W2 / W3 columns in the 32x32 accumulator's k order
+    (16-column blocks, k -> unit 8 ((k & 7) >> 2) + 4 (k >> 3) + (k & 3)); rows past the last one
+    that can be non-zero are not stored."""
+    w1, b1 = sd["fc1.weight"], sd["fc1.bias"]
+    w2, b2 = sd["fc2.weight"], sd["fc2.bias"]
+    w3, b3 = sd["out.weight"], sd["out.bias"]
+    W1 = np.zeros((204, 24), np.float32)
+    W1[:200, :in_dim] = w1
+    W1[:200, 13:16] = np.stack(_parts(b1), 1)
+    W1[200:203, 13] = 1.0
+    H1 = np.zeros((104, 224), np.float32)  # [hidden-2 unit, hidden-1 unit]
+    H1[:100, :200] = w2
+    H1[:100, 200:203] = np.stack(_parts(b2), 1)
+    H1[100:103, 200] = 1.0
+    H2 = np.zeros((9, 128), np.float32)  # [output, hidden-2 unit]
+    H2[:out_dim, :100] = w3
+    H2[:out_dim, 100:103] = np.stack(_parts(b3), 1)
+    c = np.arange(232)
+    kk = c % 16
+    src = 16 * (c // 16) + 8 * ((kk & 7) >> 2) + 4 * (kk >> 3) + (kk & 3)
+    W2 = np.where(c[None, :] < 224, H1[:, np.minimum(src, 223)], 0.0).astype(np.float32)
+    c3 = np.arange(136)
+    kk3 = c3 % 16
+    src3 = 16 * (c3 // 16) + 8 * ((kk3 & 7) >> 2) + 4 * (kk3 >> 3) + (kk3 & 3)
+    W3 = np.where(c3[None, :] < 128, H2[:, np.minimum(src3, 127)], 0.0).astype(np.float32)
+    return np.concatenate([_bf16_bits(m).reshape(-1) for m in (W1, W2, W3)]).view(np.uint8)
+
+
 @pytest.mark.parametrize("in_dim,out_dim", [(10, 3), (11, 5), (10, 8), (13, 1)])
 def test_packed_layout_restated_from_the_weights(torch, in_dim, out_dim):
     from merging_gym.policy import QNet
@@ -97,4 +127,5 @@ def test_packed_layout_restated_from_the_weights(torch, in_dim, out_dim):
     n16 = 56 * 1024 + 4 * 512  # then the 32x32 layout of the ego-only config-5 instances
     assert packed.shape == (n16 + 2 * (204 * 24 + 104 * 232 + 9 * 136),)
     np.testing.assert_array_equal(packed[:n16], _expected(sd, in_dim, out_dim))
+    np.testing.assert_array_equal(packed[n16:], _expected32(sd, in_dim, out_dim))
     np.testing.assert_array_equal(net.fragments.cpu().numpy(), packed[:n16])
