@@ -1,7 +1,9 @@
-// Cycles per Q-net forward (qnet_forward_swp, the config-5 kernel's Q-net wave code) with one or
-// two Q-net waves per SIMD and nothing else on the CU, against the 132 x 32 = 4,224 matrix-pipe
-// cycles of its MFMAs. s_memtime around `iters` forwards per wave; weights and a 64-env
-// observation tile per wave in LDS, as in the kernel.
+// Cycles per Q-net forward (qnet_forward_swp: since ABI 19 the 16x16x32 forward, 14 x 32 + 212 x 16
+// = 3,840 matrix-pipe cycles; built against the ABI-18 source it is the 32x32 forward, 132 x 32 =
+// 4,224) with one or two Q-net waves per SIMD and nothing else on the CU. The "mfma_tflops" and
+// "mfma_cycles_per_forward" fields count the 32x32 forward's 4,224 cycles of work for both, so
+// compare wall times. s_memtime around `iters` forwards per wave; weights and a 64-env observation
+// tile per wave in LDS, as in the kernel.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -I include \
 //         -o tools/micro/qfwd_probe tools/micro/qfwd_probe.hip && tools/micro/qfwd_probe
 #include "../../merging-gym_amd/csrc/merging_hip.hip"
