@@ -33,17 +33,24 @@ def main():
     ap.add_argument("--T", type=int, default=16)
     a = ap.parse_args()
     libs = {os.path.basename(p): _native._load(p) for p in a.libs}
-    rng = np.random.default_rng(0)
+    rng = None
 
     def net(i, o):  # bench.py's hdqn_leg nets: torch.nn.Linear's signed default initialisation
+        nonlocal rng
         sd = {}
         for name, (r, c) in zip(("fc1", "fc2", "out"), [(200, i), (100, 200), (o, 100)]):
             sd[f"{name}.weight"] = rng.uniform(-c ** -0.5, c ** -0.5, (r, c)).astype(np.float32)
             sd[f"{name}.bias"] = rng.uniform(-c ** -0.5, c ** -0.5, r).astype(np.float32)
         return QNet.from_state_dict(sd, device="cuda")
 
-    meta, lower, meta_op, lower_op = net(10, NUM_GOALS), net(11, 5), net(10, NUM_GOALS), net(11, 5)
-    legs = {"hdqn_L0": "none", "hdqn_self": "self", "hdqn_other": (meta_op, lower_op)}
+    # every variant packs its own copies of the same nets (the packed layout may differ between them)
+    nets = {}
+    for name, lib in libs.items():
+        _native.lib = lib
+        rng = np.random.default_rng(0)
+        meta, lower, meta_op, lower_op = net(10, NUM_GOALS), net(11, 5), net(10, NUM_GOALS), net(11, 5)
+        nets[name] = (meta, lower, {"hdqn_L0": "none", "hdqn_self": "self", "hdqn_other": (meta_op, lower_op)})
+    legs = ("hdqn_L0", "hdqn_self", "hdqn_other")
     env = MergeVecEnv(a.envs, device="cuda", final_observation=False)
     k = 1_000_000
     for _ in range(200):
@@ -54,10 +61,11 @@ def main():
     for r in range(a.rounds + 1):  # round 0 warms every variant up and is not kept
         for name in (list(libs) if r % 2 == 0 else list(reversed(libs))):
             _native.lib = libs[name]
-            for leg, opp in legs.items():
+            meta, lower, opps = nets[name]
+            for leg in legs:
                 for j in range(a.launches):
                     ev[j][0].record()
-                    env.rollout_hdqn(a.T, meta, lower, 11, opponent=opp, first_step=k, final_observation=False)
+                    env.rollout_hdqn(a.T, meta, lower, 11, opponent=opps[leg], first_step=k, final_observation=False)
                     ev[j][1].record()
                     k += a.T
                 torch.cuda.synchronize()
