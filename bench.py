@@ -573,12 +573,14 @@ def replay_leg(env, args, torch):
 
 def dropin_leg(seed: int):
     """BASELINE config 1: merging_gym.make('merging-v0') single env, 500 step() calls with
-    uniform random actions for both players, reset on done. The GPU-backed drop-in (one
-    launch + one stream sync per step: the kernel reads the actions from and writes its
-    168-byte record to pinned host memory) is timed next to the pure-Python restatement of
-    the reference's step (oracle.PyMergeEnv, numpy sin/cos + the QP solved per car-step) on
-    the same action sequence; the reference itself measured 5,090 steps/s in the survey
-    container."""
+    uniform random actions for both players, reset on done. Three steps on the same action
+    sequence: the drop-in's default host backend (mg_host_step: the kernels' own step functions
+    compiled for the CPU, one ctypes call per step), its GPU backend (a batch of one env in the
+    step kernel: one launch + one stream sync per step, the kernel reading the actions from and
+    writing its 168-byte record to pinned host memory), and the pure-Python restatement of the
+    reference's step (oracle.PyMergeEnv, numpy sin/cos + the QP solved per car-step) -- the
+    reference itself measured 5,090 steps/s in the survey container. The
+    host and GPU backends must return the same values (checked here on every step)."""
     import numpy as np
 
     import merging_gym
@@ -588,20 +590,26 @@ def dropin_leg(seed: int):
 
     rng = np.random.default_rng(seed)
     acts = rng.integers(0, 5, (500, 2)).tolist()
-    out = {}
-    for name, env in (("gpu_dropin", merging_gym.make("merging-v0")), ("cpu_python_port", merge_oracle.PyMergeEnv())):
+    out, trace = {}, {}
+    for name, env in (("host_dropin", merging_gym.make("merging-v0")),
+                      ("gpu_dropin", merging_gym.make("merging-v0", backend="gpu")),
+                      ("cpu_python_port", merge_oracle.PyMergeEnv())):
         env.reset()
         env.step(0, 0)
         env.reset()
-        episodes = 0
+        episodes, rows = 0, []
         t0 = time.perf_counter()
         for a1, a2 in acts:
-            _, _, done, _ = env.step(a1, a2)
-            if done:
+            row = env.step(a1, a2)
+            rows.append(row)
+            if row[2]:
                 env.reset()
                 episodes += 1
         dt = time.perf_counter() - t0
+        trace[name] = rows
         out[name] = {"steps_per_s": 500 / dt, "us_per_step": dt / 500 * 1e6, "episodes_finished": episodes}
+    out["host_equals_gpu"] = trace["host_dropin"] == trace["gpu_dropin"]
+    out["default_backend"] = merging_gym.make("merging-v0").backend
     out["workload"] = "config 1: one env, 500 random-action step() calls, reset on done (list API)"
     return out
 

@@ -30,12 +30,17 @@
  *   mg_qnet_pack / mg_qnet_forward / mg_qnet_packed_bytes / mg_qnet_fragments /
  *   mg_qnet_fragment_bytes: the Q-net Net (main.py:30-47,
  *                     hdqn.py:38-55) in the kernel's packed bf16 layout, and its forward pass
+ *   mg_host_step / mg_host_reset / mg_host_observe (ABI 20): mg_step / mg_reset / mg_observe on
+ *                     HOST memory, for the single env of BASELINE config 1 (the reference's CPU
+ *                     MergeEnv, merging_env.py:118-230, driven one step at a time by
+ *                     scripts/human_player.py:112-187 and the scripts' list API)
  *   mg_abi_version, mg_last_error, mg_params_default, mg_time_next_launch: library plumbing
  *                     and profiling (no reference twin).
  *
  * Conventions
  *   - Every pointer inside mg_state / mg_outputs / mg_stats / action arrays is a DEVICE
- *     pointer owned by the caller. The library never allocates, frees or synchronises.
+ *     pointer owned by the caller (HOST pointers for the mg_host_* entry points). The library
+ *     never allocates, frees or synchronises.
  *   - Calls are stream-ordered on `stream` (a hipStream_t, NULL = default stream) and
  *     return immediately. Return value: 0 on success, otherwise a hipError_t value
  *     (as int) and mg_last_error() describes it (thread-local). No exception crosses
@@ -53,7 +58,7 @@
 extern "C" {
 #endif
 
-#define MG_ABI_VERSION 19
+#define MG_ABI_VERSION 20
 #define MG_OBS_DIM 10   /* merging_env.py:75 observation_shape = (10) */
 #define MG_NUM_ACTIONS 5 /* merging_env.py:101-102 action_dict / Discrete(5) */
 #define MG_ACTION_NONE (-1) /* action2=None: the constant-speed "L0" opponent, merging_env.py:152 */
@@ -440,6 +445,21 @@ int mg_reset(const mg_params* params, const mg_state* state, const uint8_t* mask
  * and MergeEnv.is_collided (:198-206). */
 int mg_observe(const mg_params* params, const mg_state* state, const mg_outputs* out, int64_t n,
                void* stream);
+
+/* ---- host (CPU) path, ABI 20 ---------------------------------------------------------------------
+ * The same step, reset and observation functions the kernels run, compiled for the host and applied
+ * to HOST pointers, synchronously, one env after another: every output and condition is exactly
+ * mg_step's / mg_reset's / mg_observe's (done_mask / won_mask words per 64 envs included), and the
+ * doubles are the kernel's bit for bit (the host build has no contraction either; sin / cos for
+ * |theta| >= 1/16, off every live-episode state, are glibc's there). For one env at the scripts'
+ * pace (merging_env.py:138-230 called per step, scripts/human_player.py:112-187) a step costs
+ * ~1 us here against a kernel launch plus a stream synchronisation on the GPU; batches belong on
+ * the device (mg_step and the rollout kernels). */
+int mg_host_step(const mg_params* params, const mg_state* state, const int8_t* a1, const int8_t* a2,
+                 const mg_outputs* out, const mg_stats* stats, int64_t n, uint32_t flags);
+int mg_host_reset(const mg_params* params, const mg_state* state, const uint8_t* mask,
+                  const mg_outputs* out, int64_t n);
+int mg_host_observe(const mg_params* params, const mg_state* state, const mg_outputs* out, int64_t n);
 
 #ifdef __cplusplus
 }

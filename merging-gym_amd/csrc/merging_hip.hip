@@ -37,6 +37,13 @@ namespace {
 constexpr int kBlock = 256;  // 4 waves of 64 (128 and 512 measured within 0.8 %)
 constexpr int kObs = MG_OBS_DIM;
 
+// The step's functions compile for the host as well: the CPU single-env path (mg_host_step,
+// BASELINE config 1, scripts/human_player.py's 20 Hz loop on a machine without a GPU) runs this
+// same code. The host side is built with the same -ffp-contract=off, and fma / fabs / sqrt are
+// correctly rounded there too, so host and device give the same doubles; only the cold sin/cos
+// branch (|theta| >= 1/16, off every live-episode state) uses glibc on the host.
+#define MG_HD __host__ __device__ __forceinline__
+
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -49,19 +56,19 @@ __device__ __forceinline__ void st_out(T* p, T v) {
 }
 
 template <class T>
-__device__ __forceinline__ void st_state(T* p, T v) {
+MG_HD void st_state(T* p, T v) {
   *p = v;
 }
 
 // Action codes after host/device decoding: 0..4 valid, -1 None (opponent only), anything
 // else is the reference's KeyError.
-__device__ __forceinline__ bool valid_action(int a) { return a >= 0 && a < MG_NUM_ACTIONS; }
+MG_HD bool valid_action(int a) { return a >= 0 && a < MG_NUM_ACTIONS; }
 
 // x / d for a divisor fixed per launch, correctly rounded: q = x * (1/d), then Markstein's
 // FMA correction. With inv = RN(1/d) this returns RN(x / d) for d = 3 and d = 30000 (the
 // only divisors used; 0 mismatches in 8e8 random tests, incl. random exponents,
 // tests/test_division.py) at 3 instructions instead of the ~10 of a general fp64 division.
-__device__ __forceinline__ double div_const(double x, double d, double inv) {
+MG_HD double div_const(double x, double d, double inv) {
   const double q = x * inv;
   const double r = fma(-q, d, x);
   return fma(r, inv, q);
@@ -75,12 +82,12 @@ __device__ __forceinline__ double div_const(double x, double d, double inv) {
 // The device library's sincos for |t| >= 1/16 (only reached off the live-episode range, e.g.
 // stepping far past done). Kept out of line: inlined, the compiler hoists its polynomial
 // constants into VGPRs for the whole step loop of the T-step kernels, which then spill.
-__device__ __attribute__((noinline)) void sincos_cold(double t, double* s, double* c) {
+__device__ __attribute__((noinline, unused)) void sincos_cold(double t, double* s, double* c) {
   sincos(t, s, c);
 }
 
 // the polynomial branch (|t| < 1/16)
-__device__ __forceinline__ void sincos_poly(double t, double& s, double& c) {
+MG_HD void sincos_poly(double t, double& s, double& c) {
   const double t2 = t * t;
   const double ps = fma(t2, fma(t2, fma(t2, 2.7557319223985893e-06, -1.9841269841269841e-04),
                                 8.3333333333333332e-03),
@@ -94,12 +101,17 @@ __device__ __forceinline__ void sincos_poly(double t, double& s, double& c) {
   c = fma(t2, pc, 1.0);
 }
 
-__device__ __forceinline__ void arc_sincos(double t, double& s, double& c) {
+MG_HD void arc_sincos(double t, double& s, double& c) {
   if (fabs(t) < 0.0625) {
     sincos_poly(t, s, c);
     return;
   }
+#if defined(__HIP_DEVICE_COMPILE__)
   sincos_cold(t, &s, &c);
+#else
+  s = std::sin(t);
+  c = std::cos(t);
+#endif
 }
 
 // arc_sincos of M angles: when every one is in the polynomial's range (the usual case) the M
@@ -122,11 +134,11 @@ __device__ __forceinline__ void arc_sincos_n(const double (&t)[M], double (&s)[M
 // lon2coord (merging_env.py:48-58): position along the arc -> (x longitudinal, y lateral).
 // The ego rides the arc on +y, the opponent its mirror image on -y. Split in three so the
 // lockstep step can batch the sin/cos of several cars.
-__device__ __forceinline__ double arc_angle(const mg_params& P, double lon) {
+MG_HD double arc_angle(const mg_params& P, double lon) {
   return P.angle0 - div_const(lon, P.R, P.inv_R);
 }
 
-__device__ __forceinline__ void arc_xy(const mg_params& P, double s, double c, bool ego, double& x,
+MG_HD void arc_xy(const mg_params& P, double s, double c, bool ego, double& x,
                                        double& y) {
   x = P.R * s;
   const double d = P.R - P.R * c;
@@ -134,7 +146,7 @@ __device__ __forceinline__ void arc_xy(const mg_params& P, double s, double c, b
   y = ego ? (half_w + d) : (half_w - d);
 }
 
-__device__ __forceinline__ void lon2coord(const mg_params& P, double lon, bool ego, double& x,
+MG_HD void lon2coord(const mg_params& P, double lon, bool ego, double& x,
                                           double& y) {
   double s, c;
   arc_sincos(arc_angle(P, lon), s, c);
@@ -151,7 +163,7 @@ struct Box {
   double l, r, t, b;  // lateral [l, r], longitudinal [t, b]
 };
 
-__device__ __forceinline__ Box vehicle_box(const mg_params& P, double lat, double lon) {
+MG_HD Box vehicle_box(const mg_params& P, double lat, double lon) {
   const int rx = static_cast<int>(lat) - P.veh_w / 2;
   const int ry = static_cast<int>(lon) - P.veh_h / 2;
   Box bx;
@@ -163,14 +175,14 @@ __device__ __forceinline__ Box vehicle_box(const mg_params& P, double lat, doubl
 }
 
 // shapely Polygon.intersects on two axis-aligned rectangles: the closed boxes share a point.
-__device__ __forceinline__ bool boxes_intersect(const Box& a, const Box& b) {
+MG_HD bool boxes_intersect(const Box& a, const Box& b) {
   return a.l <= b.r && b.l <= a.r && a.t <= b.b && b.t <= a.b;
 }
 
 // observe (merging_env.py:118-132): computed in fp64, stored as OT (fp64 for the single-env
 // record; fp32 -- the one rounding every fp32 output gets -- for the batched kernels)
 template <class OT>
-__device__ __forceinline__ void observe(const mg_params& P, double p1, double v1, double p2,
+MG_HD void observe(const mg_params& P, double p1, double v1, double p2,
                                         double v2, double x1, double y1, double x2, double y2,
                                         OT (&o)[kObs]) {
   o[0] = static_cast<OT>(x2 - x1);
@@ -186,7 +198,7 @@ __device__ __forceinline__ void observe(const mg_params& P, double p1, double v1
 }
 
 template <class OT>
-__device__ __forceinline__ void reset_obs(const mg_params& P, OT (&o)[kObs], double* dx1 = nullptr) {
+MG_HD void reset_obs(const mg_params& P, OT (&o)[kObs], double* dx1 = nullptr) {
   double x1, y1, x2, y2;
   lon2coord(P, P.start_point, true, x1, y1);
   lon2coord(P, P.start_point, false, x2, y2);
@@ -196,7 +208,7 @@ __device__ __forceinline__ void reset_obs(const mg_params& P, OT (&o)[kObs], dou
 
 // goal_status (scripts/hdqn.py:223-236) on the reference's fp64 values: dx1 = state[0] = x2 - x1,
 // v2 = state[9] (an int 0 after max(0, ...) compares as 0.0). 0: dx1 < -v2/2, 1: dx1 < v2/2, else 2.
-__device__ __forceinline__ int goal_status(double dx1, double v2) {
+MG_HD int goal_status(double dx1, double v2) {
   return dx1 < -0.5 * v2 ? 0 : (dx1 < 0.5 * v2 ? 1 : 2);
 }
 
@@ -229,7 +241,7 @@ struct Env {
   bool done;
 };
 
-__device__ __forceinline__ Env load_env(const mg_state& S, int64_t i) {
+MG_HD Env load_env(const mg_state& S, int64_t i) {
   Env e;
   e.p1 = S.p1[i];
   e.v1 = S.v1[i];
@@ -244,11 +256,11 @@ __device__ __forceinline__ Env load_env(const mg_state& S, int64_t i) {
   return e;
 }
 
-__device__ __forceinline__ uint32_t pack_tf(const Env& e) {
+MG_HD uint32_t pack_tf(const Env& e) {
   return e.steps | (e.winner << MG_TF_WINNER_SHIFT) | (e.done ? MG_TF_DONE : 0u);
 }
 
-__device__ __forceinline__ void store_env(const mg_state& S, int64_t i, const Env& e) {
+MG_HD void store_env(const mg_state& S, int64_t i, const Env& e) {
   st_state(S.p1 + i, e.p1);
   st_state(S.v1 + i, e.v1);
   st_state(S.p2 + i, e.p2);
@@ -317,7 +329,7 @@ __device__ __forceinline__ void draw_actions(uint64_t gi, uint64_t step, uint64_
 
 // time_stamp += dT; done if time_stamp > 500 (:141-143). The fp64 clock first exceeds 500
 // on step 2501; an integer count reproduces that exactly.
-__device__ __forceinline__ void env_clock(const mg_params& P, Env& e) {
+MG_HD void env_clock(const mg_params& P, Env& e) {
   e.steps = e.steps < MG_TF_STEPS_MASK ? e.steps + 1 : e.steps;
   if (static_cast<int32_t>(e.steps) >= P.timeout_steps) e.done = true;
 }
@@ -331,23 +343,23 @@ __device__ __forceinline__ void env_clock(const mg_params& P, Env& e) {
 // qpgen2's vsmall counts as already satisfied and leaves the unconstrained minimiser u = -0.0 (dposl
 // of a = -q, q = 0). (Mathematically u0 = b / t, since
 // D.1 = 0; evaluating that closed form instead moves u0 by an ulp in most steps.)
-__device__ __forceinline__ double mpc_acc_speed(const mg_params& P, double speed, double v) {
+MG_HD double mpc_acc_speed(const mg_params& P, double speed, double v) {
   const double b = speed - v;
   const double u = div_const(b, P.qp_nz, P.qp_inv_nz) * P.qp_z0;
   return fabs(b) < P.qp_vsmall ? -0.0 : u;  // dposl's -0.0 (a = -q = -0.0): nothing violated
 }
 
-__device__ __forceinline__ double mpc_acc(const mg_params& P, int a, double v) {
+MG_HD double mpc_acc(const mg_params& P, int a, double v) {
   return mpc_acc_speed(P, P.action_speed[a], v);
 }
 
 // action_dict[a] (merging_env.py:101) or 0.0 where a is not in it (the value is then unused)
-__device__ __forceinline__ double action_speed_or0(const mg_params& P, int a) {
+MG_HD double action_speed_or0(const mg_params& P, int a) {
   return valid_action(a) ? P.action_speed[a] : 0.0;
 }
 
 // v = max(0, v + acc*dT) (an int 0 when the max picks 0), p += v*dT  (:149-150, :153-154)
-__device__ __forceinline__ void move_car(const mg_params& P, double acc, double& p, double& v,
+MG_HD void move_car(const mg_params& P, double acc, double& p, double& v,
                                          bool& v_int) {
   const double nv = v + acc * P.dT;
   v_int = !(nv > 0.0);
@@ -355,16 +367,18 @@ __device__ __forceinline__ void move_car(const mg_params& P, double acc, double&
   p = p + v * P.dT;
 }
 
-__device__ __forceinline__ void score_step(const mg_params& P, Env& e, double x1, double y1,
+MG_HD void score_step(const mg_params& P, Env& e, double x1, double y1,
                                            double x2, double y2, StepOut& r, bool frozen = false);
 
 // main.py:225's win test, state[8] > state[3] = END_POINT - p2 > END_POINT - p1, on the state a step
 // acts on, evaluated before the move: left to the compiler it sinks into the rare finishing branch
 // and keeps the pre-step positions live across the step (66 instead of 61 VGPRs in the step
 // kernel: 7 waves per SIMD, a third round of blocks at 2^20 envs).
-__device__ __forceinline__ bool win_test_early(const mg_params& P, const Env& e) {
+MG_HD bool win_test_early(const mg_params& P, const Env& e) {
   int w = (P.end_point - e.p2) > (P.end_point - e.p1) ? 1 : 0;
+#if defined(__HIP_DEVICE_COMPILE__)
   asm volatile("" : "+v"(w));
+#endif
   return w != 0;
 }
 
@@ -374,7 +388,7 @@ __device__ __forceinline__ bool win_test_early(const mg_params& P, const Env& e)
 // sp1 / sp2: action_dict[a1] / [a2], looked up by the caller (action_speed_or0), so it can issue
 // those loads before the state loads (the step kernel; env_step below looks them up itself)
 template <bool CHECKED = true>
-__device__ __forceinline__ void env_step_sp(const mg_params& P, Env& e, int a1, int a2, double sp1, double sp2,
+MG_HD void env_step_sp(const mg_params& P, Env& e, int a1, int a2, double sp1, double sp2,
                                             StepOut& r) {
   r.win_pre = win_test_early(P, e);
   r.first1 = false;
@@ -407,7 +421,7 @@ __device__ __forceinline__ void env_step_sp(const mg_params& P, Env& e, int a1, 
 }
 
 template <bool CHECKED = true>
-__device__ __forceinline__ void env_step(const mg_params& P, Env& e, int a1, int a2, StepOut& r) {
+MG_HD void env_step(const mg_params& P, Env& e, int a1, int a2, StepOut& r) {
   env_step_sp<CHECKED>(P, e, a1, a2, action_speed_or0(P, a1), action_speed_or0(P, a2), r);
 }
 
@@ -464,7 +478,7 @@ __device__ __forceinline__ void env_step_lockstep(const mg_params& P, Env (&e)[N
 // arrival / winner, collision, returns. r.r1_int / r.r2_int must be false on entry. frozen: an
 // invalid action -- the step stops before any of this (observation and rewards 0, no state
 // change), as env_step's early return.
-__device__ __forceinline__ void score_step(const mg_params& P, Env& e, double x1, double y1,
+MG_HD void score_step(const mg_params& P, Env& e, double x1, double y1,
                                            double x2, double y2, StepOut& r, bool frozen) {
   observe(P, e.p1, e.v1, e.p2, e.v2, x1, y1, x2, y2, r.o);
   r.dx1 = x2 - x1;
@@ -538,14 +552,14 @@ struct EpStats {
 };
 
 // the record as 4 x 16 bytes: {ret[0], ret[1]}, {ret_main, ret1_pending}, counts 0-3, counts 4-7
-__device__ __forceinline__ double2* stats_f64(const mg_stats& St, int64_t i) {
+MG_HD double2* stats_f64(const mg_stats& St, int64_t i) {
   return reinterpret_cast<double2*>(St.rec + i);
 }
-__device__ __forceinline__ uint4* stats_u32(const mg_stats& St, int64_t i) {
+MG_HD uint4* stats_u32(const mg_stats& St, int64_t i) {
   return reinterpret_cast<uint4*>(St.rec + i) + 2;
 }
 
-__device__ __forceinline__ void stats_load(const mg_stats& St, int64_t i, EpStats& s) {
+MG_HD void stats_load(const mg_stats& St, int64_t i, EpStats& s) {
   s.dirty_f = s.dirty_c = false;
   s.r1 = s.r2 = s.rm = s.pend = 0.0;
   s.ep_coll = s.ego_wm = s.wh = s.steps = 0u;
@@ -558,7 +572,7 @@ __device__ __forceinline__ void stats_load(const mg_stats& St, int64_t i, EpStat
   }
 }
 
-__device__ __forceinline__ void stats_store(const mg_stats& St, int64_t i, const EpStats& s) {
+MG_HD void stats_store(const mg_stats& St, int64_t i, const EpStats& s) {
   if (!St.rec) return;
   if (s.dirty_f) {
     stats_f64(St, i)[0] = make_double2(s.r1, s.r2);
@@ -579,7 +593,7 @@ __device__ __forceinline__ void stats_store(const mg_stats& St, int64_t i, const
 
 // The ego arrived first on a step that did not end the episode: keep r1_accumulate as it stood
 // before that step -- main.py's ep_reward stops there (:209-211), since winner stays 1.
-__device__ __forceinline__ void note_first_arrival(const mg_stats& St, int64_t i, const StepOut& r,
+MG_HD void note_first_arrival(const mg_stats& St, int64_t i, const StepOut& r,
                                                    EpStats* sreg = nullptr) {
   if (sreg) {
     sreg->pend = r.ret_pre;
@@ -595,7 +609,7 @@ __device__ __forceinline__ void note_first_arrival(const mg_stats& St, int64_t i
 // r{1,2}_accumulate (hdqn.py's ep_reward), main.py's winner-filtered ep_reward (r1_accumulate
 // before the ego-first step while winner == 1), main.py:225's win test on the state the last step
 // acted on (r.win_pre) and hdqn.py:342's on the terminal state.
-__device__ __forceinline__ void finish_episode(const mg_params& P, Env& e, StepOut& r,
+MG_HD void finish_episode(const mg_params& P, Env& e, StepOut& r,
                                                const mg_stats& St, float* final_obs_row,
                                                int64_t i, EpStats* sreg = nullptr) {
   const bool ego_won = e.winner == 1;
@@ -643,7 +657,7 @@ __device__ __forceinline__ void finish_episode(const mg_params& P, Env& e, StepO
 }
 
 // After a step with statistics: the first-arrival bookkeeping, then autoreset where done.
-__device__ __forceinline__ void after_step(const mg_params& P, Env& e, StepOut& r, const mg_stats& St,
+MG_HD void after_step(const mg_params& P, Env& e, StepOut& r, const mg_stats& St,
                                            float* final_obs_row, int64_t i, bool autoreset,
                                            EpStats* sreg = nullptr) {
   const bool finish = autoreset && r.done;
@@ -745,7 +759,7 @@ __device__ __forceinline__ int64_t opaque_index(int64_t i) {
 
 // One env-step's four byte outputs (a1, a2, done, collision) as the little-endian u32 of an
 // interleaved [.., 4] uint8 buffer (mg_outputs.flags, mg_traj.flags).
-__device__ __forceinline__ uint32_t pack_step_bytes(int a1, int a2, bool done, bool coll) {
+MG_HD uint32_t pack_step_bytes(int a1, int a2, bool done, bool coll) {
   return static_cast<uint32_t>(a1 & 0xff) | (static_cast<uint32_t>(a2 & 0xff) << 8) |
          (done ? 0x10000u : 0u) | (coll ? 0x1000000u : 0u);
 }
@@ -2778,6 +2792,101 @@ __global__ __launch_bounds__(kBlock) void goal_status_kernel(const double* dx1, 
   if (i < n) out[i] = static_cast<int8_t>(goal_status(dx1[i], v2[i]));
 }
 
+// ============================================================================ host (CPU) path
+// The step kernel's per-env body on the host, over host pointers: the single env of BASELINE
+// config 1 (MergeEnv.step / reset / observe, merging_env.py:118-230, driven one step at a time by
+// scripts/human_player.py:112-187 at 20 Hz), where a kernel launch plus a stream synchronisation
+// per step (28.5 us, BENCH_r03 dropin_single_env) costs 20x the step's own ~1 us of fp64 work.
+// The same MG_HD functions as the kernels, so a host step gives the kernel's doubles bit for bit
+// (tests/test_dropin.py: golden traces on the CPU; test_host_step_equals_kernel on the GPU box).
+// Outputs and their conditions follow step_kernel<kActArrays, OUT64 = rec64 != NULL> exactly.
+void host_step_env(const Launch& L, int64_t i, bool& done, bool& won) {
+  const mg_params& P = L.P;
+  const int a1 = L.a1[i];
+  const int a2 = L.a2 ? static_cast<int>(L.a2[i]) : MG_ACTION_NONE;
+  Env e = load_env(L.S, i);
+  StepOut r;
+  env_step_sp(P, e, a1, a2, action_speed_or0(P, a1), action_speed_or0(P, a2), r);
+  done = won = false;
+  if (r.bad) {
+    if (L.O.error) *L.O.error |= r.bad;
+    store_env(L.S, i, e);
+  } else {
+    if (L.O.rec64) {
+      mg_rec64* rec = L.O.rec64 + i;
+      double x1, y1, x2, y2, od[kObs];
+      lon2coord(P, e.p1, true, x1, y1);
+      lon2coord(P, e.p2, false, x2, y2);
+      observe(P, e.p1, e.v1, e.p2, e.v2, x1, y1, x2, y2, od);
+      for (int k = 0; k < kObs; ++k) rec->obs[k] = od[k];
+      rec->rew[0] = r.r1;
+      rec->rew[1] = r.r2;
+      rec->acc[0] = r.acc1;
+      rec->acc[1] = r.acc2;
+      rec->pos[0] = e.p1;
+      rec->pos[1] = e.p2;
+      rec->vel[0] = e.v1;
+      rec->vel[1] = e.v2;
+      rec->ret[0] = e.ret1;
+      rec->ret[1] = e.ret2;
+      rec->tf = pack_tf(e);
+      rec->status = (r.done ? MG_ST_DONE : 0u) | (r.coll ? MG_ST_COLLISION : 0u) |
+                    (r.r1_int ? MG_ST_R1_INT : 0u) | (r.r2_int ? MG_ST_R2_INT : 0u) |
+                    (r.v1_int ? MG_ST_V1_INT : 0u) | (r.v2_int ? MG_ST_V2_INT : 0u);
+    } else if (L.O.rew) {
+      L.O.rew[2 * i] = static_cast<float>(r.r1);
+      L.O.rew[2 * i + 1] = static_cast<float>(r.r2);
+    }
+    if (L.O.flags) {
+      reinterpret_cast<uint32_t*>(L.O.flags)[i] = pack_step_bytes(a1, a2, r.done, r.coll);
+    } else {
+      if (L.O.done) L.O.done[i] = r.done ? 1 : 0;
+      if (L.O.coll) L.O.coll[i] = r.coll ? 1 : 0;
+    }
+    done = r.done;
+    won = e.winner == 1;
+    after_step(P, e, r, L.St, L.O.final_obs ? L.O.final_obs + i * kObs : nullptr, i,
+               (L.flags & MG_AUTORESET) != 0);
+    store_env(L.S, i, e);
+  }
+  if (!L.O.rec64 && L.O.obs) {  // the kernel's observation tile: zeros for a bad action's env
+    for (int k = 0; k < kObs; ++k) L.O.obs[i * kObs + k] = r.o[k];
+  }
+}
+
+void host_reset_env(const mg_params& P, const mg_state& S, const mg_outputs& O, int64_t i) {
+  S.p1[i] = S.p2[i] = P.start_point;
+  S.v1[i] = S.v2[i] = P.start_vel;
+  S.ret1[i] = S.ret2[i] = 0.0;
+  S.tf[i] = 0u;
+  if (!O.obs && !O.rec64) return;
+  double o[kObs];
+  reset_obs(P, o);
+  if (O.obs)
+    for (int k = 0; k < kObs; ++k) O.obs[i * kObs + k] = static_cast<float>(o[k]);
+  if (O.rec64) {
+    mg_rec64* rec = O.rec64 + i;
+    std::memset(rec, 0, sizeof(*rec));
+    for (int k = 0; k < kObs; ++k) rec->obs[k] = o[k];
+    rec->pos[0] = rec->pos[1] = P.start_point;
+    rec->vel[0] = rec->vel[1] = P.start_vel;
+  }
+}
+
+void host_observe_env(const mg_params& P, const mg_state& S, const mg_outputs& O, int64_t i) {
+  const double p1 = S.p1[i], v1 = S.v1[i], p2 = S.p2[i], v2 = S.v2[i];
+  double x1, y1, x2, y2, o[kObs];
+  lon2coord(P, p1, true, x1, y1);
+  lon2coord(P, p2, false, x2, y2);
+  observe(P, p1, v1, p2, v2, x1, y1, x2, y2, o);
+  if (O.obs)
+    for (int k = 0; k < kObs; ++k) O.obs[i * kObs + k] = static_cast<float>(o[k]);
+  if (O.rec64)
+    for (int k = 0; k < kObs; ++k) O.rec64[i].obs[k] = o[k];
+  uint8_t* coll = O.flags ? O.flags + 4 * i + 3 : (O.coll ? O.coll + i : nullptr);
+  if (coll) *coll = boxes_intersect(vehicle_box(P, y1, x1), vehicle_box(P, y2, x2)) ? 1 : 0;
+}
+
 }  // namespace
 
 // one config-5 launch (with dispatch-packet events when mg_time_next_launch armed them)
@@ -3201,6 +3310,56 @@ int mg_observe(const mg_params* params, const mg_state* state, const mg_outputs*
   hipLaunchKernelGGL(observe_kernel, dim3(blocks), dim3(kBlock), 0,
                      static_cast<hipStream_t>(stream), *params, *state, *out, n);
   return finish_launch("mg_observe");
+}
+
+int mg_host_step(const mg_params* params, const mg_state* state, const int8_t* a1, const int8_t* a2,
+                 const mg_outputs* out, const mg_stats* stats, int64_t n, uint32_t flags) {
+  if (int e = check_common(params, state, out, n)) return e;
+  if (n == 0) return 0;
+  if (!a1) return fail(hipErrorInvalidValue, "%s", "a1 is NULL");
+  Launch L{};
+  L.P = *params;
+  L.S = *state;
+  L.O = *out;
+  if (stats) L.St = *stats;
+  L.a1 = a1;
+  L.a2 = a2;
+  L.n = n;
+  L.flags = flags;
+  for (int64_t w = 0; w < n; w += 64) {  // one 64-env group per done / won mask word
+    uint64_t dm = 0, wm = 0;
+    const int64_t end = n - w < 64 ? n : w + 64;
+    for (int64_t i = w; i < end; ++i) {
+      bool d, won;
+      host_step_env(L, i, d, won);
+      dm |= static_cast<uint64_t>(d) << (i - w);
+      wm |= static_cast<uint64_t>(won) << (i - w);
+    }
+    if (L.O.done_mask) L.O.done_mask[w >> 6] = dm;
+    if (L.O.won_mask) L.O.won_mask[w >> 6] = wm;
+  }
+  g_err[0] = '\0';
+  return 0;
+}
+
+int mg_host_reset(const mg_params* params, const mg_state* state, const uint8_t* mask,
+                  const mg_outputs* out, int64_t n) {
+  if (!params) return fail(hipErrorInvalidValue, "%s", "params is NULL");
+  if (n < 0) return fail(hipErrorInvalidValue, "%s", "n < 0");
+  if (int e = check_state(state)) return e;
+  mg_outputs o{};
+  if (out) o = *out;
+  for (int64_t i = 0; i < n; ++i)
+    if (!mask || mask[i]) host_reset_env(*params, *state, o, i);
+  g_err[0] = '\0';
+  return 0;
+}
+
+int mg_host_observe(const mg_params* params, const mg_state* state, const mg_outputs* out, int64_t n) {
+  if (int e = check_common(params, state, out, n)) return e;
+  for (int64_t i = 0; i < n; ++i) host_observe_env(*params, *state, *out, i);
+  g_err[0] = '\0';
+  return 0;
 }
 
 }  // extern "C"

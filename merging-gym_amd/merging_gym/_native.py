@@ -15,7 +15,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libmerging_hip.so"
 LIB_PATH = os.environ.get("MERGING_HIP_LIB", os.path.join(_HERE, LIB_NAME))
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 OBS_DIM = 10
 NUM_ACTIONS = 5
@@ -88,6 +88,17 @@ REC64_DTYPE = np.dtype([("obs", np.float64, (OBS_DIM,)), ("rew", np.float64, (2,
 assert REC64_DTYPE.itemsize == 168
 
 
+class Rec64(_c.Structure):
+    """struct mg_rec64 as a ctypes structure: the single env reads its fields straight from the
+    record's memory (host memory, or pinned memory the kernel wrote) without a numpy view."""
+    _fields_ = [("obs", _c.c_double * OBS_DIM), ("rew", _c.c_double * 2), ("acc", _c.c_double * 2),
+                ("pos", _c.c_double * 2), ("vel", _c.c_double * 2), ("ret", _c.c_double * 2),
+                ("tf", _c.c_uint32), ("status", _c.c_uint32)]
+
+
+assert _c.sizeof(Rec64) == REC64_DTYPE.itemsize
+
+
 class NativeError(RuntimeError):
     pass
 
@@ -126,6 +137,10 @@ def _load(path=LIB_PATH):
                                     _c.c_int64, _c.c_uint64, _c.c_uint64, _c.c_int32, _P, _c.c_int32, _P,
                                     _c.c_int32, _c.c_uint64, _c.c_int32, _P, _P, _P, _P, _c.c_int64, _c.c_uint32,
                                     _P]
+    # ABI 20: the same step / reset / observe on host memory (the CPU single env, BASELINE config 1)
+    lib.mg_host_step.argtypes = [PP, SP, _P, _P, OP, STP, _c.c_int64, _c.c_uint32]
+    lib.mg_host_reset.argtypes = [PP, SP, _P, OP, _c.c_int64]
+    lib.mg_host_observe.argtypes = [PP, SP, OP, _c.c_int64]
     lib.mg_time_next_launch.argtypes = [_P, _P]
     lib.mg_goal_status.argtypes = [_P, _P, _P, _c.c_int64, _P]
     lib.mg_replay_scratch_bytes.argtypes = [_c.c_int64, _c.c_int32]
@@ -137,7 +152,7 @@ def _load(path=LIB_PATH):
     for f in (lib.mg_step, lib.mg_step_random, lib.mg_reset, lib.mg_observe, lib.mg_rollout_random,
               lib.mg_time_next_launch, lib.mg_qnet_pack, lib.mg_qnet_forward, lib.mg_rollout_qnet,
               lib.mg_rollout_hdqn, lib.mg_replay_store, lib.mg_replay_sample, lib.mg_goal_status,
-              lib.mg_qnet_fragments):
+              lib.mg_qnet_fragments, lib.mg_host_step, lib.mg_host_reset, lib.mg_host_observe):
         f.restype = _c.c_int
     v = lib.mg_abi_version()
     if v != ABI_VERSION:

@@ -4,6 +4,7 @@
 // a GPU (nothing here launches a kernel); any sanitizer report aborts the run.
 #include <cstdio>
 #include <cstring>
+#include <vector>
 
 #include "merging_hip.h"
 
@@ -13,6 +14,59 @@ static int expect_error(int rc, const char* what) {
     return 1;
   }
   return 0;
+}
+
+// The host step path (ABI 20) actually runs: 130 envs (a partial last mask word) in exactly sized
+// heap arrays, 3,000 autoreset steps with every optional output, None / invalid actions and
+// observe / reset calls in between, so the sanitizers see every access the host loop makes.
+static int host_step_run(const mg_params& p) {
+  const int64_t n = 130, words = (n + 63) / 64;
+  std::vector<double> p1(n), v1(n), p2(n), v2(n), r1(n), r2(n);
+  std::vector<uint16_t> tf(n);
+  std::vector<float> obs(n * MG_OBS_DIM), rew(n * 2), fobs(n * MG_OBS_DIM);
+  std::vector<uint8_t> flags(n * 4), done(n), coll(n), mask(n);
+  std::vector<uint64_t> dm(words), wm(words);
+  std::vector<mg_episode_stats> st(n);
+  std::vector<mg_rec64> rec(n);
+  std::vector<int8_t> a1(n), a2(n);
+  int32_t err = 0;
+  mg_state s{p1.data(), v1.data(), p2.data(), v2.data(), r1.data(), r2.data(), tf.data()};
+  mg_outputs of{};
+  of.obs = obs.data();
+  of.rew = rew.data();
+  of.done_mask = dm.data();
+  of.final_obs = fobs.data();
+  of.error = &err;
+  of.won_mask = wm.data();
+  of.flags = flags.data();
+  mg_outputs ob{};  // the byte arrays and the fp64 record instead of the interleaved step record
+  ob.done = done.data();
+  ob.coll = coll.data();
+  ob.rec64 = rec.data();
+  ob.error = &err;
+  mg_stats ms{st.data()};
+  int bad = 0;
+  if (mg_host_reset(&p, &s, nullptr, &of, n) != 0) ++bad;
+  uint32_t episodes = 0;
+  for (int k = 0; k < 3000; ++k) {
+    for (int64_t i = 0; i < n; ++i) {
+      a1[i] = static_cast<int8_t>((k * 7 + i) % 5);
+      a2[i] = static_cast<int8_t>((k + 3 * i) % 6 - 1);  // -1 = None
+    }
+    if (k % 500 == 499) a1[k % n] = 9;  // the reference's KeyError path
+    const bool f64 = k % 3 == 0;
+    if (mg_host_step(&p, &s, a1.data(), a2.data(), f64 ? &ob : &of, &ms, n, f64 ? 0u : MG_AUTORESET) != 0) ++bad;
+    if (k % 500 == 499 && err != 1) ++bad;
+    err = 0;
+    if (k % 400 == 0) {
+      for (int64_t i = 0; i < n; ++i) mask[i] = static_cast<uint8_t>(i % 3 == 0);
+      if (mg_host_observe(&p, &s, &ob, n) != 0 || mg_host_reset(&p, &s, mask.data(), &ob, n) != 0) ++bad;
+    }
+  }
+  for (int64_t i = 0; i < n; ++i) episodes += st[i].episodes;
+  if (episodes == 0) ++bad;
+  std::printf("host step run: %u episodes finished\n", episodes);
+  return bad;
 }
 
 int main() {
@@ -88,6 +142,7 @@ int main() {
   // empty batches return before any launch
   if (mg_step(&p, &sf, static_cast<int8_t*>(fake), nullptr, &o, nullptr, 0, 0, nullptr) != 0) bad += 1;
   if (mg_reset(&p, &sf, nullptr, &o, 0, nullptr) != 0) bad += 1;
+  bad += host_step_run(p);
   std::printf("abi sanitizer run: %d failures\n", bad);
   return bad;
 }

@@ -36,6 +36,9 @@ def test_constants_module(golden):
 
 
 def test_no_cpu_fallback():
+    """The batched env and the single env's GPU backend refuse without a GPU. The single env's
+    default backend is the host step (mg_host_step: the kernels' own step functions built for the
+    CPU, BASELINE config 1), which is not a fallback: it is chosen without looking for a GPU."""
     import torch
 
     if torch.cuda.is_available():
@@ -43,7 +46,12 @@ def test_no_cpu_fallback():
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         merging_gym.MergeVecEnv(8)
     with pytest.raises(RuntimeError, match="no CPU fallback"):
-        merging_gym.make("merging_env-v0")
+        merging_gym.make("merging_env-v0", backend="gpu")
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        merging_gym.make("merging_env-v0", device="cuda:0")
+    assert merging_gym.make("merging_env-v0").backend == "host"
+    with pytest.raises(ValueError):
+        merging_gym.make("merging_env-v0", backend="oracle")
 
 
 def test_extend_env_is_the_print_stub(capsys):
@@ -68,8 +76,8 @@ def _stub_env():
 def test_gym_registration_through_the_package_import():
     """With gym importable (the gym 0.20 stand-in in tests/stubs), importing merging_gym runs
     its registration: the reference's ids resolve to the env classes, re-importing skips ids gym
-    already holds instead of failing, and gym.make builds the env (here without a GPU, so the
-    GPU-backed MergeEnv refuses loudly -- the drop-in itself is driven by test_gpu_dropin)."""
+    already holds instead of failing, and gym.make builds the env (the host-step single env; its
+    GPU backend refuses loudly without a GPU -- the drop-in itself is driven by test_dropin)."""
     import subprocess
 
     code = r'''
@@ -84,9 +92,10 @@ assert getattr(importlib.import_module(mod), attr) is MergeEnv
 ext = gym.make("merging_env_extend-v0").unwrapped
 assert type(ext).__name__ == "MergeEnvExtend"
 import torch
+assert gym.make("merging_env-v0").unwrapped.backend == "host"
 if not torch.cuda.is_available():
     try:
-        gym.make("merging_env-v0")
+        gym.make("merging_env-v0", backend="gpu")
     except RuntimeError as e:
         assert "no CPU fallback" in str(e)
     else:

@@ -1,4 +1,4 @@
-"""GPU side of the CSV trajectory logs (scripts/human_player.py:108-111, :180-181).
+"""The drop-in and device sides of the CSV trajectory logs (scripts/human_player.py:108-111, :180-181).
 
 * The drop-in MergeEnv, logged with EpisodeCSVWriter in human_player.py's loop, reproduces
   the reference env's own files (tests/golden/csv): same rows, same int-typed field text,
@@ -17,17 +17,18 @@ import pytest
 
 from test_trajlog import CSV_DIR, assert_csv_equivalent
 
-pytestmark = pytest.mark.gpu
+BACKENDS = ["host", pytest.param("gpu", marks=pytest.mark.gpu)]
 
 
+@pytest.mark.parametrize("backend", BACKENDS)
 @pytest.mark.parametrize("ep", [0, 1, 2, 3])
-def test_dropin_episode_csv_matches_reference(tmp_path, ep):
+def test_dropin_episode_csv_matches_reference(tmp_path, ep, backend):
     import merging_gym
     from merging_gym.trajlog import EpisodeCSVWriter
 
     acts = np.load(os.path.join(CSV_DIR, "actions.npz"))
     a1, a2 = acts[f"ep{ep}_a1"], acts[f"ep{ep}_a2"]
-    env = merging_gym.make("merging_env-v0")
+    env = merging_gym.make("merging_env-v0", backend=backend)
     state = env.reset()
     path = tmp_path / f"episode{ep}"
     with EpisodeCSVWriter(str(path)) as w:
@@ -47,6 +48,7 @@ def _read_rows(path):
     return rows[1:]
 
 
+@pytest.mark.gpu
 @pytest.mark.parametrize("opp", [True, False])
 def test_trajectory_logger_segments_filters_and_round_trips(tmp_path, opp):
     from merging_gym import MergeVecEnv

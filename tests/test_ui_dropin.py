@@ -1,10 +1,12 @@
-"""UI drawn from device state: the golden human-experiment session replayed on the GPU envs.
+"""UI drawn from the env's step record: the golden human-experiment session (human_player.py's
+loop) replayed on the drop-in MergeEnv (host and GPU step backends) and on a GPU MergeVecEnv row.
 
 tests/golden/render_golden.json (gen_render.py) is the reference MergeEnv's own session:
 resets, steps with recorded actions and UI calls with the pygame calls they made. Here the
-same resets and steps run through the HIP step kernel, and each UI call draws the state read
-back from the device -- MergeEnv's step record, and row 0 of an 8-env MergeVecEnv stepped with
-the same actions -- through the same recording stand-in. Text and structure must be
+same resets and steps run through the library's step (mg_host_step on the CPU, the HIP step
+kernel on the GPU), and each UI call draws the state read back from it -- MergeEnv's step
+record, and row 0 of an 8-env MergeVecEnv stepped with the same actions -- through the same
+recording stand-in. Text and structure must be
 identical; coordinates agree to 1e-9 relative (the device state equals the reference's
 fp64 state up to the last-bit rounding of the QP stand-in the golden traces were recorded with).
 """
@@ -17,7 +19,7 @@ import pytest
 
 from test_ui import GOLDEN, call_ui, load_stub
 
-pytestmark = pytest.mark.gpu
+BACKENDS = ["host", pytest.param("gpu", marks=pytest.mark.gpu)]
 
 
 def same_log(ours, ref, rel=1e-9):
@@ -35,13 +37,14 @@ def golden():
         return json.load(f)
 
 
-def test_merge_env_ui_session_matches_reference(golden):
+@pytest.mark.parametrize("backend", BACKENDS)
+def test_merge_env_ui_session_matches_reference(golden, backend):
     from merging_gym.envs.merging_env import MergeEnv
     from merging_gym.envs.ui import MergeUI
 
     stub = load_stub()
     stub.clear()
-    env = MergeEnv(device="cuda:0")
+    env = MergeEnv(backend=backend)
     env.ui = MergeUI(pygame=stub)
     assert json.loads(json.dumps(stub.LOG)) == golden["init"]
     renders = 0
@@ -68,6 +71,7 @@ def test_merge_env_ui_session_matches_reference(golden):
     assert renders > 40
 
 
+@pytest.mark.gpu
 def test_vector_env_row_renders_like_reference(golden):
     """render_view(i) of a MergeVecEnv row (autoreset off, every env given the session's
     actions) drawn by MergeUI equals the reference's render of the same state."""
