@@ -614,6 +614,12 @@ def dropin_leg(seed: int):
     return out
 
 
+def _native_build_info():
+    from merging_gym import _native
+
+    return _native.build_info()
+
+
 def sync_spin():
     """hipDeviceScheduleSpin for this process, before the HIP context exists: a synchronize then
     spins on the host instead of yielding, so the host thread that issues the timed launches is
@@ -811,6 +817,7 @@ def main():
                        "envs_per_gpu": E, "global_envs": world * E,
                        "parallelism": f"dp{world} (env shards, no per-step collective)"},
             "burn_in_steps": args.burn_in + args.burn_in_launches,
+            "build": _native_build_info(),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBPS) if achieved else None,
                          "traffic": pmc, "kernel": KERNEL_NAME,

@@ -34,7 +34,7 @@
  *                     HOST memory, for the single env of BASELINE config 1 (the reference's CPU
  *                     MergeEnv, merging_env.py:118-230, driven one step at a time by
  *                     scripts/human_player.py:112-187 and the scripts' list API)
- *   mg_abi_version, mg_last_error, mg_params_default, mg_time_next_launch: library plumbing
+ *   mg_abi_version, mg_last_error, mg_build_info, mg_params_default, mg_time_next_launch: library plumbing
  *                     and profiling (no reference twin).
  *
  * Conventions
@@ -249,6 +249,8 @@ typedef struct mg_stats {
 
 int mg_abi_version(void);
 const char* mg_last_error(void);
+/* (ABI 20) The compiler and HIP version the library was built with, e.g. for test logs. */
+const char* mg_build_info(void);
 
 /* Profiling hook: the next mg_step / mg_step_random / mg_rollout_random launch made by the calling thread records
  * start_event / stop_event (hipEvent_t created by the caller; either may be NULL) in its own

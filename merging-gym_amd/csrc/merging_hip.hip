@@ -43,6 +43,8 @@ constexpr int kObs = MG_OBS_DIM;
 // correctly rounded there too, so host and device give the same doubles; only the cold sin/cos
 // branch (|theta| >= 1/16, off every live-episode state) uses glibc on the host.
 #define MG_HD __host__ __device__ __forceinline__
+#define MG_STR_(x) #x
+#define MG_STR(x) MG_STR_(x)
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -2910,6 +2912,14 @@ int mg_time_next_launch(void* start_event, void* stop_event) {
 }
 
 const char* mg_last_error(void) { return g_err; }
+
+// The compiler that built this library (its hipcc version decides the inline-asm permlane hazard
+// padding of qnet_gather_q, which hipcc 7.2's builtins miscompiled): printed in the GPU test log
+// header and the bench line.
+const char* mg_build_info(void) {
+  return "clang " __clang_version__ "; HIP " MG_STR(HIP_VERSION_MAJOR) "." MG_STR(HIP_VERSION_MINOR) "."
+         MG_STR(HIP_VERSION_PATCH) "; ABI " MG_STR(MG_ABI_VERSION) "; gfx950, -ffp-contract=off";
+}
 
 void mg_params_default(mg_params* p) {
   if (!p) return;

@@ -114,6 +114,7 @@ def _load(path=LIB_PATH):
     lib = _c.CDLL(path)
     lib.mg_abi_version.restype = _c.c_int
     lib.mg_last_error.restype = _c.c_char_p
+    lib.mg_build_info.restype = _c.c_char_p
     lib.mg_params_default.argtypes = [_c.POINTER(Params)]
     lib.mg_params_default.restype = None
     PP, SP, OP, STP = (_c.POINTER(Params), _c.POINTER(State), _c.POINTER(Outputs),
@@ -167,6 +168,11 @@ def check(rc: int, what: str) -> None:
     if rc != 0:
         msg = lib.mg_last_error().decode(errors="replace")
         raise NativeError(f"{what} failed (hipError {rc}): {msg}")
+
+
+def build_info() -> str:
+    """Compiler / HIP version the loaded library was built with (mg_build_info)."""
+    return lib.mg_build_info().decode()
 
 
 def default_params() -> Params:

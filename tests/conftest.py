@@ -31,6 +31,17 @@ def coracle():
     return merge_oracle.COracle()
 
 
+def pytest_report_header(config):
+    """The library under test and the compiler that built it (the Q-net forward's permlane
+    hazard padding is written for hipcc 7.2's code generation)."""
+    try:
+        from merging_gym import _native
+
+        return [f"libmerging_hip: {_native.LIB_PATH}", f"built with: {_native.build_info()}"]
+    except Exception as e:  # noqa: BLE001 - the header must not break collection
+        return [f"libmerging_hip: not loadable ({e})"]
+
+
 def _gpu_available():
     try:
         import torch
