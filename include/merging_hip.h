@@ -17,6 +17,8 @@
  *                     device -- DQN.store_transition (scripts/main.py:115-119, hdqn.py:180-184)
  *                     for a whole batch of transitions, and learn()'s uniform minibatch draw
  *                     np.random.choice(MEMORY_CAPACITY, BATCH_SIZE) (main.py:130-131)
+ *   mg_stats_reduce (ABI 20) the batch's episode-statistics records summed in a fixed order: the
+ *                     running totals of the scripts' logging loops (hdqn.py:330-346, main.py:221-228)
  *   mg_reset        replaces MergeEnv.reset()                        merging_env.py:208-230
  *   mg_observe      replaces MergeEnv.observe() and is_collided()    merging_env.py:118-132,
  *                     :198-206 (no state change)
@@ -247,6 +249,14 @@ typedef struct mg_stats {
   mg_episode_stats* rec;  /* [n] records, or NULL: no statistics */
 } mg_stats;
 
+/* (ABI 20) The records of a batch summed: what the logging loops of scripts/hdqn.py:330-346 and
+ * scripts/main.py:221-228 total over completed episodes. 72 bytes, the per-rank contribution of the
+ * multi-GPU statistics all-gather (merging_gym/distributed.py). */
+typedef struct mg_stats_totals {
+  double ret[3];      /* sums of ret[0], ret[1], ret_main */
+  int64_t counts[6];  /* sums of episodes, collisions, ego_first, steps, win_main, win_hdqn */
+} mg_stats_totals;
+
 int mg_abi_version(void);
 const char* mg_last_error(void);
 /* (ABI 20) The compiler and HIP version the library was built with, e.g. for test logs. */
@@ -436,6 +446,18 @@ int mg_replay_store(float* rows, uint64_t* counter, int64_t capacity, int32_t ro
 int mg_replay_sample(const float* rows, const uint64_t* counter, int64_t capacity,
                      int32_t row_floats, uint64_t seed, uint64_t draw, int32_t filled_only,
                      float* out, int64_t* idx_out, int64_t batch, void* stream);
+
+/* (ABI 20) *totals = the n records summed on the device, in a fixed order so the fp64 sums are
+ * reproducible bit for bit: blocks of 1,024 records, thread t of 256 adding records t, t + 256,
+ * t + 512, t + 768 of its block in that order onto -0.0, the 256 values folded in halves
+ * (v[t] += v[t + o] for o = 128, 64, ..., 1); then the block partials the same way (thread t adding
+ * partials t, t + 256, ... in order, then the fold). Counts are exact. scratch: device buffer of at
+ * least mg_stats_reduce_scratch_bytes(n) bytes (16-byte aligned); rec 16-byte aligned, totals (a
+ * device mg_stats_totals) 8-byte aligned. Two launches, stream-ordered; n == 0 gives zero counts
+ * and -0.0 sums. */
+size_t mg_stats_reduce_scratch_bytes(int64_t n);
+int mg_stats_reduce(const mg_episode_stats* rec, int64_t n, mg_stats_totals* totals, void* scratch,
+                    size_t scratch_bytes, void* stream);
 
 /* Resets the envs whose mask byte is non-zero (mask == NULL: all n) and writes their reset
  * observation to out->obs / out->rec64 when given. Replaces MergeEnv.reset (merging_env.py:208-230). */

@@ -48,6 +48,8 @@ constexpr int kObs = MG_OBS_DIM;
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // Store of a per-step output (observation, reward, flags, actions): written once, never
 // re-read by the step, so optionally non-temporal. The env state is stored normally: the
@@ -2787,6 +2789,104 @@ void mpc_qp_constants(double t, double* nz_out, double* z0_out, double* vsmall_o
   *vsmall_out = vs;
 }
 
+// ============================================================================ statistics reduction
+// The per-env 64-byte records (mg_episode_stats) summed to one mg_stats_totals in a FIXED order, so
+// the fp64 sums are reproducible bit for bit (oracle/merge_numpy.py stats_reduce restates it):
+//   pass 1 (block b of kRedThreads threads, kRedEnvs envs): thread t adds the records of envs
+//          b kRedEnvs + j kRedThreads + t, j = 0..kRedPer-1, in j order onto -0.0 (the additive
+//          identity), then the block folds its kRedThreads values in halves (v[t] += v[t + o],
+//          o = 128, 64, ..., 1) -> partial b;
+//   pass 2 (one block): thread t adds partials t, t + 256, ... in order onto -0.0, then the same fold.
+// The counts are exact int64 sums. Replaces the logging loops' running totals (hdqn.py:330-346,
+// main.py:221-228) for a whole batch; a torch sum over strided record columns took 7.6 ms at 2^20
+// envs (BENCH_r03 episodes.reduce_ms) for 64 MB of records.
+constexpr int kRedThreads = 256;
+constexpr int kRedPer = 4;
+constexpr int kRedEnvs = kRedThreads * kRedPer;  // 1,024 records (64 KB) per pass-1 block
+
+__device__ __forceinline__ void red_fold(double (*sd)[kRedThreads], int64_t (*si)[kRedThreads], int t) {
+#pragma unroll
+  for (int o = kRedThreads / 2; o > 0; o >>= 1) {
+    __syncthreads();
+    if (t < o) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) sd[k][t] = sd[k][t] + sd[k][t + o];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) si[k][t] += si[k][t + o];
+    }
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void red_store(mg_stats_totals* out, double (*sd)[kRedThreads],
+                                          int64_t (*si)[kRedThreads]) {
+  mg_stats_totals o;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) o.ret[k] = sd[k][0];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) o.counts[k] = si[k][0];
+  *out = o;
+}
+
+__global__ __launch_bounds__(kRedThreads) void stats_reduce_kernel(const mg_episode_stats* rec, int64_t n,
+                                                                   mg_stats_totals* part) {
+  __shared__ double sd[3][kRedThreads];
+  __shared__ int64_t si[6][kRedThreads];
+  const int t = threadIdx.x;
+  double a0 = -0.0, a1 = -0.0, a2 = -0.0;
+  int64_t c[6] = {0, 0, 0, 0, 0, 0};
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kRedEnvs + t;
+#pragma unroll
+  for (int j = 0; j < kRedPer; ++j) {
+    const int64_t i = base + j * kRedThreads;
+    if (i < n) {
+      // the record as four 16-byte loads: {ret[0], ret[1]}, {ret_main, pending}, counts 0-3, 4-7
+      const f64x2* r2 = reinterpret_cast<const f64x2*>(rec + i);
+      const f64x2 f0 = __builtin_nontemporal_load(r2), f1 = __builtin_nontemporal_load(r2 + 1);
+      const u32x4* u = reinterpret_cast<const u32x4*>(rec + i) + 2;
+      const u32x4 u0 = __builtin_nontemporal_load(u), u1 = __builtin_nontemporal_load(u + 1);
+      a0 = a0 + f0.x;
+      a1 = a1 + f0.y;
+      a2 = a2 + f1.x;
+      c[0] += u0.x;
+      c[1] += u0.y;
+      c[2] += u0.z;
+      c[3] += u0.w;
+      c[4] += u1.x;
+      c[5] += u1.y;
+    }
+  }
+  sd[0][t] = a0;
+  sd[1][t] = a1;
+  sd[2][t] = a2;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) si[k][t] = c[k];
+  red_fold(sd, si, t);
+  if (t == 0) red_store(part + blockIdx.x, sd, si);
+}
+
+__global__ __launch_bounds__(kRedThreads) void stats_reduce_final_kernel(const mg_stats_totals* part, int64_t nb,
+                                                                         mg_stats_totals* out) {
+  __shared__ double sd[3][kRedThreads];
+  __shared__ int64_t si[6][kRedThreads];
+  const int t = threadIdx.x;
+  double a[3] = {-0.0, -0.0, -0.0};
+  int64_t c[6] = {0, 0, 0, 0, 0, 0};
+  for (int64_t k = t; k < nb; k += kRedThreads) {
+    const mg_stats_totals p = part[k];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) a[q] = a[q] + p.ret[q];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) c[q] += p.counts[q];
+  }
+#pragma unroll
+  for (int q = 0; q < 3; ++q) sd[q][t] = a[q];
+#pragma unroll
+  for (int q = 0; q < 6; ++q) si[q][t] = c[q];
+  red_fold(sd, si, t);
+  if (t == 0) red_store(out, sd, si);
+}
+
 // goal_status of n (dx1, v2) pairs, the function the h-DQN kernel evaluates (tests, evaluation)
 __global__ __launch_bounds__(kBlock) void goal_status_kernel(const double* dx1, const double* v2, int8_t* out,
                                                              int64_t n) {
@@ -3320,6 +3420,30 @@ int mg_observe(const mg_params* params, const mg_state* state, const mg_outputs*
   hipLaunchKernelGGL(observe_kernel, dim3(blocks), dim3(kBlock), 0,
                      static_cast<hipStream_t>(stream), *params, *state, *out, n);
   return finish_launch("mg_observe");
+}
+
+size_t mg_stats_reduce_scratch_bytes(int64_t n) {
+  if (n <= 0) return 0;
+  return static_cast<size_t>((n + kRedEnvs - 1) / kRedEnvs) * sizeof(mg_stats_totals);
+}
+
+int mg_stats_reduce(const mg_episode_stats* rec, int64_t n, mg_stats_totals* totals, void* scratch,
+                    size_t scratch_bytes, void* stream) {
+  if (!totals || (n > 0 && !rec)) return fail(hipErrorInvalidValue, "%s", "mg_stats_reduce: NULL pointer");
+  if (n < 0) return fail(hipErrorInvalidValue, "%s", "n < 0");
+  if (((reinterpret_cast<uintptr_t>(rec) | reinterpret_cast<uintptr_t>(scratch)) & 15) ||
+      (reinterpret_cast<uintptr_t>(totals) & 7))
+    return fail(hipErrorInvalidValue, "%s", "mg_stats_reduce: rec and scratch must be 16-byte, totals 8-byte aligned");
+  const int64_t nb = (n + kRedEnvs - 1) / kRedEnvs;
+  if (nb > 0x7fffffff) return fail(hipErrorInvalidValue, "%s", "n exceeds the grid limit");
+  if (n > 0 && (!scratch || scratch_bytes < mg_stats_reduce_scratch_bytes(n)))
+    return fail(hipErrorInvalidValue, "%s", "mg_stats_reduce: scratch smaller than mg_stats_reduce_scratch_bytes(n)");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  mg_stats_totals* part = static_cast<mg_stats_totals*>(scratch);
+  if (nb > 0)
+    hipLaunchKernelGGL(stats_reduce_kernel, dim3(static_cast<unsigned>(nb)), dim3(kRedThreads), 0, st, rec, n, part);
+  hipLaunchKernelGGL(stats_reduce_final_kernel, dim3(1), dim3(kRedThreads), 0, st, part, nb, totals);
+  return finish_launch("mg_stats_reduce");
 }
 
 int mg_host_step(const mg_params* params, const mg_state* state, const int8_t* a1, const int8_t* a2,

@@ -142,6 +142,9 @@ def _load(path=LIB_PATH):
     lib.mg_host_step.argtypes = [PP, SP, _P, _P, OP, STP, _c.c_int64, _c.c_uint32]
     lib.mg_host_reset.argtypes = [PP, SP, _P, OP, _c.c_int64]
     lib.mg_host_observe.argtypes = [PP, SP, OP, _c.c_int64]
+    lib.mg_stats_reduce_scratch_bytes.argtypes = [_c.c_int64]
+    lib.mg_stats_reduce_scratch_bytes.restype = _c.c_size_t
+    lib.mg_stats_reduce.argtypes = [_P, _c.c_int64, _P, _P, _c.c_size_t, _P]
     lib.mg_time_next_launch.argtypes = [_P, _P]
     lib.mg_goal_status.argtypes = [_P, _P, _P, _c.c_int64, _P]
     lib.mg_replay_scratch_bytes.argtypes = [_c.c_int64, _c.c_int32]
@@ -153,7 +156,7 @@ def _load(path=LIB_PATH):
     for f in (lib.mg_step, lib.mg_step_random, lib.mg_reset, lib.mg_observe, lib.mg_rollout_random,
               lib.mg_time_next_launch, lib.mg_qnet_pack, lib.mg_qnet_forward, lib.mg_rollout_qnet,
               lib.mg_rollout_hdqn, lib.mg_replay_store, lib.mg_replay_sample, lib.mg_goal_status,
-              lib.mg_qnet_fragments, lib.mg_host_step, lib.mg_host_reset, lib.mg_host_observe):
+              lib.mg_qnet_fragments, lib.mg_host_step, lib.mg_host_reset, lib.mg_host_observe, lib.mg_stats_reduce):
         f.restype = _c.c_int
     v = lib.mg_abi_version()
     if v != ABI_VERSION:

@@ -76,14 +76,52 @@ NUM_RETURNS, NUM_COUNTS = 3, 6
 PARTIAL_BYTES = (NUM_RETURNS + NUM_COUNTS) * 8  # one rank's contribution to gather_episode_summary
 
 
+def _records_of(returns, counts):
+    """The [n, 8] f64 record tensor (mg_episode_stats, 64 B per env) that returns / counts are the
+    MergeVecEnv views of, or None when they are separate tensors."""
+    n = returns.shape[0]
+    if (returns.dtype.itemsize != 8 or returns.stride() != (8, 1) or counts.stride() != (16, 1)
+            or counts.data_ptr() != returns.data_ptr() + 32 or returns.storage_offset() % 8):
+        return None
+    base = returns.as_strided((n, 8), (8, 1))
+    return base if base.untyped_storage().nbytes() >= (returns.storage_offset() + 8 * n) * 8 else None
+
+
+def device_totals(records):
+    """[n, 8] f64 device records (mg_episode_stats) -> their totals as one [9] int64 device tensor,
+    summed by mg_stats_reduce in its fixed order (bit-reproducible; include/merging_hip.h). Two
+    launches on the current stream, no synchronisation."""
+    import ctypes
+
+    import torch
+
+    from . import _native
+
+    n = records.shape[0]
+    dev = records.device
+    out = torch.empty(9, dtype=torch.int64, device=dev)
+    scratch = torch.empty(max(1, (_native.lib.mg_stats_reduce_scratch_bytes(n) + 7) // 8), dtype=torch.int64,
+                          device=dev)
+    _native.check(_native.lib.mg_stats_reduce(
+        ctypes.c_void_p(records.data_ptr()), n, ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(scratch.data_ptr()),
+        scratch.numel() * 8, ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)), "mg_stats_reduce")
+    return out
+
+
 def partial_stats(returns, counts):
     """This shard's totals as one [9] int64 tensor on the stats' device: the three return sums
     (r1_accumulate, r2_accumulate, main.py's filtered ep_reward; f64, bit-preserved), then
-    episodes, collisions, ego-first arrivals, steps, main.py wins, hdqn.py wins."""
+    episodes, collisions, ego-first arrivals, steps, main.py wins, hdqn.py wins. On the GPU, for
+    MergeVecEnv's record views, one mg_stats_reduce (fixed summation order, ~64 B of reads per env);
+    other tensors (gloo tests on CPU) are summed by torch."""
     import torch
 
     if returns.shape[1] != NUM_RETURNS or counts.shape[1] != NUM_COUNTS:
         raise ValueError(f"need returns [n,{NUM_RETURNS}] and counts [n,{NUM_COUNTS}] (MergeVecEnv.returns / .counts)")
+    if returns.is_cuda:
+        rec = _records_of(returns, counts)
+        if rec is not None:
+            return device_totals(rec)
     r = returns.sum(0).contiguous().view(torch.int64)
     c = counts.to(torch.int64).sum(0)
     return torch.cat([r, c])
@@ -120,7 +158,10 @@ def gather_episode_summary(returns, counts, group=None, timings=None):
     import torch
     import torch.distributed as dist
 
-    sync = (lambda: torch.cuda.synchronize(returns.device)) if returns.is_cuda else (lambda: None)  # noqa: E731
+    # synchronise only to time the two steps apart: otherwise stream order carries the reduction
+    # into the collective, and summarize_partials' host copy waits for both
+    sync = ((lambda: torch.cuda.synchronize(returns.device)) if returns.is_cuda and timings is not None
+            else (lambda: None))  # noqa: E731
     sync()
     t0 = time.perf_counter()
     part = partial_stats(returns, counts)

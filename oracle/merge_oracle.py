@@ -446,6 +446,45 @@ def goal_status64(obs):
     return np.where(dx1 < -0.5 * v2, 0, np.where(dx1 < 0.5 * v2, 1, 2))
 
 
+def stats_reduce_fixed(records):
+    """mg_stats_reduce's totals (include/merging_hip.h, merging_hip.hip stats_reduce_kernel) restated
+    in numpy, operation for operation: records [n, 8] f64 (the 64-byte mg_episode_stats rows) ->
+    (three f64 sums of ret[0], ret[1], ret_main; six int64 counts). Blocks of 1,024 records; thread t
+    of 256 adds records t, t + 256, t + 512, t + 768 of its block onto -0.0 in that order; the 256
+    values fold in halves (v[t] + v[t + o], o = 128 ... 1); the block partials the same way, thread t
+    adding partials t, t + 256, ... in order. Padding is -0.0, the exact additive identity. The
+    logging loops this replaces (hdqn.py:330-346, main.py:221-228) keep running sums per episode;
+    their order is not reproducible across a parallel batch, this one is."""
+    rec = np.ascontiguousarray(records, np.float64).reshape(-1, 8)
+    n = rec.shape[0]
+    cnt = rec[:, 4:].copy().view(np.uint32)[:, :6].astype(np.int64).sum(0)
+
+    def fold(v):  # [..., 256] -> [...]
+        o = v.shape[-1] // 2
+        while o >= 1:
+            v = v[..., :o] + v[..., o:2 * o]
+            o //= 2
+        return v[..., 0]
+
+    nb = (n + 1023) // 1024
+    sums = []
+    for k in range(3):
+        col = np.full(max(nb, 1) * 1024, -0.0)
+        col[:n] = rec[:, k]
+        x = col.reshape(-1, 4, 256)
+        acc = ((x[:, 0] + x[:, 1]) + x[:, 2]) + x[:, 3]  # (-0.0 + x0) = x0 exactly
+        part = fold(acc)[:nb]
+        m = max(1, (nb + 255) // 256)
+        p = np.full(m * 256, -0.0)
+        p[:nb] = part
+        p = p.reshape(m, 256)
+        a = np.full(256, -0.0)
+        for row in p:
+            a = a + row
+        sums.append(float(fold(a)))
+    return sums, [int(c) for c in cnt]
+
+
 def oracle_envs_from(coracle, state, idx=None):
     """C-oracle envs holding a device batch's state (MergeVecEnv or its state_dict), for replaying
     it from mid-episode: positions, speeds, returns, step count, winner, the float clock the

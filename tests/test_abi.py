@@ -21,7 +21,8 @@ def test_header_declares_the_step_path():
             "mg_last_error", "mg_params_default", "mg_rollout_random", "mg_rollout_qnet",
             "mg_qnet_pack", "mg_qnet_forward", "mg_qnet_packed_bytes", "mg_replay_store",
             "mg_replay_sample", "mg_replay_scratch_bytes", "mg_goal_status", "mg_qnet_fragments",
-            "mg_qnet_fragment_bytes"} <= _declared()
+            "mg_qnet_fragment_bytes", "mg_host_step", "mg_host_reset", "mg_host_observe", "mg_stats_reduce",
+            "mg_stats_reduce_scratch_bytes", "mg_build_info"} <= _declared()
 
 
 def test_library_exports_every_declared_symbol():
@@ -44,6 +45,7 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_native.Transitions) == 12 * 8
     assert ctypes.sizeof(_native.Stats) == 8
     assert ctypes.sizeof(_native.HdqnTraj) == 6 * 8
+    assert ctypes.sizeof(_native.Rec64) == 168
     assert _native.EPISODE_STATS_BYTES == 64  # mg_episode_stats: 4 f64 + 8 u32 (ABI 17)
     assert _native.EPISODE_STATS_DTYPE.fields["counts"][1] == 32
     assert _native.REC64_DTYPE.itemsize == 168
@@ -188,6 +190,13 @@ def test_argument_errors_without_gpu():
     # 65536 write blocks in 1024 scan groups: ticket (8) + bases u64 + offsets u32 + totals u32
     assert _native.lib.mg_replay_scratch_bytes(1 << 20, 16) == 8 + 1024 * 8 + 65536 * 4 + 1024 * 4
     assert _native.lib.mg_replay_scratch_bytes(0, 4) == 0
+    # the statistics reduction (ABI 20): one 72-byte partial per 1,024 records; NULL / misaligned refused
+    assert _native.lib.mg_stats_reduce_scratch_bytes(1 << 20) == 1024 * 72
+    assert _native.lib.mg_stats_reduce_scratch_bytes(1025) == 2 * 72 and _native.lib.mg_stats_reduce_scratch_bytes(0) == 0
+    assert _native.lib.mg_stats_reduce(fake, 4, None, fake, 1 << 20, None) != 0 and b"NULL" in _native.lib.mg_last_error()
+    assert _native.lib.mg_stats_reduce(fake, 4, fake, fake, 8, None) != 0 and b"scratch" in _native.lib.mg_last_error()
+    assert _native.lib.mg_stats_reduce(odd, 4, fake, fake, 1 << 20, None) != 0
+    assert b"aligned" in _native.lib.mg_last_error()
 
 
 def test_empty_batches_are_no_ops_without_gpu():

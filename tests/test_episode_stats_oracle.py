@@ -143,3 +143,49 @@ def test_goal_status_rows(g):
     f32 = np.where(dx1.astype(np.float32) < np.float32(-0.5) * v2.astype(np.float32), 0,
                    np.where(dx1.astype(np.float32) < np.float32(0.5) * v2.astype(np.float32), 1, 2))
     assert (f32 != st).sum() > 10  # the rows do separate fp64 from fp32 evaluation
+
+
+def test_stats_reduce_restatement_order():
+    """merge_oracle.stats_reduce_fixed (the checker of mg_stats_reduce) against a scalar loop written
+    from the header's description (include/merging_hip.h mg_stats_reduce): thread-strided adds onto
+    -0.0, then the halving fold, per block and over the block partials."""
+    import numpy as np
+
+    import merge_oracle as mo
+
+    def fold(v):
+        v = list(v)
+        o = len(v) // 2
+        while o:
+            v = [v[t] + v[t + o] for t in range(o)]
+            o //= 2
+        return v[0]
+
+    def scalar(col):
+        n = len(col)
+        parts = []
+        for b in range((n + 1023) // 1024):
+            th = []
+            for t in range(256):
+                a = -0.0
+                for j in range(4):
+                    i = b * 1024 + j * 256 + t
+                    if i < n:
+                        a = a + col[i]
+                th.append(a)
+            parts.append(fold(th))
+        th = []
+        for t in range(256):
+            a = -0.0
+            for k in range(t, len(parts), 256):
+                a = a + parts[k]
+            th.append(a)
+        return fold(th)
+
+    rng = np.random.default_rng(4)
+    for n in (0, 5, 1024, 3000):
+        rec = rng.normal(0, 1, (n, 8)) * 10.0 ** rng.integers(-9, 5, (n, 8))
+        sums, _ = mo.stats_reduce_fixed(rec)
+        for k in range(3):
+            ref = scalar(rec[:, k].tolist())
+            assert np.float64(sums[k]).view(np.uint64) == np.float64(ref).view(np.uint64), (n, k)
