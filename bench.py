@@ -755,6 +755,9 @@ def main():
         episodes = gather_episode_summary(env.returns, env.counts, timings=timings)
         payload = PARTIAL_BYTES if world > 1 else 0
     episodes.update(allgather_ms=timings.get("allgather_ms"), reduce_ms=timings.get("reduce_ms"),
+                    reduce_wall_ms=timings.get("reduce_wall_ms"),
+                    reduce_how=("mg_stats_reduce, fixed order (64 B of records per env): reduce_ms = HIP events "
+                                "around its two launches, reduce_wall_ms = the Python call on the host clock"),
                     allgather_bytes_per_rank=payload,
                     completed_in_timed_window_rank0=completed_in_window,
                     counted_since="start of the timed window (statistics cleared after the warm-up)",

@@ -87,6 +87,9 @@ def _records_of(returns, counts):
     return base if base.untyped_storage().nbytes() >= (returns.storage_offset() + 8 * n) * 8 else None
 
 
+_SCRATCH = {}  # device -> mg_stats_reduce scratch (block partials)
+
+
 def device_totals(records):
     """[n, 8] f64 device records (mg_episode_stats) -> their totals as one [9] int64 device tensor,
     summed by mg_stats_reduce in its fixed order (bit-reproducible; include/merging_hip.h). Two
@@ -100,8 +103,10 @@ def device_totals(records):
     n = records.shape[0]
     dev = records.device
     out = torch.empty(9, dtype=torch.int64, device=dev)
-    scratch = torch.empty(max(1, (_native.lib.mg_stats_reduce_scratch_bytes(n) + 7) // 8), dtype=torch.int64,
-                          device=dev)
+    words = max(1, (_native.lib.mg_stats_reduce_scratch_bytes(n) + 7) // 8)
+    scratch = _SCRATCH.get(dev)
+    if scratch is None or scratch.numel() < words:  # one buffer per device, reused (stream-ordered)
+        scratch = _SCRATCH[dev] = torch.empty(words, dtype=torch.int64, device=dev)
     _native.check(_native.lib.mg_stats_reduce(
         ctypes.c_void_p(records.data_ptr()), n, ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(scratch.data_ptr()),
         scratch.numel() * 8, ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)), "mg_stats_reduce")
@@ -151,8 +156,9 @@ def summarize_partials(parts):
 def gather_episode_summary(returns, counts, group=None, timings=None):
     """All-gather every rank's 72-byte partial totals and reduce them: the global summary on
     every rank (the default collective of a sharded run). timings (a dict, optional) receives
-    "reduce_ms" (this shard's device reduction to its partial totals, synchronised) and
-    "allgather_ms" (the collective alone; None without one, world size 1)."""
+    "reduce_ms" (this shard's reduction to its partial totals: HIP events around its launches on
+    the GPU), "reduce_wall_ms" (the same call on the host clock, synchronised: Python and launch
+    overheads included) and "allgather_ms" (the collective alone; None without one, world size 1)."""
     import time
 
     import torch
@@ -162,14 +168,22 @@ def gather_episode_summary(returns, counts, group=None, timings=None):
     # into the collective, and summarize_partials' host copy waits for both
     sync = ((lambda: torch.cuda.synchronize(returns.device)) if returns.is_cuda and timings is not None
             else (lambda: None))  # noqa: E731
+    events = None
+    if timings is not None and returns.is_cuda:
+        events = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     sync()
     t0 = time.perf_counter()
+    if events:
+        events[0].record()
     part = partial_stats(returns, counts)
+    if events:
+        events[1].record()
     sync()
     t1 = time.perf_counter()
     world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
     if timings is not None:
-        timings["reduce_ms"] = (t1 - t0) * 1e3
+        timings["reduce_wall_ms"] = (t1 - t0) * 1e3
+        timings["reduce_ms"] = events[0].elapsed_time(events[1]) if events else timings["reduce_wall_ms"]
         timings["allgather_ms"] = None
     if world == 1:
         return summarize_partials(part)
