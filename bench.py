@@ -7,7 +7,7 @@ A step = one launch of mg_step_random over this rank's 2^20 envs: Philox actions
 players drawn on the device, the full reference step (merging_env.py:138-195), autoreset,
 episode statistics. Envs are sharded across ranks (rank r owns global envs [r E, (r+1) E),
 Philox keyed by the global index), with no collective inside the timed loop; after it, one
-RCCL all-gather of each rank's 72-byte statistics totals (timed separately).
+RCCL all-gather of each rank's 80-byte statistics totals (timed separately).
 
 Before the W warm-up steps the batch is burned in (--burn-in-launches untimed one-step launches
 of the same kernel, optionally preceded by --burn-in steps of fused rollouts) so the timed window
@@ -83,7 +83,7 @@ def parse():
                     help="allocate the 2^22 leg's env before the other legs, whenever it runs (A/B of where "
                          "its memory lands)")
     ap.add_argument("--gather", choices=("summary", "per-env"), default="summary",
-                    help="statistics collective: 72-byte totals per rank, or every env's row")
+                    help="statistics collective: 80-byte totals per rank, or every env's row")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="per CPU-baseline leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="skip per-launch HIP events")
@@ -336,6 +336,7 @@ def qnet_leg(env, args, world, dist, torch, opponent):
         env.rollout_qnet(T, qnet, args.seed, opponent=opponent, first_step=k, final_observation=False,
                          won_mask=False)
         k += T
+    env.clear_statistics()  # the leg's own episodes: main.py's logged quantities, q_eval included
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     if world > 1:
@@ -366,7 +367,10 @@ def qnet_leg(env, args, world, dist, torch, opponent):
     h = torch.relu(x @ w["fc1.weight"].T + w["fc1.bias"])
     h = torch.relu(h @ w["fc2.weight"].T + w["fc2.bias"])
     greedy_cpu = (h @ w["out.weight"].T + w["out.bias"]).argmax(1)
-    return {"kernel": f"qnet_rollout_ws_kernel<{ {'none': '0, false', 'uniform': '1, false', 'self': '2, true', 'other': '3, true'}[label] }>",
+    summ = env.episode_summary()  # untimed: mg_stats_reduce over the records of the timed launches
+    return {"episodes": {k: summ[k] for k in ("completed", "mean_q_eval", "mean_ep_reward_main", "win_rate_main",
+                                               "collision_rate")},
+            "q_eval_logged_as": "eval_net(state)[action] on each episode's last input and action (main.py:221)","kernel": f"qnet_rollout_ws_kernel<{ {'none': '0, false', 'uniform': '1, false', 'self': '2, true', 'other': '3, true'}[label] }>",
             "opponent": label if label != "other" else "other net (main.py Strategy_OP L1; checkpoint l3)",
             "steps_per_launch": T, "launches": L, "dtype": "bf16 (fp32 accumulate)",
             "value": world * E * T * L / elapsed, "unit": "env-steps/s",
@@ -413,6 +417,7 @@ def hdqn_leg(env, args, world, dist, torch):
     for _ in range(max(1, args.leg_warmup)):
         env.rollout_hdqn(T, meta, lower, args.seed, first_step=k, final_observation=False)
         k += T
+    env.clear_statistics()  # the leg's own episodes: hdqn.py's logged quantities, q_eval included
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     if world > 1:
@@ -429,6 +434,8 @@ def hdqn_leg(env, args, world, dist, torch):
     elapsed = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / L
     per_s = E * T / (kernel_ms * 1e-3)
+    summ = env.episode_summary()  # untimed: the timed launches' episodes (mg_stats_reduce)
+    episodes = {k: summ[k] for k in ("completed", "mean_q_eval", "mean_return_ego", "win_rate_hdqn", "collision_rate")}
     # untimed: one launch with Goal_DQN's columns, for the inner-loop break rate (:322)
     tr = env.rollout_hdqn(T, meta, lower, args.seed, first_step=k, final_observation=False, goal_memory=True)
     k += T
@@ -510,7 +517,9 @@ def hdqn_leg(env, args, world, dist, torch):
             "mfma_tflops": 2 * QNET_MFMA_FLOP * per_s / 1e12, "sustained_tflops": MFMA_BF16_SUSTAINED_TFLOPS,
             "mfma_frac_of_sustained": 2 * QNET_MFMA_FLOP * per_s / 1e12 / MFMA_BF16_SUSTAINED_TFLOPS,
             "nets": "seeded, torch.nn.Linear default init U(-1/sqrt(in), 1/sqrt(in)) (signed)",
-            "goal_break_rate_per_step": break_rate, "next_goal_share": greedy_goal_spread}
+            "goal_break_rate_per_step": break_rate, "next_goal_share": greedy_goal_spread,
+            "episodes": episodes,
+            "q_eval_logged_as": "meta_eval_net(state)[goal] on each episode's terminal state and its goal (hdqn.py:330)"}
 
 
 def replay_algorithmic_bytes(n, T, kept, done_rows, capacity):
@@ -734,7 +743,7 @@ def main():
     elapsed, kernel_ms_max = float(t[0]), float(t[1])
 
     # episode statistics (every episode completed since the window opened), the quantities the
-    # reference's scripts log: each rank reduces its shard on the device to 72 bytes of totals,
+    # reference's scripts log: each rank reduces its shard on the device to 80 bytes of totals,
     # which one RCCL all-gather (xGMI) brings to every rank, outside the timed loop. The device
     # reduction and the collective are timed apart; at world size 1 there is no collective.
     from merging_gym.distributed import (NUM_COUNTS, NUM_RETURNS, PARTIAL_BYTES, gather_episode_stats,

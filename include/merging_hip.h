@@ -242,7 +242,12 @@ typedef struct mg_episode_stats {
   uint32_t steps;       /* total steps of the completed episodes */
   uint32_t win_main;    /* main.py:225's win test on the pre-terminal observation */
   uint32_t win_hdqn;    /* hdqn.py:342's win test on the terminal observation */
-  uint32_t reserved[2]; /* 0 */
+  double q_eval;        /* (ABI 20; reserved zero bytes until ABI 19) sum over the completed episodes
+                           of the Q value the scripts log for each (q_eval_value): the fused policy
+                           kernels add eval_net(state)[action] on the last step's input and action
+                           (mg_rollout_qnet, main.py:221) or meta_eval_net(state)[goal] on the terminal
+                           state and the goal chosen on it (mg_rollout_hdqn, hdqn.py:330); the kernels
+                           without a net leave it unchanged */
 } mg_episode_stats;
 
 typedef struct mg_stats {
@@ -250,10 +255,11 @@ typedef struct mg_stats {
 } mg_stats;
 
 /* (ABI 20) The records of a batch summed: what the logging loops of scripts/hdqn.py:330-346 and
- * scripts/main.py:221-228 total over completed episodes. 72 bytes, the per-rank contribution of the
- * multi-GPU statistics all-gather (merging_gym/distributed.py). */
+ * scripts/main.py:221-228 total over completed episodes: the per-rank contribution of the
+ * multi-GPU statistics all-gather (merging_gym/distributed.py), 80 bytes. */
 typedef struct mg_stats_totals {
   double ret[3];      /* sums of ret[0], ret[1], ret_main */
+  double q_eval;      /* sum of q_eval */
   int64_t counts[6];  /* sums of episodes, collisions, ego_first, steps, win_main, win_hdqn */
 } mg_stats_totals;
 

@@ -49,7 +49,6 @@ constexpr int kObs = MG_OBS_DIM;
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // Store of a per-step output (observation, reward, flags, actions): written once, never
 // re-read by the step, so optionally non-temporal. The env state is stored normally: the
@@ -605,6 +604,13 @@ MG_HD void note_first_arrival(const mg_stats& St, int64_t i, const StepOut& r,
   } else if (St.rec) {
     reinterpret_cast<double*>(St.rec + i)[3] = r.ret_pre;  // ret1_pending
   }
+}
+
+// The Q value the scripts log for a finished episode (q_eval_value, main.py:221, hdqn.py:330),
+// added to the env's record (mg_episode_stats.q_eval) by the env's only writer of that field.
+MG_HD void stats_add_q_eval(const mg_stats& St, int64_t i, double q) {
+  double* f = &St.rec[i].q_eval;
+  *f = *f + q;
 }
 
 // gym.vector autoreset: record the finished episode, keep its terminal observation, reset
@@ -1696,11 +1702,13 @@ struct QRollout {
 // explore draw, u.y its random action, u.z the opponent's explore draw, u.w its random action. Envs
 // past n (live[j] false) are stepped too but never stored. A greedy action outside 0..4 (a
 // net with out_dim > 5) gets env_step's KeyError semantics (env_step_lockstep).
+// qrow: the tile row of env i0 (rows of envs i0 + 64 j follow 64 rows apart), where the Q-net wave
+// left eval_net(state)[0..4] of the state the step acts on: a finishing env logs q[a1] (main.py:221).
 template <int OPP, int N, bool CHECKED>
 __device__ __forceinline__ void qnet_policy_step_n(const QRollout& R, Env (&e)[N], StepOut (&r)[N],
                                                    int64_t i0, const bool (&live)[N], int t,
                                                    const int (&greedy1)[N], const int (&greedy2)[N],
-                                                   bool (&won)[N]) {
+                                                   bool (&won)[N], const float* qrow) {
   const uint64_t step = R.first_step + t;
   int a1[N], a2[N];
 #pragma unroll
@@ -1728,8 +1736,10 @@ __device__ __forceinline__ void qnet_policy_step_n(const QRollout& R, Env (&e)[N
              f32x2{static_cast<float>(r[j].r1), static_cast<float>(r[j].r2)});
     store_step_bytes(R.T, row, a1[j], a2[j], r[j].done, r[j].coll);
     won[j] = e[j].winner == 1;
+    const bool finish = (R.flags & MG_AUTORESET) && r[j].done;
     after_step(R.P, e[j], r[j], R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i,
                (R.flags & MG_AUTORESET) != 0);
+    if (finish && R.St.rec) stats_add_q_eval(R.St, i, qrow[64 * j * kObs + a1[j]]);  // a1 in 0..4 here
   }
 }
 
@@ -1820,15 +1830,23 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
         for (int tt = 0; tt < kTiles; ++tt) {
           const int row0 = (p & 1) * kHalf + (4 * tt + wave) * 64;
           float q[8];
+          if constexpr (OPP >= 2) {  // the opponent's view state[5:] + state[:5] (main.py:199)
+            qnet_forward_swp(OPP == 3 ? lds_net2 : lds_net, tile, row0, true, q);
+            greedy[1][row0 + lane] = static_cast<uint8_t>(argmax_first(q, R.out_dim));
+          }
           if constexpr (kNet32)
             qnet32_forward(lds_net, tile, row0, false, q);
           else
             qnet_forward_swp(lds_net, tile, row0, false, q);
           greedy[0][row0 + lane] = static_cast<uint8_t>(argmax_first(q, R.out_dim));
-          if constexpr (OPP >= 2) {  // the opponent's view state[5:] + state[:5] (main.py:199)
-            qnet_forward_swp(OPP == 3 ? lds_net2 : lds_net, tile, row0, true, q);
-            greedy[1][row0 + lane] = static_cast<uint8_t>(argmax_first(q, R.out_dim));
-          }
+          // eval_net(state)[0..4] into the env's tile row, whose observation both forwards have
+          // read (the MFMA chain behind q waits for every read): the env wave steps the env in the
+          // next phase and logs q[action] when the episode ends (main.py:221), before it writes
+          // the next observation into the row
+          float* qr = tile + (row0 + lane) * kObs;
+          reinterpret_cast<f32x2*>(qr)[0] = f32x2{q[0], q[1]};
+          reinterpret_cast<f32x2*>(qr)[1] = f32x2{q[2], q[3]};
+          qr[4] = q[4];
         }
       }
       __syncthreads();
@@ -1861,10 +1879,11 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
       }
       bool won[kIlp];
       // wave-uniform branch: each group's envs stay in named registers
+      const float* qrow = tile + (local0 + lane) * kObs;
       if (g == 0)
-        qnet_policy_step_n<OPP, kIlp, CHECKED>(R, e0, r, base + local0 + lane, live0, t, greedy1, greedy2, won);
+        qnet_policy_step_n<OPP, kIlp, CHECKED>(R, e0, r, base + local0 + lane, live0, t, greedy1, greedy2, won, qrow);
       else
-        qnet_policy_step_n<OPP, kIlp, CHECKED>(R, e1, r, base + local0 + lane, live1, t, greedy1, greedy2, won);
+        qnet_policy_step_n<OPP, kIlp, CHECKED>(R, e1, r, base + local0 + lane, live1, t, greedy1, greedy2, won, qrow);
       const int64_t wbase = base + local0;
 #pragma unroll
       for (int j = 0; j < kIlp; ++j) {
@@ -2030,6 +2049,7 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
       int goal_t;
       const bool need_meta = t > 0 || __ballot(live && goal_prev < 0) != 0;
       int gstar = 0;
+      float qe = 0.f;  // meta_eval_net(terminal state)[goal chosen on it], logged at an episode end (:330)
       if (need_meta) {  // meta-net on the next state of step t - 1 (on s_0 for a launch's first goals)
         const bool d0 = t > 0 && b_done[row0 + r], d1 = t > 0 && b_done[row0 + 32 + r];
         const bf16x8 x0 = d0 ? qnet_input_pairs(side + (row0 + r) * 5, h)
@@ -2039,6 +2059,10 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
         float q[8];
         qnet_mlp_swp(lds_meta, x0, x1, q);
         gstar = argmax_first(q, R.num_goals);
+        const int dg = b_dg[j];
+        const int g2 = dg == kHGreedy ? gstar : dg;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) qe = k == g2 ? q[k] : qe;
       }
       const int df = b_df[j];
       bool brk = false;  // step t - 1 left the inner loop (:322): a new outer iteration starts
@@ -2054,6 +2078,9 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
           if (R.H.reward) st_out(R.H.reward + row, goal2 == b_st_old[j] ? 1.0f : 0.0f);
         }
         b_g2[j] = static_cast<uint8_t>(goal2);  // for the fused ring row of step t - 1
+        // the episode's q_eval (hdqn.py:330): the env wave recorded the episode in E(X, t - 1); this
+        // lane is the only writer of the field, so no-return atomics keep the adds in step order
+        if (done && live && R.St.rec) unsafeAtomicAdd(&R.St.rec[i].q_eval, static_cast<double>(qe));
       } else {
         goal_t = goal_prev >= 0 ? goal_prev : (df == kHGreedy ? gstar : df);
       }
@@ -2797,12 +2824,14 @@ void mpc_qp_constants(double t, double* nz_out, double* z0_out, double* vsmall_o
 //          identity), then the block folds its kRedThreads values in halves (v[t] += v[t + o],
 //          o = 128, 64, ..., 1) -> partial b;
 //   pass 2 (one block): thread t adds partials t, t + 256, ... in order onto -0.0, then the same fold.
-// The counts are exact int64 sums. Replaces the logging loops' running totals (hdqn.py:330-346,
+// The counts are exact int64 sums; the fp64 ones are ret[0], ret[1], ret_main and q_eval. Replaces the logging loops' running totals (hdqn.py:330-346,
 // main.py:221-228) for a whole batch; a torch sum over strided record columns took 7.6 ms at 2^20
 // envs (BENCH_r03 episodes.reduce_ms) for 64 MB of records.
 constexpr int kRedThreads = 256;
 constexpr int kRedPer = 4;
 constexpr int kRedEnvs = kRedThreads * kRedPer;  // 1,024 records (64 KB) per pass-1 block
+
+constexpr int kRedSums = 4;  // ret[0], ret[1], ret_main, q_eval
 
 __device__ __forceinline__ void red_fold(double (*sd)[kRedThreads], int64_t (*si)[kRedThreads], int t) {
 #pragma unroll
@@ -2810,7 +2839,7 @@ __device__ __forceinline__ void red_fold(double (*sd)[kRedThreads], int64_t (*si
     __syncthreads();
     if (t < o) {
 #pragma unroll
-      for (int k = 0; k < 3; ++k) sd[k][t] = sd[k][t] + sd[k][t + o];
+      for (int k = 0; k < kRedSums; ++k) sd[k][t] = sd[k][t] + sd[k][t + o];
 #pragma unroll
       for (int k = 0; k < 6; ++k) si[k][t] += si[k][t + o];
     }
@@ -2823,6 +2852,7 @@ __device__ __forceinline__ void red_store(mg_stats_totals* out, double (*sd)[kRe
   mg_stats_totals o;
 #pragma unroll
   for (int k = 0; k < 3; ++k) o.ret[k] = sd[k][0];
+  o.q_eval = sd[3][0];
 #pragma unroll
   for (int k = 0; k < 6; ++k) o.counts[k] = si[k][0];
   *out = o;
@@ -2830,10 +2860,10 @@ __device__ __forceinline__ void red_store(mg_stats_totals* out, double (*sd)[kRe
 
 __global__ __launch_bounds__(kRedThreads) void stats_reduce_kernel(const mg_episode_stats* rec, int64_t n,
                                                                    mg_stats_totals* part) {
-  __shared__ double sd[3][kRedThreads];
+  __shared__ double sd[kRedSums][kRedThreads];
   __shared__ int64_t si[6][kRedThreads];
   const int t = threadIdx.x;
-  double a0 = -0.0, a1 = -0.0, a2 = -0.0;
+  double a0 = -0.0, a1 = -0.0, a2 = -0.0, a3 = -0.0;
   int64_t c[6] = {0, 0, 0, 0, 0, 0};
   const int64_t base = static_cast<int64_t>(blockIdx.x) * kRedEnvs + t;
 #pragma unroll
@@ -2848,6 +2878,7 @@ __global__ __launch_bounds__(kRedThreads) void stats_reduce_kernel(const mg_epis
       a0 = a0 + f0.x;
       a1 = a1 + f0.y;
       a2 = a2 + f1.x;
+      a3 = a3 + __builtin_bit_cast(double, (static_cast<uint64_t>(u1.w) << 32) | u1.z);
       c[0] += u0.x;
       c[1] += u0.y;
       c[2] += u0.z;
@@ -2859,6 +2890,7 @@ __global__ __launch_bounds__(kRedThreads) void stats_reduce_kernel(const mg_epis
   sd[0][t] = a0;
   sd[1][t] = a1;
   sd[2][t] = a2;
+  sd[3][t] = a3;
 #pragma unroll
   for (int k = 0; k < 6; ++k) si[k][t] = c[k];
   red_fold(sd, si, t);
@@ -2867,20 +2899,21 @@ __global__ __launch_bounds__(kRedThreads) void stats_reduce_kernel(const mg_epis
 
 __global__ __launch_bounds__(kRedThreads) void stats_reduce_final_kernel(const mg_stats_totals* part, int64_t nb,
                                                                          mg_stats_totals* out) {
-  __shared__ double sd[3][kRedThreads];
+  __shared__ double sd[kRedSums][kRedThreads];
   __shared__ int64_t si[6][kRedThreads];
   const int t = threadIdx.x;
-  double a[3] = {-0.0, -0.0, -0.0};
+  double a[kRedSums] = {-0.0, -0.0, -0.0, -0.0};
   int64_t c[6] = {0, 0, 0, 0, 0, 0};
   for (int64_t k = t; k < nb; k += kRedThreads) {
     const mg_stats_totals p = part[k];
 #pragma unroll
     for (int q = 0; q < 3; ++q) a[q] = a[q] + p.ret[q];
+    a[3] = a[3] + p.q_eval;
 #pragma unroll
     for (int q = 0; q < 6; ++q) c[q] += p.counts[q];
   }
 #pragma unroll
-  for (int q = 0; q < 3; ++q) sd[q][t] = a[q];
+  for (int q = 0; q < kRedSums; ++q) sd[q][t] = a[q];
 #pragma unroll
   for (int q = 0; q < 6; ++q) si[q][t] = c[q];
   red_fold(sd, si, t);

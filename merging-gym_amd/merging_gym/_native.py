@@ -71,11 +71,13 @@ class Stats(_c.Structure):
     _fields_ = [("rec", _P)]  # mg_episode_stats [n] (64 bytes each, see EPISODE_STATS_DTYPE)
 
 
-# numpy view of struct mg_episode_stats (ABI 17): the fp64 sums, main.py's pending r1_accumulate,
-# then the counts (episodes, collisions, ego_first, steps, win_main, win_hdqn) and two reserved
+# numpy view of struct mg_episode_stats (ABI 20): the fp64 sums, main.py's pending r1_accumulate,
+# the counts (episodes, collisions, ego_first, steps, win_main, win_hdqn), then the q_eval sum
+# (reserved zero bytes in ABI 17-19)
 EPISODE_STATS_DTYPE = np.dtype([("ret", np.float64, (2,)), ("ret_main", np.float64),
                                 ("ret1_pending", np.float64), ("counts", np.uint32, (6,)),
-                                ("reserved", np.uint32, (2,))])
+                                ("q_eval", np.float64)])
+EPISODE_STATS_FORMAT = 2  # state_dict tag: 1 = ABI 17-19 records (no q_eval), 2 = ABI 20
 EPISODE_STATS_BYTES = 64
 assert EPISODE_STATS_DTYPE.itemsize == EPISODE_STATS_BYTES
 

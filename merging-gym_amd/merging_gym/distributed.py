@@ -4,11 +4,12 @@ Envs never interact, so the step needs no exchange: rank r owns global envs
 [offset, offset + count) and steps them alone (MergeVecEnv(env_offset=offset) keys its
 Philox stream by the global index, so a sharded run draws exactly the unsharded actions).
 The only collective is reducing completed-episode statistics after a rollout: by default
-each rank contributes its shard's nine totals (three return sums as f64 bits -- both players'
-r_accumulate and main.py's winner-filtered ep_reward -- and episodes / collisions / ego-first
-arrivals / steps / main.py wins / hdqn.py wins as int64: 72 bytes) to one all-gather over RCCL
-(torch backend "nccl" on ROCm, xGMI between MI355X GPUs), and every rank reduces the [world, 9]
-result in rank order (the quantities hdqn.py:330-346 and main.py:221-228 log).
+each rank contributes its shard's ten totals (four sums as f64 bits -- both players'
+r_accumulate, main.py's winner-filtered ep_reward and the logged q_eval -- and episodes /
+collisions / ego-first arrivals / steps / main.py wins / hdqn.py wins as int64: 80 bytes, summed on
+the device by mg_stats_reduce in a fixed order) to one all-gather over RCCL (torch backend "nccl"
+on ROCm, xGMI between MI355X GPUs), and every rank reduces the [world, 10] result in rank order
+(the quantities hdqn.py:330-346 and main.py:221-228 log).
 `gather_episode_stats` gathers the per-env rows instead ([N/W, 6] int64 per rank), for a caller
 that needs them. gloo carries the same calls on CPU tensors in tests.
 """
@@ -73,7 +74,8 @@ def all_gather_rows(rows, group=None):
 
 
 NUM_RETURNS, NUM_COUNTS = 3, 6
-PARTIAL_BYTES = (NUM_RETURNS + NUM_COUNTS) * 8  # one rank's contribution to gather_episode_summary
+NUM_SUMS = NUM_RETURNS + 1  # the return sums and the q_eval sum (mg_stats_totals)
+PARTIAL_BYTES = (NUM_SUMS + NUM_COUNTS) * 8  # one rank's contribution to gather_episode_summary: 80
 
 
 def _records_of(returns, counts):
@@ -91,7 +93,7 @@ _SCRATCH = {}  # device -> mg_stats_reduce scratch (block partials)
 
 
 def device_totals(records):
-    """[n, 8] f64 device records (mg_episode_stats) -> their totals as one [9] int64 device tensor,
+    """[n, 8] f64 device records (mg_episode_stats) -> their totals as one [10] int64 device tensor,
     summed by mg_stats_reduce in its fixed order (bit-reproducible; include/merging_hip.h). Two
     launches on the current stream, no synchronisation."""
     import ctypes
@@ -102,7 +104,7 @@ def device_totals(records):
 
     n = records.shape[0]
     dev = records.device
-    out = torch.empty(9, dtype=torch.int64, device=dev)
+    out = torch.empty(NUM_SUMS + NUM_COUNTS, dtype=torch.int64, device=dev)
     words = max(1, (_native.lib.mg_stats_reduce_scratch_bytes(n) + 7) // 8)
     scratch = _SCRATCH.get(dev)
     if scratch is None or scratch.numel() < words:  # one buffer per device, reused (stream-ordered)
@@ -113,9 +115,10 @@ def device_totals(records):
     return out
 
 
-def partial_stats(returns, counts):
-    """This shard's totals as one [9] int64 tensor on the stats' device: the three return sums
-    (r1_accumulate, r2_accumulate, main.py's filtered ep_reward; f64, bit-preserved), then
+def partial_stats(returns, counts, q_eval=None):
+    """This shard's totals as one [10] int64 tensor on the stats' device: the three return sums
+    (r1_accumulate, r2_accumulate, main.py's filtered ep_reward; f64, bit-preserved), the q_eval sum
+    (the record's own for MergeVecEnv's views; else the q_eval [n] tensor given, or 0), then
     episodes, collisions, ego-first arrivals, steps, main.py wins, hdqn.py wins. On the GPU, for
     MergeVecEnv's record views, one mg_stats_reduce (fixed summation order, ~64 B of reads per env);
     other tensors (gloo tests on CPU) are summed by torch."""
@@ -127,34 +130,39 @@ def partial_stats(returns, counts):
         rec = _records_of(returns, counts)
         if rec is not None:
             return device_totals(rec)
-    r = returns.sum(0).contiguous().view(torch.int64)
+    rec = _records_of(returns, counts)
+    if q_eval is None and rec is not None:
+        q_eval = rec[:, 7]
+    r = returns.sum(0)
+    q = q_eval.sum().reshape(1).to(r) if q_eval is not None else torch.zeros(1, dtype=r.dtype, device=r.device)
     c = counts.to(torch.int64).sum(0)
-    return torch.cat([r, c])
+    return torch.cat([torch.cat([r, q]).contiguous().view(torch.int64), c])
 
 
 def summarize_partials(parts):
-    """[world, 9] partial totals (partial_stats rows) -> the summary dict, reduced in rank order:
+    """[world, 10] partial totals (partial_stats rows) -> the summary dict, reduced in rank order:
     the quantities the reference's scripts log per episode, as rates / means over all completed
     episodes -- hdqn.py:330-346 (reward = r1_accumulate, collision_rate, win_rate on the terminal
     observation) and main.py:221-228 (reward = the winner-filtered ep_reward, win on the
     pre-terminal observation) -- plus the ego-first rate (winner == 1) and the mean length."""
     import torch
 
-    w = NUM_RETURNS + NUM_COUNTS
+    w = NUM_SUMS + NUM_COUNTS
     parts = parts.reshape(-1, w).cpu()
-    r = parts[:, :NUM_RETURNS].contiguous().view(torch.float64)
-    c = parts[:, NUM_RETURNS:].sum(0).tolist()
-    sums = [0.0] * NUM_RETURNS
+    r = parts[:, :NUM_SUMS].contiguous().view(torch.float64)
+    c = parts[:, NUM_SUMS:].sum(0).tolist()
+    sums = [0.0] * NUM_SUMS
     for row in r.tolist():
         sums = [a + b for a, b in zip(sums, row)]
     ep = max(c[0], 1)
     return {"completed": c[0], "mean_return_ego": sums[0] / ep, "mean_return_opp": sums[1] / ep,
             "mean_ep_reward_main": sums[2] / ep, "collision_rate": c[1] / ep, "ego_first_rate": c[2] / ep,
-            "win_rate_main": c[4] / ep, "win_rate_hdqn": c[5] / ep, "mean_length": c[3] / ep}
+            "win_rate_main": c[4] / ep, "win_rate_hdqn": c[5] / ep, "mean_length": c[3] / ep,
+            "mean_q_eval": sums[3] / ep}
 
 
 def gather_episode_summary(returns, counts, group=None, timings=None):
-    """All-gather every rank's 72-byte partial totals and reduce them: the global summary on
+    """All-gather every rank's 80-byte partial totals and reduce them: the global summary on
     every rank (the default collective of a sharded run). timings (a dict, optional) receives
     "reduce_ms" (this shard's reduction to its partial totals: HIP events around its launches on
     the GPU), "reduce_wall_ms" (the same call on the host clock, synchronised: Python and launch

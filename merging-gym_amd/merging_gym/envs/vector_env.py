@@ -117,6 +117,9 @@ class MergeVecEnv:
         self.ret_sum = self._ep_stats[:, :2] if episode_stats else None
         self.ret_main = self._ep_stats[:, 2] if episode_stats else None
         self.counts = self._ep_stats[:, 4:].view(torch.int32)[:, :6] if episode_stats else None
+        # [N] f64: sum of each completed episode's logged Q value (q_eval_value, main.py:221 /
+        # hdqn.py:330), kept by the fused policy rollouts (rollout_qnet, rollout_hdqn)
+        self.q_eval = self._ep_stats[:, 7] if episode_stats else None
 
         ptr = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
         self._state = _native.State(*(ptr(t) for t in (self.p1, self.v1, self.p2, self.v2,
@@ -475,9 +478,19 @@ class MergeVecEnv:
         (sums of r1_accumulate = hdqn.py's ep_reward, r2_accumulate, main.py's winner-filtered
         ep_reward, scripts/main.py:209-211), "ret_sum" = returns[:, :2], "ret_main" =
         returns[:, 2], "counts" [N,6] i32 (episodes, collisions, ego-first arrivals, steps,
-        main.py:225 wins, hdqn.py:342 wins)."""
+        main.py:225 wins, hdqn.py:342 wins), "q_eval" [N] f64 (the sum of the Q value logged per
+        episode by the fused policy rollouts: main.py:221, hdqn.py:330)."""
         return {"returns": self.returns, "ret_sum": self.ret_sum, "ret_main": self.ret_main,
-                "counts": self.counts}
+                "counts": self.counts, "q_eval": self.q_eval}
+
+    def episode_summary(self):
+        """This batch's completed episodes summarised as the scripts log them (distributed.summarize:
+        rates, mean rewards, mean_q_eval), reduced on the device by mg_stats_reduce."""
+        from ..distributed import summarize
+
+        if self.returns is None:
+            raise ValueError("built with episode_stats=False")
+        return summarize(self.returns, self.counts)
 
     def clear_statistics(self):
         """Zero the sums and counts (each env's pending main.py value stays: it belongs to the
@@ -485,6 +498,7 @@ class MergeVecEnv:
         if self.ret_sum is not None:
             self.returns.zero_()
             self.counts.zero_()
+            self.q_eval.zero_()
 
     # ------------------------------------------------------------------ checkpoint / resume
     _STATE_KEYS = ("p1", "v1", "p2", "v2", "ret1", "ret2", "tf")
@@ -499,6 +513,7 @@ class MergeVecEnv:
         sd["env_offset"] = self.env_offset
         if self.ret_sum is not None:
             sd["episode_stats"] = self._ep_stats.clone()  # the 64-byte records, pending value included
+            sd["episode_stats_format"] = self._nat.EPISODE_STATS_FORMAT
         if getattr(self, "hdqn_goal", None) is not None:
             sd["hdqn_goal"] = self.hdqn_goal.clone()  # rollout_hdqn's current goals
         if getattr(self, "hdqn_goal_op", None) is not None:
@@ -517,14 +532,30 @@ class MergeVecEnv:
         if int(sd.get("env_offset", self.env_offset)) != self.env_offset:
             raise ValueError("the checkpoint is of another env shard (env_offset differs)")
         self._step_idx = int(sd["step_idx"])
-        if self.ret_sum is not None and "episode_stats" in sd:
-            self._ep_stats.copy_(self._torch.as_tensor(sd["episode_stats"]))
+        if self.ret_sum is not None:
+            self._load_episode_stats(sd)
         if "hdqn_goal" in sd:
             self.hdqn_goal = self._torch.as_tensor(sd["hdqn_goal"]).to(self.device, self._torch.int8).clone()
         if "hdqn_goal_op" in sd:
             self.hdqn_goal_op = self._torch.as_tensor(sd["hdqn_goal_op"]).to(self.device, self._torch.int8).clone()
         if "hdqn_ext" in sd:
             self.hdqn_ext = self._torch.as_tensor(sd["hdqn_ext"]).to(self.device, self._torch.float64).clone()
+
+    def _load_episode_stats(self, sd):
+        """The 64-byte records of a checkpoint. ABI <= 16 checkpoints kept 'ret_sum' / 'counts'
+        arrays: main.py's filtered return and both scripts' win counts are not in them, so they are
+        refused rather than loaded half. ABI 17-19 records (format 1) lack q_eval: it loads as NaN
+        (unknown), so a summary over them says so instead of reporting a diluted mean."""
+        if "episode_stats" not in sd:
+            if "ret_sum" in sd or "counts" in sd:
+                raise ValueError("checkpoint holds the ABI <= 16 statistics ('ret_sum' / 'counts'); the 64-byte "
+                                 "records (ABI 17+) add main.py's filtered ep_reward and both scripts' win counts, "
+                                 "which cannot be recovered: rebuild the env or load with episode_stats=False")
+            raise ValueError("checkpoint holds no episode statistics ('episode_stats'): build the env with "
+                             "episode_stats=False to resume it")
+        self._ep_stats.copy_(self._torch.as_tensor(sd["episode_stats"]))
+        if int(sd.get("episode_stats_format", 1)) < 2:
+            self.q_eval.fill_(float("nan"))
 
     def close(self):
         pass

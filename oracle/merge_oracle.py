@@ -449,7 +449,7 @@ def goal_status64(obs):
 def stats_reduce_fixed(records):
     """mg_stats_reduce's totals (include/merging_hip.h, merging_hip.hip stats_reduce_kernel) restated
     in numpy, operation for operation: records [n, 8] f64 (the 64-byte mg_episode_stats rows) ->
-    (three f64 sums of ret[0], ret[1], ret_main; six int64 counts). Blocks of 1,024 records; thread t
+    (four f64 sums of ret[0], ret[1], ret_main, q_eval; six int64 counts). Blocks of 1,024 records; thread t
     of 256 adds records t, t + 256, t + 512, t + 768 of its block onto -0.0 in that order; the 256
     values fold in halves (v[t] + v[t + o], o = 128 ... 1); the block partials the same way, thread t
     adding partials t, t + 256, ... in order. Padding is -0.0, the exact additive identity. The
@@ -468,7 +468,7 @@ def stats_reduce_fixed(records):
 
     nb = (n + 1023) // 1024
     sums = []
-    for k in range(3):
+    for k in (0, 1, 2, 7):
         col = np.full(max(nb, 1) * 1024, -0.0)
         col[:n] = rec[:, k]
         x = col.reshape(-1, 4, 256)

@@ -62,3 +62,21 @@ class ChoiceCheck:
         if self.max_frac is not None:
             assert self.frac <= self.max_frac, (self.name, self.excused, self.greedy)
         return self.frac
+
+
+def check_q_eval(dev, exp, abs_sum, what=""):
+    """The q_eval sums a fused policy kernel keeps (mg_episode_stats.q_eval: the Q value the scripts
+    log per finished episode, main.py:221 / hdqn.py:330) against the bf16-emulated reference's, env
+    by env. The kernel's fp32 sums run in another order than the emulation's, and a hidden unit that
+    lands on a bf16 rounding boundary can round the other way, so the bound is the Q-net forward's
+    own (tests/test_gpu_qnet.py): median relative error < 1e-5, max < 1e-2 of max(1, sum |q|)."""
+    import numpy as np
+
+    dev, exp, abs_sum = (np.asarray(a, np.float64) for a in (dev, exp, abs_sum))
+    logged = abs_sum > 0
+    assert logged.sum() > 0, f"{what}: no episode ended"
+    assert (dev[~logged] == exp[~logged]).all(), f"{what}: q_eval changed without a finished episode"
+    err = np.abs(dev - exp)[logged] / np.maximum(1.0, abs_sum[logged])
+    assert np.median(err) < 1e-5 and err.max() < 1e-2, (what, float(np.median(err)), float(err.max()))
+    SUMMARY.append(f"[q_eval] {what}: {int(logged.sum())} envs with logged episodes, median rel err "
+                   f"{float(np.median(err)):.2e}, max {float(err.max()):.2e}")

@@ -1,7 +1,7 @@
 """One-rank RCCL run for tests/test_gpu_distributed.py::test_rccl_device_gather: launched by
 torch.distributed.run with the "nccl" backend (RCCL on ROCm) on the test box's one GPU, it steps a
 MergeVecEnv and runs distributed.all_gather_rows -- the all_gather_into_tensor device branch every
-rank of a sharded run takes for the 72-byte episode summary and the per-env rows -- on device
+rank of a sharded run takes for the 80-byte episode summary and the per-env rows -- on device
 tensors, then saves what came back beside the local values.
 
     python -m torch.distributed.run --nproc-per-node 1 --master-addr 127.0.0.1 \\

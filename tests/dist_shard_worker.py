@@ -1,7 +1,7 @@
 """One rank of the sharded-run GPU test (tests/test_gpu_distributed.py), launched by
 torch.distributed.run with the gloo backend; every rank steps its own contiguous shard of the
 global batch on cuda:0 (the test box has one GPU) exactly as bench.py's ranks do on their own
-GPUs, then the statistics are gathered -- the 72-byte summary (the default collective) and the
+GPUs, then the statistics are gathered -- the 80-byte summary (the default collective) and the
 per-env rows (opt-in) -- and rank 0 saves both with its shard bookkeeping.
 
     python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 \

@@ -190,9 +190,9 @@ def test_argument_errors_without_gpu():
     # 65536 write blocks in 1024 scan groups: ticket (8) + bases u64 + offsets u32 + totals u32
     assert _native.lib.mg_replay_scratch_bytes(1 << 20, 16) == 8 + 1024 * 8 + 65536 * 4 + 1024 * 4
     assert _native.lib.mg_replay_scratch_bytes(0, 4) == 0
-    # the statistics reduction (ABI 20): one 72-byte partial per 1,024 records; NULL / misaligned refused
-    assert _native.lib.mg_stats_reduce_scratch_bytes(1 << 20) == 1024 * 72
-    assert _native.lib.mg_stats_reduce_scratch_bytes(1025) == 2 * 72 and _native.lib.mg_stats_reduce_scratch_bytes(0) == 0
+    # the statistics reduction (ABI 20): one 80-byte partial per 1,024 records; NULL / misaligned refused
+    assert _native.lib.mg_stats_reduce_scratch_bytes(1 << 20) == 1024 * 80
+    assert _native.lib.mg_stats_reduce_scratch_bytes(1025) == 2 * 80 and _native.lib.mg_stats_reduce_scratch_bytes(0) == 0
     assert _native.lib.mg_stats_reduce(fake, 4, None, fake, 1 << 20, None) != 0 and b"NULL" in _native.lib.mg_last_error()
     assert _native.lib.mg_stats_reduce(fake, 4, fake, fake, 8, None) != 0 and b"scratch" in _native.lib.mg_last_error()
     assert _native.lib.mg_stats_reduce(odd, 4, fake, fake, 1 << 20, None) != 0

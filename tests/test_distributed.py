@@ -66,7 +66,7 @@ def _summary_worker(rank, world, port, n_per_rank, out_path):
 
 
 def test_gather_episode_summary_gloo(tmp_path):
-    """The default collective: 72 bytes per rank, every rank gets the global summary, equal to
+    """The default collective: 80 bytes per rank, every rank gets the global summary, equal to
     summarizing the concatenated per-env statistics (counts exactly, returns to fp64 rounding)."""
     world, n = 2, 1500
     out = str(tmp_path / "s")

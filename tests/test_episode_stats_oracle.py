@@ -186,6 +186,6 @@ def test_stats_reduce_restatement_order():
     for n in (0, 5, 1024, 3000):
         rec = rng.normal(0, 1, (n, 8)) * 10.0 ** rng.integers(-9, 5, (n, 8))
         sums, _ = mo.stats_reduce_fixed(rec)
-        for k in range(3):
-            ref = scalar(rec[:, k].tolist())
+        for k, col in enumerate((0, 1, 2, 7)):
+            ref = scalar(rec[:, col].tolist())
             assert np.float64(sums[k]).view(np.uint64) == np.float64(ref).view(np.uint64), (n, k)

@@ -2,7 +2,7 @@
 launched with torch.distributed.run (gloo; both ranks on cuda:0 of the one-GPU test box), each
 step a MergeVecEnv(env_offset=...) shard for 200 Philox steps and gather the statistics. The
 result must equal one unsharded run of the whole batch: per-env statistics and positions bit
-for bit (Philox is keyed by the global env index, envs never interact), the 72-byte-per-rank
+for bit (Philox is keyed by the global env index, envs never interact), the 80-byte-per-rank
 summary to fp64 summation order. The reference has no parallelism (its envs are independent,
 merging_env.py:138-195); this pins the build's own sharding."""
 
@@ -60,7 +60,7 @@ def test_two_rank_shards_equal_unsharded_run(tmp_path):
 
 def test_rccl_device_gather(tmp_path):
     """The RCCL branch of the statistics gather (distributed.all_gather_rows, backend "nccl"):
-    all_gather_into_tensor of the 72-byte partial totals and of the per-env rows, on device
+    all_gather_into_tensor of the 80-byte partial totals and of the per-env rows, on device
     tensors, in a one-rank RCCL group on the test box's one GPU (RCCL refuses two ranks on one
     device; the 8-GPU runs are the driver's). What comes back must equal what went in, bit for bit."""
     import torch
@@ -73,6 +73,6 @@ def test_rccl_device_gather(tmp_path):
     run = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
     assert run.returncode == 0, run.stderr[-3000:]
     got = torch.load(out, weights_only=True)
-    assert got["got_part"].shape == (1, 9) and torch.equal(got["got_part"][0], got["part"])
+    assert got["got_part"].shape == (1, 10) and torch.equal(got["got_part"][0], got["part"])
     assert torch.equal(got["got_rows"], got["rows"]) and got["rows"].shape == (4099, 6)
     assert int(got["part"][3]) > 0  # episodes completed inside the run

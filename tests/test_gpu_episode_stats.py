@@ -184,6 +184,7 @@ def test_stats_reduce_fixed_order(n):
     rng = np.random.default_rng(n)
     rec = np.zeros((max(n, 1), 8))[:n]
     rec[:, :4] = rng.normal(0, 1, (n, 4)) * 10.0 ** rng.integers(-12, 6, (n, 4))
+    rec[:, 7] = rng.normal(0, 1, n) * 10.0 ** rng.integers(-6, 4, n)  # q_eval
     if n:
         rec[:: 7, 0] = -0.0
         rec[:: 11, 2] = rng.uniform(-1e-300, 1e-300, rec[:: 11, 2].shape)
@@ -192,14 +193,15 @@ def test_stats_reduce_fixed_order(n):
     dev = torch.from_numpy(rec.copy()).cuda()
     tot = device_totals(dev).cpu().numpy()
     sums, counts = mo.stats_reduce_fixed(rec)
-    np.testing.assert_array_equal(tot[:3].view(np.float64).view(np.uint64),
+    np.testing.assert_array_equal(tot[:4].view(np.float64).view(np.uint64),
                                   np.array(sums, np.float64).view(np.uint64))
-    assert tot[3:].tolist() == counts
+    assert tot[4:].tolist() == counts
     if n:  # the MergeVecEnv views (returns [n,3], counts [n,6] i32) take the same path
         views = dev[:, :3], dev[:, 4:].view(torch.int32)[:, :6]
         assert torch.equal(partial_stats(*views).cpu(), torch.from_numpy(tot))
         s = summarize_partials(torch.from_numpy(tot))
         assert s["completed"] == counts[0] and s["mean_return_ego"] == sums[0] / counts[0]
+        assert s["mean_q_eval"] == sums[3] / counts[0]
 
 
 def test_stats_reduce_is_cheap_at_full_size():

@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 
 import merge_oracle as mo
-from choice_check import ChoiceCheck
+from choice_check import ChoiceCheck, check_q_eval
 
 pytestmark = pytest.mark.gpu
 
@@ -195,6 +195,7 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
         env.step_random(5, opponent_random=False, step_idx=k)
     envs = mo.oracle_envs_from(coracle, env)
     stats = (env.returns.cpu().numpy().copy(), env.counts.cpu().numpy().astype(np.uint32))
+    qe, qe_abs = env.q_eval.cpu().numpy().copy(), np.zeros(n)  # hdqn.py:330's q_eval per episode
     obs = env.observe().cpu().numpy().copy()
     obs64 = coracle.observe(envs)  # the fp64 state goal_status reads
     kind = _kind(opponent)
@@ -284,6 +285,10 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
             exp_g2 = np.where(gg, q2.argmax(1), _pick(ua[:, 3], NUM_GOALS))
             g2 = g["next_goal"][t].astype(np.int64)
             cc_g.check(g2, exp_g2, gg, q2, f"next goal, launch {launch} step {t}")
+            # meta_eval_net(state)[goal] on the terminal state and the goal chosen on it (:330)
+            qg = q2[np.arange(n), g2]
+            qe += np.where(d, qg, 0.0)
+            qe_abs += np.where(d, np.abs(qg), 0.0)
             # :314 on the state acted on and :322 on the next state, in fp64 as the reference
             np.testing.assert_array_equal(g["reward"][t], (g2 == _status(obs64)).astype(np.float32))
             # the goal of the next step: kept, or fresh once reached / after an episode end
@@ -345,6 +350,7 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
     # the episode statistics the launch's finishing envs recorded (both scripts' logged values)
     np.testing.assert_array_equal(env.returns.cpu().numpy(), stats[0])
     np.testing.assert_array_equal(env.counts.cpu().numpy().astype(np.uint32), stats[1])
+    check_q_eval(env.q_eval.cpu().numpy(), qe, qe_abs, f"fused h-DQN {opponent} n={n}")
     cc_a.finish()
     cc_g.finish()
     if selfplay:
@@ -387,6 +393,7 @@ def test_fused_hdqn_rollout_full_size(coracle, nets):
     idx = torch.from_numpy(idx_np).to(dev)
     envs = mo.oracle_envs_from(coracle, env, idx)
     stats = (env.returns[idx].cpu().numpy().copy(), env.counts[idx].cpu().numpy().astype(np.uint32))
+    qe, qe_abs = env.q_eval[idx].cpu().numpy().copy(), np.zeros(len(idx_np))
     obs = env.observe()[idx].cpu().numpy().copy()
     obs64 = coracle.observe(envs)
     reset_goal = meta.reset_argmax()
@@ -430,6 +437,9 @@ def test_fused_hdqn_rollout_full_size(coracle, nets):
         gg = ua[:, 2] < thr
         g2 = sub["next_goal"][t].astype(np.int64)
         cc_g.check(g2, np.where(gg, q2.argmax(1), _pick(ua[:, 3], NUM_GOALS)), gg, q2, f"next goal, step {t}")
+        qg = q2[np.arange(len(idx_np)), g2]  # hdqn.py:330
+        qe += np.where(d, qg, 0.0)
+        qe_abs += np.where(d, np.abs(qg), 0.0)
         np.testing.assert_array_equal(sub["reward"][t], (g2 == _status(obs64)).astype(np.float32))
         brk = d | (g2 == _status(s2_64))
         gf = ub[:, 0] < thr
@@ -443,6 +453,7 @@ def test_fused_hdqn_rollout_full_size(coracle, nets):
         np.testing.assert_array_equal(src[idx].cpu().numpy(), envs[name], err_msg=name)
     np.testing.assert_array_equal(env.returns[idx].cpu().numpy(), stats[0])
     np.testing.assert_array_equal(env.counts[idx].cpu().numpy().astype(np.uint32), stats[1])
+    check_q_eval(env.q_eval[idx].cpu().numpy(), qe, qe_abs, f"full-size h-DQN ({nets})")
     cc_a.finish()
     cc_g.finish()
 

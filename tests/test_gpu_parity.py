@@ -422,3 +422,13 @@ def test_checkpoint_resume_is_bit_exact(torch):
     assert torch.equal(ring2.memory, ring.memory) and ring2.memory_counter == ring.memory_counter
     with pytest.raises(ValueError):
         MergeVecEnv(3000, device="cuda:0").load_state_dict(end)
+    # older checkpoints: ABI <= 16 arrays are refused (their main.py / win statistics are gone); ABI
+    # 17-19 records load with q_eval unknown (NaN), not a silently diluted sum
+    legacy = {k: v for k, v in end.items() if k not in ("episode_stats", "episode_stats_format")}
+    legacy.update(ret_sum=torch.zeros((3001, 2), dtype=torch.float64), counts=torch.zeros((3001, 4), dtype=torch.int32))
+    with pytest.raises(ValueError, match="ABI <= 16"):
+        MergeVecEnv(3001, device="cuda:0").load_state_dict(legacy)
+    fmt1 = {k: v for k, v in end.items() if k != "episode_stats_format"}
+    env3 = MergeVecEnv(3001, device="cuda:0")
+    env3.load_state_dict(fmt1)
+    assert bool(torch.isnan(env3.q_eval).all()) and torch.equal(env3.returns, end["episode_stats"][:, :3])

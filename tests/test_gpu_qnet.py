@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 
 import merge_oracle as mo
-from choice_check import ChoiceCheck
+from choice_check import ChoiceCheck, check_q_eval
 from conftest import ROOT
 
 pytestmark = pytest.mark.gpu
@@ -136,6 +136,8 @@ def test_rollout_qnet_policy_and_transitions(torch, coracle, nets, opponent, n):
     obs_in = env.observe().cpu().numpy().copy()
     opp_key = "l3" if opponent == "other" else "l1"
     opp = QNet.from_state_dict(nets["l3"], device="cuda:0") if opponent == "other" else opponent
+    qe = env.q_eval.cpu().numpy().copy()  # main.py:221's q_eval, per finished episode
+    qe_abs = np.zeros(n)
     traj = env.rollout_qnet(T, qnet, seed, opponent=opp, first_step=k0)
     traj = {k: (v.cpu().numpy() if v is not None else None) for k, v in traj.items()}
     thr = greedy_threshold(0.7)
@@ -167,9 +169,14 @@ def test_rollout_qnet_policy_and_transitions(torch, coracle, nets, opponent, n):
         np.testing.assert_allclose(traj["rew"][t], o_rew.astype(np.float32), **OBS_TOL)
         d = o_done.astype(bool)
         np.testing.assert_allclose(traj["final_observation"][t][d], o_fobs[d].astype(np.float32), **OBS_TOL)
+        # eval_net(state)[action] on the input and action of an episode's last step (main.py:221)
+        qa = q[np.arange(n), traj["a1"][t].astype(np.int64)]
+        qe += np.where(d, qa, 0.0)
+        qe_abs += np.where(d, np.abs(qa), 0.0)
         obs_in = traj["obs"][t]
     np.testing.assert_array_equal(env.p1.cpu().numpy(), envs["pos1"])
     np.testing.assert_array_equal(env.ret2.cpu().numpy(), envs["r2_acc"])
+    check_q_eval(env.q_eval.cpu().numpy(), qe, qe_abs, f"rollout ego l1 ({opponent}, n={n})")
     assert env._step_idx == k0 + T
     cc1.finish()
     if opponent in ("self", "other"):
@@ -255,6 +262,7 @@ def test_rollout_qnet_full_size(torch, coracle, nets, opponent):
     envs = mo.oracle_envs_from(coracle, env, idx)  # main.py's running ep_reward from the device's pending value
     obs_in = env.observe()[idx].cpu().numpy().copy()
     ret_sum0, counts0 = env.returns[idx].cpu().numpy(), env.counts[idx].cpu().numpy().astype(np.uint32)
+    qe, qe_abs = env.q_eval[idx].cpu().numpy().copy(), np.zeros(len(idx_np))
 
     opp_key = "l3" if opponent == "other" else "l1"
     opp = QNet.from_state_dict(nets["l3"], device="cuda:0") if opponent == "other" else opponent
@@ -298,6 +306,9 @@ def test_rollout_qnet_full_size(torch, coracle, nets, opponent):
         np.testing.assert_allclose(sub["rew"][t], o_rew.astype(np.float32), **OBS_TOL)
         d = o_done.astype(bool)
         np.testing.assert_allclose(sub["final_observation"][t][d], o_fobs[d].astype(np.float32), **OBS_TOL)
+        qa = q[np.arange(len(idx_np)), sub["a1"][t].astype(np.int64)]  # main.py:221
+        qe += np.where(d, qa, 0.0)
+        qe_abs += np.where(d, np.abs(qa), 0.0)
         obs_in = sub["obs"][t]
     for name, src in (("pos1", env.p1), ("vel1", env.v1), ("pos2", env.p2), ("vel2", env.v2),
                       ("r1_acc", env.ret1), ("r2_acc", env.ret2)):
@@ -305,6 +316,7 @@ def test_rollout_qnet_full_size(torch, coracle, nets, opponent):
     np.testing.assert_array_equal(env.counts[idx].cpu().numpy().astype(np.uint32), stats[1])
     np.testing.assert_array_equal(env.returns[idx].cpu().numpy(), stats[0])
     assert stats[1][:, 0].sum() > counts0[:, 0].sum()  # episodes ended in the window
+    check_q_eval(env.q_eval[idx].cpu().numpy(), qe, qe_abs, f"full-size ego l1 ({opponent})")
     cc1.finish()
     if opponent in ("self", "other"):
         cc2.finish()
