@@ -38,6 +38,8 @@ _ARENA_STAGGER = int(os.environ.get("MG_ARENA_STAGGER", "4160"))
 # One interleaved [N, 4] uint8 record (a1, a2, done, collision) per step instead of four byte
 # arrays (mg_outputs.flags). MG_STEP_FLAGS=0 restores the four arrays (A/B, and the tests run both).
 _STEP_FLAGS = os.environ.get("MG_STEP_FLAGS", "1") != "0"
+# mg_rollout_random's limit per launch (16-bit per-launch episode counts in registers)
+_MAX_ROLLOUT_STEPS = 65535
 
 
 class MergeVecEnv:
@@ -268,18 +270,32 @@ class MergeVecEnv:
         step -- ReplayRing.store_rollout's filter; None with won_mask=False, which saves a
         ballot and a store per wave-step). a1, a2, done and collision are strided views of one
         [T, N, 4] uint8 buffer, returned as "flags" (one 32-bit store per env-step in the
-        kernel). The buffers are reused by the next rollout with the same T and output choices."""
+        kernel). The buffers are reused by the next rollout with the same T and output choices.
+        A launch keeps each env's episode counts in 16-bit registers, so mg_rollout_random takes at
+        most 65,535 steps: longer rollouts run as consecutive launches into slices of the same
+        buffers, bit-identical to one launch (the step index keys the draws)."""
         nat = self._nat
         T, n = int(num_steps), self.num_envs
         k0 = self._step_idx if first_step is None else int(first_step)
         buf = self._traj(T, final_observation, won_mask)
-        rc = nat.lib.mg_rollout_random(
-            self._p_ref, self._s_ref, ctypes.byref(buf["_traj"]), self._st_ref, n, self.env_offset,
-            seed & 0xFFFFFFFFFFFFFFFF, k0 & 0xFFFFFFFFFFFFFFFF, T, 1 if opponent_random else 0,
-            self._flags, self._stream())
-        nat.check(rc, "mg_rollout_random")
+        for t0 in range(0, max(T, 1), _MAX_ROLLOUT_STEPS):
+            tc = min(_MAX_ROLLOUT_STEPS, T - t0)
+            traj = buf["_traj"] if t0 == 0 else self._traj_slice(buf, t0)
+            rc = nat.lib.mg_rollout_random(
+                self._p_ref, self._s_ref, ctypes.byref(traj), self._st_ref, n, self.env_offset,
+                seed & 0xFFFFFFFFFFFFFFFF, (k0 + t0) & 0xFFFFFFFFFFFFFFFF, tc, 1 if opponent_random else 0,
+                self._flags, self._stream())
+            nat.check(rc, "mg_rollout_random")
         self._step_idx = k0 + T
         return buf["_result"]
+
+    def _traj_slice(self, buf, t0):
+        """mg_traj of the trajectory buffers from step t0 on (a chunk of a long rollout)."""
+        n = self.num_envs
+        ptr = lambda t, row: None if t is None else t.data_ptr() + t0 * row  # noqa: E731
+        return self._nat.Traj(ptr(buf["obs"], n * _OBS_DIM * 4), ptr(buf["rew"], n * 8), None, None, None, None,
+                              ptr(buf["final_observation"], n * _OBS_DIM * 4), ptr(buf["won_mask"], (n + 63) // 64 * 8),
+                              ptr(buf["flags"], n * 4))
 
     def _traj(self, T, final_observation, won_mask=True):
         """[T, N, ...] trajectory buffers, reused while T and the output choices stay the same."""
@@ -414,8 +430,8 @@ class MergeVecEnv:
             self._st_ref, self.hdqn_goal.data_ptr(), None if gop is None else gop.data_ptr(),
             None if ext is None else ext.data_ptr(), n, self.env_offset, seed & 0xFFFFFFFFFFFFFFFF, k0 & 0xFFFFFFFFFFFFFFFF,
             T, meta.packed.data_ptr(), meta.out_dim, lower.packed.data_ptr(), meta.reset_argmax(),
-            greedy_threshold(episilo), mode, None if opp_meta is None else opp_meta.fragments.data_ptr(),
-            None if opp_lower is None else opp_lower.fragments.data_ptr(), None if ring is None else ring.memory.data_ptr(),
+            greedy_threshold(episilo), mode, None if opp_meta is None else opp_meta.packed.data_ptr(),
+            None if opp_lower is None else opp_lower.packed.data_ptr(), None if ring is None else ring.memory.data_ptr(),
             None if ring is None else ring._counter.data_ptr(), 0 if ring is None else ring.capacity,
             self._flags, self._stream())
         nat.check(rc, "mg_rollout_hdqn")

@@ -17,8 +17,15 @@ NUM_GOALS = 3  # hdqn.py:31
 def goal_status(states):
     """hdqn.py:223-237: the sub-goal an observation is in -- 0 if dx1 < -0.5 v2, 1 if dx1 < 0.5 v2,
     else 2 (dx1 = obs[0], v2 = obs[9]). One observation (10 values) gives an int, as the reference;
-    a [N, 10] tensor gives int64 [N] on its device (the comparisons are exact in fp32: -0.5 v2 is a
-    power-of-two scaling, so only the observation's own rounding to fp32 can differ)."""
+    a [N, 10] tensor gives int64 [N] on its device.
+
+    Pass fp64 observations for the reference's decisions: the reference compares the Python floats
+    env.step returned, and the fused h-DQN kernel compares the fp64 x2 - x1 and v2 of its state
+    (mg_goal_status). On MergeVecEnv's fp32 observations the rounding of dx1 to fp32 flips the status
+    of states near the thresholds (a sixth of the boundary rows in
+    tests/test_gpu_episode_stats.py::test_hdqn_intrinsic_reward_uses_fp64_goal_status), so the result
+    can disagree with the kernel's intrinsic rewards there; use mg_goal_status on the env's fp64
+    state (the mg_observe rec64 path) when it must agree."""
     try:
         import torch
 
@@ -67,17 +74,11 @@ class QNet:
 
     @property
     def fragments(self):
-        """The fragment-major copy of the packed net (mg_qnet_fragments, made once): the layout
-        mg_rollout_hdqn reads an opponent from another checkpoint in from global memory."""
-        if getattr(self, "_fragments", None) is None:
-            import torch
-
-            f = torch.empty(self._nat.lib.mg_qnet_fragment_bytes(), dtype=torch.uint8, device=self.device)
-            stream = torch.cuda.current_stream(self.device).cuda_stream
-            self._nat.check(self._nat.lib.mg_qnet_fragments(self.packed.data_ptr(), f.data_ptr(), stream),
-                            "mg_qnet_fragments")
-            self._fragments = f
-        return self._fragments
+        """Deprecated alias of `packed` (ABI 18 kept a separate fragment-major copy here): since ABI 19
+        the packed layout begins with the fragment-major 16x16 forward mg_rollout_hdqn reads an
+        opponent from another checkpoint in, so the kernels take `packed` itself and no second copy
+        can go stale when `packed` changes."""
+        return self.packed
 
     def reset_argmax(self) -> int:
         """argmax of this net on the reset observation (merging_env.py:208-230), computed once on

@@ -128,4 +128,11 @@ def test_packed_layout_restated_from_the_weights(torch, in_dim, out_dim):
     assert packed.shape == (n16 + 2 * (204 * 24 + 104 * 232 + 9 * 136),)
     np.testing.assert_array_equal(packed[:n16], _expected(sd, in_dim, out_dim))
     np.testing.assert_array_equal(packed[n16:], _expected32(sd, in_dim, out_dim))
-    np.testing.assert_array_equal(net.fragments.cpu().numpy(), packed[:n16])
+    # mg_qnet_fragments (ABI 18 callers) copies the fragment-major first part; QNet.fragments is a
+    # deprecated alias of packed itself, which the kernels read an other-checkpoint opponent from
+    from merging_gym import _native
+
+    frag = torch.empty(n16, dtype=torch.uint8, device="cuda:0")
+    _native.check(_native.lib.mg_qnet_fragments(net.packed.data_ptr(), frag.data_ptr(), None), "mg_qnet_fragments")
+    np.testing.assert_array_equal(frag.cpu().numpy(), packed[:n16])
+    assert net.fragments is net.packed
