@@ -124,7 +124,7 @@ def test_rollout_qnet_policy_and_transitions(torch, coracle, nets, opponent, n):
     T, seed, k0 = 24, 17, 500
     qnet = QNet.from_state_dict(nets["l1"], device="cuda:0")
     env = MergeVecEnv(n, device="cuda:0")
-    for k in range(60):  # mid-episode start
+    for k in range(200):  # mid-episode start: episodes end inside the window (autoreset, q_eval)
         env.step_random(seed + 1, step_idx=k)
     envs = coracle.new_envs(n)
     for name, src in (("pos1", env.p1), ("vel1", env.v1), ("pos2", env.p2), ("vel2", env.v2),
