@@ -69,7 +69,9 @@ def check_q_eval(dev, exp, abs_sum, what=""):
     log per finished episode, main.py:221 / hdqn.py:330) against the bf16-emulated reference's, env
     by env. The kernel's fp32 sums run in another order than the emulation's, and a hidden unit that
     lands on a bf16 rounding boundary can round the other way, so the bound is the Q-net forward's
-    own (tests/test_gpu_qnet.py): median relative error < 1e-5, max < 1e-2 of max(1, sum |q|)."""
+    own (tests/test_gpu_qnet.py): median relative error < 1e-5, max < 1e-2 of max(1, abs_sum), abs_sum
+    being the env's sum over its logged episodes of max_a |q| of the logged row (the forward test's
+    per-row scale)."""
     import numpy as np
 
     dev, exp, abs_sum = (np.asarray(a, np.float64) for a in (dev, exp, abs_sum))

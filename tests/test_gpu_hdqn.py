@@ -288,7 +288,7 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
             # meta_eval_net(state)[goal] on the terminal state and the goal chosen on it (:330)
             qg = q2[np.arange(n), g2]
             qe += np.where(d, qg, 0.0)
-            qe_abs += np.where(d, np.abs(qg), 0.0)
+            qe_abs += np.where(d, np.abs(q2).max(1), 0.0)
             # :314 on the state acted on and :322 on the next state, in fp64 as the reference
             np.testing.assert_array_equal(g["reward"][t], (g2 == _status(obs64)).astype(np.float32))
             # the goal of the next step: kept, or fresh once reached / after an episode end
@@ -439,7 +439,7 @@ def test_fused_hdqn_rollout_full_size(coracle, nets):
         cc_g.check(g2, np.where(gg, q2.argmax(1), _pick(ua[:, 3], NUM_GOALS)), gg, q2, f"next goal, step {t}")
         qg = q2[np.arange(len(idx_np)), g2]  # hdqn.py:330
         qe += np.where(d, qg, 0.0)
-        qe_abs += np.where(d, np.abs(qg), 0.0)
+        qe_abs += np.where(d, np.abs(q2).max(1), 0.0)
         np.testing.assert_array_equal(sub["reward"][t], (g2 == _status(obs64)).astype(np.float32))
         brk = d | (g2 == _status(s2_64))
         gf = ub[:, 0] < thr

@@ -172,7 +172,7 @@ def test_rollout_qnet_policy_and_transitions(torch, coracle, nets, opponent, n):
         # eval_net(state)[action] on the input and action of an episode's last step (main.py:221)
         qa = q[np.arange(n), traj["a1"][t].astype(np.int64)]
         qe += np.where(d, qa, 0.0)
-        qe_abs += np.where(d, np.abs(qa), 0.0)
+        qe_abs += np.where(d, np.abs(q).max(1), 0.0)
         obs_in = traj["obs"][t]
     np.testing.assert_array_equal(env.p1.cpu().numpy(), envs["pos1"])
     np.testing.assert_array_equal(env.ret2.cpu().numpy(), envs["r2_acc"])
@@ -308,7 +308,7 @@ def test_rollout_qnet_full_size(torch, coracle, nets, opponent):
         np.testing.assert_allclose(sub["final_observation"][t][d], o_fobs[d].astype(np.float32), **OBS_TOL)
         qa = q[np.arange(len(idx_np)), sub["a1"][t].astype(np.int64)]  # main.py:221
         qe += np.where(d, qa, 0.0)
-        qe_abs += np.where(d, np.abs(qa), 0.0)
+        qe_abs += np.where(d, np.abs(q).max(1), 0.0)
         obs_in = sub["obs"][t]
     for name, src in (("pos1", env.p1), ("vel1", env.v1), ("pos2", env.p2), ("vel2", env.v2),
                       ("r1_acc", env.ret1), ("r2_acc", env.ret2)):
