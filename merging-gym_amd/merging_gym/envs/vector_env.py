@@ -6,7 +6,7 @@ uint32 of step count, winner and done); a step is one launch of `mg_step` (or
 `mg_step_random`, actions drawn on the device) from libmerging_hip.so. Nothing is computed
 on the host and there is no CPU fallback.
 
-API (gym 0.20 VectorEnv conventions, two players like the reference's step(a1, a2=None)):
+API (after gym 0.20's VectorEnv, with two players like the reference's step(a1, a2=None)):
 
     env = MergeVecEnv(num_envs, device="cuda:0")
     obs = env.reset()                                # [N,10] float32 tensor
@@ -17,6 +17,13 @@ API (gym 0.20 VectorEnv conventions, two players like the reference's step(a1, a
 Outputs are views of buffers the env owns and overwrites on the next call (clone them to
 keep them). With autoreset (the default) an env that finishes is reset inside the same
 kernel: `obs` holds its reset observation and `info["final_observation"]` the terminal one.
+
+Deviation from gym 0.20 (the version the reference pins, requirements.txt:2): its vector envs
+return `infos` as N per-env dicts with the last observation of a finished env in
+`infos[i]["terminal_observation"]`. This env returns ONE dict of batched device tensors (the layout
+of later gym versions' batched infos), so no host loop over N envs runs per step; the terminal
+observations are also under `info["terminal_observation"]` (the same [N,10] tensor). Observations,
+rewards and dones are device tensors, and `step` takes both players' action arrays.
 """
 
 from __future__ import annotations
@@ -143,6 +150,7 @@ class MergeVecEnv:
         info = {"collision": self.coll.view(torch.bool)}
         if self.final_obs is not None and self.autoreset:
             info["final_observation"] = self.final_obs
+            info["terminal_observation"] = self.final_obs  # gym 0.20's key (batched here, see above)
         self._result = (self.obs, self.rew, self.done.view(torch.bool), info)
 
         self.single_observation_space = spaces.observation_space()

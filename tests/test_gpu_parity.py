@@ -60,6 +60,7 @@ def _check_step(out, ref, k):
     np.testing.assert_allclose(obs.cpu().numpy(), o_obs.astype(np.float32), **OBS_TOL, err_msg=f"obs @ {k}")
     np.testing.assert_allclose(rew.cpu().numpy(), o_rew.astype(np.float32), **OBS_TOL, err_msg=f"rew @ {k}")
     if o_fobs is not None and "final_observation" in info:
+        assert info["terminal_observation"] is info["final_observation"]  # gym 0.20's key, batched
         d = o_done.astype(bool)
         np.testing.assert_allclose(info["final_observation"].cpu().numpy()[d], o_fobs[d].astype(np.float32),
                                    **OBS_TOL, err_msg=f"final_obs @ {k}")
