@@ -182,6 +182,25 @@ MG_HD bool boxes_intersect(const Box& a, const Box& b) {
   return a.l <= b.r && b.l <= a.r && a.t <= b.b && b.t <= a.b;
 }
 
+// is_collided (:198-206) of cars at (lateral y, longitudinal x): boxes_intersect(vehicle_box(y1, x1),
+// vehicle_box(y2, x2)) with the lateral edges as integers where that is exact. For y >= 8 the corner
+// k = trunc(y) - w/2 (or + w/2) lies within [y/2, 2y], so k - y is exact (Sterbenz) and (k - y) + y is
+// k itself: the fp64 lateral edges are the integer ones and their comparison is an integer one. Every
+// lateral coordinate of a live episode is 150 +- d with d <= 59 (|theta| < 1/16); the opponent's mirror
+// arc reaches y < 8 only far past the end of an episode, where the fp64 form stays. Same result as
+// the fp64 test for every input (tests/test_host_step.py drives both on the host).
+MG_HD bool vehicles_collide(const mg_params& P, double y1, double x1, double y2, double x2) {
+  if (y1 >= 8.0 && y2 >= 8.0) {
+    const int l1 = static_cast<int>(y1) - P.veh_w / 2, l2 = static_cast<int>(y2) - P.veh_w / 2;
+    if (l1 > l2 + P.veh_w || l2 > l1 + P.veh_w) return false;
+    const int t1 = static_cast<int>(x1) - P.veh_h / 2, t2 = static_cast<int>(x2) - P.veh_h / 2;
+    const double a_t = (static_cast<double>(t1) - x1) + x1, a_b = (static_cast<double>(t1 + P.veh_h) - x1) + x1;
+    const double b_t = (static_cast<double>(t2) - x2) + x2, b_b = (static_cast<double>(t2 + P.veh_h) - x2) + x2;
+    return a_t <= b_b && b_t <= a_b;
+  }
+  return boxes_intersect(vehicle_box(P, y1, x1), vehicle_box(P, y2, x2));
+}
+
 // observe (merging_env.py:118-132): computed in fp64, stored as OT (fp64 for the single-env
 // record; fp32 -- the one rounding every fp32 output gets -- for the batched kernels)
 template <class OT>
@@ -207,6 +226,21 @@ MG_HD void reset_obs(const mg_params& P, OT (&o)[kObs], double* dx1 = nullptr) {
   lon2coord(P, P.start_point, false, x2, y2);
   observe(P, P.start_point, P.start_vel, P.start_point, P.start_vel, x1, y1, x2, y2, o);
   if (dx1) *dx1 = x2 - x1;
+}
+
+// The reset observation (merging_env.py:208-230 then observe): the same ten fp32 values and fp64
+// x2 - x1 for every env, so each launch computes it once on the host (the same MG_HD functions, the
+// same doubles) and the kernels copy it from the launch arguments (scalar loads) where autoreset
+// fires, instead of two sin / cos and the observation in the divergent finishing branch.
+struct Reset0 {
+  float o[kObs];
+  double dx1;
+};
+
+MG_HD Reset0 reset0(const mg_params& P) {
+  Reset0 z;
+  reset_obs(P, z.o, &z.dx1);
+  return z;
 }
 
 // goal_status (scripts/hdqn.py:223-236) on the reference's fp64 values: dx1 = state[0] = x2 - x1,
@@ -523,7 +557,7 @@ MG_HD void score_step(const mg_params& P, Env& e, double x1, double y1,
   }
 
   // is_collided (:183-187, :198-206)
-  r.coll = !frozen && boxes_intersect(vehicle_box(P, y1, x1), vehicle_box(P, y2, x2));
+  r.coll = !frozen && vehicles_collide(P, y1, x1, y2, x2);
   if (r.coll) {
     e.done = true;
     r1 += P.r_collision;
@@ -621,7 +655,7 @@ MG_HD void stats_add_q_eval(const mg_stats& St, int64_t i, double q) {
 // acted on (r.win_pre) and hdqn.py:342's on the terminal state.
 MG_HD void finish_episode(const mg_params& P, Env& e, StepOut& r,
                                                const mg_stats& St, float* final_obs_row,
-                                               int64_t i, EpStats* sreg = nullptr) {
+                                               int64_t i, EpStats* sreg = nullptr, const Reset0* r0 = nullptr) {
   const bool ego_won = e.winner == 1;
   const bool win_hdqn = (P.end_point - e.p2) > (P.end_point - e.p1);
   if (sreg) {
@@ -663,16 +697,22 @@ MG_HD void finish_episode(const mg_params& P, Env& e, StepOut& r,
   e.steps = 0;
   e.winner = 0;
   e.done = false;
-  reset_obs(P, r.o, &r.dx1);
+  if (r0) {  // the launch's precomputed reset observation (reset0)
+#pragma unroll
+    for (int k = 0; k < kObs; ++k) r.o[k] = r0->o[k];
+    r.dx1 = r0->dx1;
+  } else {
+    reset_obs(P, r.o, &r.dx1);
+  }
 }
 
 // After a step with statistics: the first-arrival bookkeeping, then autoreset where done.
 MG_HD void after_step(const mg_params& P, Env& e, StepOut& r, const mg_stats& St,
                                            float* final_obs_row, int64_t i, bool autoreset,
-                                           EpStats* sreg = nullptr) {
+                                           EpStats* sreg = nullptr, const Reset0* r0 = nullptr) {
   const bool finish = autoreset && r.done;
   if (r.first1 && !finish) note_first_arrival(St, i, r, sreg);
-  if (finish) finish_episode(P, e, r, St, final_obs_row, i, sreg);
+  if (finish) finish_episode(P, e, r, St, final_obs_row, i, sreg, r0);
 }
 
 // Wave-scope ordering of LDS accesses between the lanes of ONE wave (no s_barrier): the LDS
@@ -776,6 +816,7 @@ MG_HD uint32_t pack_step_bytes(int a1, int a2, bool done, bool coll) {
 
 struct Launch {
   mg_params P;
+  Reset0 R0;
   mg_state S;
   mg_outputs O;
   mg_stats St;
@@ -863,7 +904,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const Launch L) {
       }
       won = e.winner == 1;
       after_step(P, e, r, L.St, L.O.final_obs ? L.O.final_obs + i * kObs : nullptr, i,
-                 (L.flags & MG_AUTORESET) != 0);
+                 (L.flags & MG_AUTORESET) != 0, nullptr, &L.R0);
       store_env(L.S, opaque_index(i), e);
     }
   }
@@ -906,6 +947,7 @@ __device__ __forceinline__ void store_step_bytes(const mg_traj& T, int64_t row, 
 
 struct Rollout {
   mg_params P;
+  Reset0 R0;
   mg_state S;
   mg_traj T;
   mg_stats St;
@@ -968,7 +1010,7 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(const Rollout R) {
                f32x2{static_cast<float>(r.r1), static_cast<float>(r.r2)});
       store_step_bytes(R.T, row, a1, a2, r.done, r.coll);
       won = e.winner == 1;
-      after_step(P, e, r, R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i, autoreset, &sreg);
+      after_step(P, e, r, R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i, autoreset, &sreg, &R.R0);
     }
     store_won_mask(R.T.won_mask, won, t, R.n, wbase, wrows);
     if (R.T.obs)  // staged per wave: waves never wait for each other
@@ -1680,6 +1722,7 @@ __global__ __launch_bounds__(kBlock) void qnet_forward_kernel(const uint8_t* net
 
 struct QRollout {
   mg_params P;
+  Reset0 R0;
   mg_state S;
   mg_traj T;
   mg_stats St;
@@ -1738,7 +1781,7 @@ __device__ __forceinline__ void qnet_policy_step_n(const QRollout& R, Env (&e)[N
     won[j] = e[j].winner == 1;
     const bool finish = (R.flags & MG_AUTORESET) && r[j].done;
     after_step(R.P, e[j], r[j], R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i,
-               (R.flags & MG_AUTORESET) != 0);
+               (R.flags & MG_AUTORESET) != 0, nullptr, &R.R0);
     if (finish && R.St.rec) stats_add_q_eval(R.St, i, qrow[64 * j * kObs + a1[j]]);  // a1 in 0..4 here
   }
 }
@@ -1938,6 +1981,7 @@ __global__ void counter_add_kernel(uint64_t* counter, uint64_t k) { *counter += 
 // the episode ended, kept in LDS as bf16 pairs) and picks step t's action; E(X,t) steps.
 struct HRollout {
   mg_params P;
+  Reset0 R0;
   mg_state S;
   mg_traj T;
   mg_hdqn_traj H;
@@ -2299,7 +2343,7 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
           for (int q2 = 0; q2 < kObs / 2; ++q2)
             sd[q2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(
                                                       f32x2{static_cast<float>(rv.o[2 * q2]), static_cast<float>(rv.o[2 * q2 + 1])}, bf16x2));
-          finish_episode(R.P, ev, rv, R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i);
+          finish_episode(R.P, ev, rv, R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i, nullptr, &R.R0);
           st = goal_status(rv.dx1, ev.v2);  // the reset state the next step acts on
         } else if (lv && rv.first1) {
           note_first_arrival(R.St, i, rv);
@@ -2981,7 +3025,7 @@ void host_step_env(const Launch& L, int64_t i, bool& done, bool& won) {
     done = r.done;
     won = e.winner == 1;
     after_step(P, e, r, L.St, L.O.final_obs ? L.O.final_obs + i * kObs : nullptr, i,
-               (L.flags & MG_AUTORESET) != 0);
+               (L.flags & MG_AUTORESET) != 0, nullptr, &L.R0);
     store_env(L.S, i, e);
   }
   if (!L.O.rec64 && L.O.obs) {  // the kernel's observation tile: zeros for a bad action's env
@@ -3099,6 +3143,7 @@ int mg_step(const mg_params* params, const mg_state* state, const int8_t* a1, co
   if (!a1) return fail(hipErrorInvalidValue, "%s", "a1 is NULL");
   Launch L{};
   L.P = *params;
+  L.R0 = reset0(*params);
   L.S = *state;
   L.O = *out;
   if (stats) L.St = *stats;
@@ -3117,6 +3162,7 @@ int mg_step_random(const mg_params* params, const mg_state* state, int8_t* a1_ou
   if (n == 0) return 0;
   Launch L{};
   L.P = *params;
+  L.R0 = reset0(*params);
   L.S = *state;
   L.O = *out;
   if (stats) L.St = *stats;
@@ -3150,6 +3196,7 @@ int mg_rollout_random(const mg_params* params, const mg_state* state, const mg_t
   if (n == 0 || num_steps == 0) return 0;
   Rollout R{};
   R.P = *params;
+  R.R0 = reset0(*params);
   R.S = *state;
   R.T = *traj;
   if (stats) R.St = *stats;
@@ -3238,6 +3285,7 @@ int mg_rollout_qnet(const mg_params* params, const mg_state* state, const mg_tra
   if (n == 0 || num_steps == 0) return 0;
   QRollout R{};
   R.P = *params;
+  R.R0 = reset0(*params);
   R.S = *state;
   R.T = *traj;
   if (stats) R.St = *stats;
@@ -3311,6 +3359,7 @@ int mg_rollout_hdqn(const mg_params* params, const mg_state* state, const mg_tra
     return fail(hipErrorInvalidValue, "%s", "mg_rollout_hdqn needs MG_AUTORESET (hdqn.py resets every episode)");
   HRollout R{};
   R.P = *params;
+  R.R0 = reset0(*params);
   R.S = *state;
   R.T = *traj;
   if (htraj) R.H = *htraj;
@@ -3486,6 +3535,7 @@ int mg_host_step(const mg_params* params, const mg_state* state, const int8_t* a
   if (!a1) return fail(hipErrorInvalidValue, "%s", "a1 is NULL");
   Launch L{};
   L.P = *params;
+  L.R0 = reset0(*params);
   L.S = *state;
   L.O = *out;
   if (stats) L.St = *stats;

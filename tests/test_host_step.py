@@ -225,3 +225,30 @@ def test_host_step_equals_kernel():
     np.testing.assert_array_equal(drew.cpu().numpy().view(np.uint32), hb.rew.view(np.uint32))
     assert derr.item() == hb.err[0] == 3
     assert hb.flags[:, 2].any() and hb.flags[:, 3].any() and np.isfinite(hb.fobs).any()
+
+
+def test_host_collision_test_over_the_whole_plane(coracle):
+    """The step's collision test takes integer lateral edges where they equal the fp64 ones (y >= 8,
+    merging_hip.hip vehicles_collide) and the fp64 form elsewhere. Pairs of cars placed over the
+    whole reachable plane -- positions far past the end point, where the opponent's mirror arc
+    crosses y = 8 and 0, and pairs packed within a few metres of each other around the merge point
+    x = 0 -- collide exactly when the C oracle's fp64 boxes do (no autoreset, both cars held still)."""
+    n = 1 << 16
+    rng = np.random.default_rng(12)
+    hb = HostBatch(n)
+    base = rng.uniform(-3000, 9000, n)
+    p1 = np.where(rng.random(n) < 0.5, base, rng.uniform(985, 1016, n))
+    p2 = np.where(rng.random(n) < 0.7, p1 + rng.uniform(-10, 10, n), rng.uniform(-3000, 9000, n))
+    for k, v in (("p1", p1), ("p2", p2)):
+        hb.s[k][:] = v
+    hb.s["v1"][:] = hb.s["v2"][:] = 0.0
+    envs = coracle.new_envs(n)
+    envs["pos1"], envs["pos2"] = p1, p2
+    a1 = np.zeros(n, np.int8)  # target speed 0 from speed 0: the cars stay where they are
+    hb.step(a1, None, autoreset=False)
+    _, _, _, o_coll, _, _, err = coracle.step(envs, a1, None)
+    assert err == 0
+    np.testing.assert_array_equal(hb.flags[:, 3], o_coll)
+    y2 = 150.0 - 30000.0 * (1 - np.cos(np.arctan2(1000, 30000) - p2 / 30000))
+    # the fp64 branch runs (y2 < 8: the ego's arc stays at y >= 150, so those pairs never touch)
+    assert o_coll.sum() > 1000 and (y2 < 8).sum() > 1000
