@@ -337,13 +337,18 @@ int mg_qnet_fragments(const void* packed, void* fragments, void* stream);
 int mg_qnet_forward(const void* packed, const float* x, int32_t in_dim, int32_t swap_halves, float* q,
                     int64_t n, void* stream);
 
-/* num_steps steps in ONE launch with the epsilon-greedy Q-net policy computed on the device:
- * for each env and step, Philox4x32-10 (key = seed, counter = (env_offset + i, first_step + t))
- * gives u = (u0, u1, u2, u3); the ego acts greedily (argmax of Q(obs), lowest index on ties)
- * when u0 < greedy_threshold and takes floor(5 u1 / 2^32) otherwise -- greedy_threshold =
- * round(Phi(0.7) 2^32) reproduces `np.random.randn() <= EPISILO` (main.py:105). The opponent
- * is None (opponent_mode 0), uniform floor(5 u3 / 2^32) (1), the same net on the swapped
- * observation with u2 / u3 and opp_greedy_threshold (2, Strategy_OP "selfplay", main.py:165-166),
+/* num_steps steps in ONE launch with the epsilon-greedy Q-net policy computed on the device,
+ * Philox4x32-10 draws with key = seed. The ego acts greedily (argmax of Q(obs), lowest index on
+ * ties) when its explore draw e < greedy_threshold and at random otherwise -- greedy_threshold =
+ * round(Phi(0.7) 2^32) reproduces `np.random.randn() <= EPISILO` (main.py:105).
+ * opponent_mode 0 (None) and 1 (uniform) -- two draws per step (ABI 20): step k = first_step + t
+ * of env gi = env_offset + i takes words (u0, u1) of counter (gi, k div 2) when k is even and
+ * (u2, u3) when k is odd; e = the first, and the second w gives the random action floor(5 w / 2^32)
+ * (mode 0, opponent None) or the pair x = floor(25 w / 2^32), a1 = x div 5 (used when exploring),
+ * a2 = x mod 5 (the uniform opponent, mode 1).
+ * opponent_mode 2 and 3 -- counter (gi, k): u0 / u1 the ego's explore draw / random action
+ * floor(5 u1 / 2^32), u2 / u3 the opponent's with opp_greedy_threshold: the same net on the swapped
+ * observation (2, Strategy_OP "selfplay", main.py:165-166),
  * or another packed net opp_net (same out_dim) on the swapped observation the same way (3,
  * main.py's default Strategy_OP "L1": a separately trained DQN as the opponent, :161-168, :199;
  * ABI 14; opp_net is ignored by the other modes). Outputs as mg_rollout_random

@@ -1741,9 +1741,15 @@ struct QRollout {
 
 
 // One epsilon-greedy step (main.py:99-112) of the N envs i0 + 64 j of one env-wave lane given their
-// greedy actions, stepped in lockstep: Philox4x32-10 per (global env, step) gives u.x the ego's
-// explore draw, u.y its random action, u.z the opponent's explore draw, u.w its random action. Envs
-// past n (live[j] false) are stepped too but never stored. A greedy action outside 0..4 (a
+// greedy actions, stepped in lockstep. Draws (ABI 20), Philox4x32-10 keyed by seed:
+//  * OPP 0 / 1 (no net opponent): two draws per step, so one call serves two steps -- step k takes
+//    words (x, y) of call (gi, k div 2) when k is even and (z, w) when k is odd (kept from the even
+//    step in `keep`, or computed when a launch starts on an odd step). The first word is the ego's
+//    explore draw; the second its random action floor(5 w / 2^32), or with the uniform opponent the
+//    pair x = floor(25 w / 2^32), a1 = x div 5, a2 = x mod 5 (one word, as the random-policy stream).
+//  * OPP 2 / 3: call (gi, k) per step: u.x the ego's explore draw, u.y its random action, u.z the
+//    opponent's explore draw, u.w its random action.
+// Envs past n (live[j] false) are stepped too but never stored. A greedy action outside 0..4 (a
 // net with out_dim > 5) gets env_step's KeyError semantics (env_step_lockstep).
 // qrow: the tile row of env i0 (rows of envs i0 + 64 j follow 64 rows apart), where the Q-net wave
 // left eval_net(state)[0..4] of the state the step acts on: a finishing env logs q[a1] (main.py:221).
@@ -1751,21 +1757,44 @@ template <int OPP, int N, bool CHECKED>
 __device__ __forceinline__ void qnet_policy_step_n(const QRollout& R, Env (&e)[N], StepOut (&r)[N],
                                                    int64_t i0, const bool (&live)[N], int t,
                                                    const int (&greedy1)[N], const int (&greedy2)[N],
-                                                   bool (&won)[N], const float* qrow) {
+                                                   bool (&won)[N], const float* qrow, uint2 (&keep)[N]) {
   const uint64_t step = R.first_step + t;
   int a1[N], a2[N];
 #pragma unroll
   for (int j = 0; j < N; ++j) {
     const uint64_t gi = static_cast<uint64_t>(R.env_offset + i0 + 64 * j);
-    const uint4 u = philox4x32_10(
-        make_uint4(static_cast<uint32_t>(gi), static_cast<uint32_t>(gi >> 32),
-                   static_cast<uint32_t>(step), static_cast<uint32_t>(step >> 32)),
-        static_cast<uint32_t>(R.seed), static_cast<uint32_t>(R.seed >> 32));
-    a1[j] = (static_cast<uint64_t>(u.x) < R.greedy_thr) ? greedy1[j] : action_from_u32(u.y);
-    a2[j] = MG_ACTION_NONE;
-    if constexpr (OPP == 1) a2[j] = action_from_u32(u.w);
-    if constexpr (OPP >= 2)
+    if constexpr (OPP < 2) {
+      uint32_t ex, pick;
+      if ((step & 1) == 0 || t == 0) {  // wave-uniform: a fresh call feeds this step and the next
+        const uint4 u = philox4x32_10(
+            make_uint4(static_cast<uint32_t>(gi), static_cast<uint32_t>(gi >> 32),
+                       static_cast<uint32_t>(step >> 1), static_cast<uint32_t>(step >> 33)),
+            static_cast<uint32_t>(R.seed), static_cast<uint32_t>(R.seed >> 32));
+        keep[j] = make_uint2(u.z, u.w);
+        ex = (step & 1) ? u.z : u.x;
+        pick = (step & 1) ? u.w : u.y;
+      } else {
+        ex = keep[j].x;
+        pick = keep[j].y;
+      }
+      const bool greedy = static_cast<uint64_t>(ex) < R.greedy_thr;
+      if constexpr (OPP == 1) {  // (random a1, uniform a2) from one 25-way draw
+        const uint32_t x = static_cast<uint32_t>((static_cast<uint64_t>(pick) * 25u) >> 32);
+        const int b1 = static_cast<int>((x * 13u) >> 6);  // x div 5 for x < 25
+        a1[j] = greedy ? greedy1[j] : b1;
+        a2[j] = static_cast<int>(x) - 5 * b1;
+      } else {
+        a1[j] = greedy ? greedy1[j] : action_from_u32(pick);
+        a2[j] = MG_ACTION_NONE;
+      }
+    } else {
+      const uint4 u = philox4x32_10(
+          make_uint4(static_cast<uint32_t>(gi), static_cast<uint32_t>(gi >> 32),
+                     static_cast<uint32_t>(step), static_cast<uint32_t>(step >> 32)),
+          static_cast<uint32_t>(R.seed), static_cast<uint32_t>(R.seed >> 32));
+      a1[j] = (static_cast<uint64_t>(u.x) < R.greedy_thr) ? greedy1[j] : action_from_u32(u.y);
       a2[j] = (static_cast<uint64_t>(u.z) < R.opp_greedy_thr) ? greedy2[j] : action_from_u32(u.w);
+    }
   }
   env_step_lockstep<N, CHECKED>(R.P, e, a1, a2, r);
 #pragma unroll
@@ -1901,6 +1930,7 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
   Env e0[kIlp], e1[kIlp];
   StepOut r[kIlp];
   bool live0[kIlp], live1[kIlp];
+  uint2 keep0[kIlp], keep1[kIlp];  // OPP 0 / 1: the odd step's two draw words (qnet_policy_step_n)
 #pragma unroll
   for (int j = 0; j < kIlp; ++j) {
     const int la = lbase + 64 * j + lane, lb = kHalf + la;
@@ -1924,9 +1954,11 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
       // wave-uniform branch: each group's envs stay in named registers
       const float* qrow = tile + (local0 + lane) * kObs;
       if (g == 0)
-        qnet_policy_step_n<OPP, kIlp, CHECKED>(R, e0, r, base + local0 + lane, live0, t, greedy1, greedy2, won, qrow);
+        qnet_policy_step_n<OPP, kIlp, CHECKED>(R, e0, r, base + local0 + lane, live0, t, greedy1, greedy2, won, qrow,
+                                               keep0);
       else
-        qnet_policy_step_n<OPP, kIlp, CHECKED>(R, e1, r, base + local0 + lane, live1, t, greedy1, greedy2, won, qrow);
+        qnet_policy_step_n<OPP, kIlp, CHECKED>(R, e1, r, base + local0 + lane, live1, t, greedy1, greedy2, won, qrow,
+                                               keep1);
       const int64_t wbase = base + local0;
 #pragma unroll
       for (int j = 0; j < kIlp; ++j) {

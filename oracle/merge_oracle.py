@@ -436,6 +436,26 @@ def qnet_reference(weights, obs, bf16: bool = True, swap: bool = False):
     return h.numpy()
 
 
+def qnet_policy_draws(words, step, opponent):
+    """The epsilon-greedy draws of mg_rollout_qnet at global step `step` (merging_hip.hip
+    qnet_policy_step_n, ABI 20), restated: words(c) -> [n, 4] uint32 Philox4x32-10 words of counter
+    (gi, c) for the envs checked. opponent "none" / "uniform" (two draws per step, one call per two
+    steps): words (x, y) of call step div 2 on even steps, (z, w) on odd ones; explore = the first,
+    the random action floor(5 w / 2^32) of the second -- or with the uniform opponent the pair
+    x = floor(25 w / 2^32), a1 = x div 5, a2 = x mod 5. Net opponents ("self" / "other"): call `step`,
+    (x, y) the ego's explore / random action, (z, w) the opponent's. Returns (explore [n] u64,
+    random a1 [n], opponent explore [n] u64 or None, random a2 [n] or None)."""
+    if opponent in ("none", "uniform"):
+        u = words(step >> 1).astype(np.uint64)
+        ex, pick = (u[:, 2], u[:, 3]) if step & 1 else (u[:, 0], u[:, 1])
+        if opponent == "none":
+            return ex, (pick * 5) >> 32, None, None
+        x = (pick * 25) >> 32
+        return ex, x // 5, None, x % 5
+    u = words(step).astype(np.uint64)
+    return u[:, 0], (u[:, 1] * 5) >> 32, u[:, 2], (u[:, 3] * 5) >> 32
+
+
 # --------------------------------------------------------------------------- replay memory oracle
 
 def goal_status64(obs):

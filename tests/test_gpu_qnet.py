@@ -110,8 +110,8 @@ def test_qnet_forward_hdqn_nets(torch, coracle, in_dim, out_dim):
         qnet.forward(torch.zeros((4, in_dim + 1), device="cuda:0"))
 
 
-@pytest.mark.parametrize("opponent,n", [("none", 4096), ("uniform", 4096), ("self", 4096),
-                                        ("none", 1000), ("self", 577), ("other", 4096), ("other", 577)])
+@pytest.mark.parametrize("opponent,n", [("none", 4096), ("uniform", 4096), ("self", 4096), ("none", 1000),
+                                        ("uniform", 1001), ("self", 577), ("other", 4096), ("other", 577)])
 def test_rollout_qnet_policy_and_transitions(torch, coracle, nets, opponent, n):
     """Every action is the epsilon-greedy choice (Philox draws exact, greedy = argmax of the
     bf16 reference except near-ties) and every transition equals the CPU oracle's. The odd
@@ -121,7 +121,7 @@ def test_rollout_qnet_policy_and_transitions(torch, coracle, nets, opponent, n):
     from merging_gym import MergeVecEnv
     from merging_gym.policy import QNet, greedy_threshold
 
-    T, seed, k0 = 24, 17, 500
+    T, seed, k0 = 24, 17, 500 + n % 2  # odd sizes start on an odd step (the second word pair of a call)
     qnet = QNet.from_state_dict(nets["l1"], device="cuda:0")
     env = MergeVecEnv(n, device="cuda:0")
     for k in range(200):  # mid-episode start: episodes end inside the window (autoreset, q_eval)
@@ -143,22 +143,21 @@ def test_rollout_qnet_policy_and_transitions(torch, coracle, nets, opponent, n):
     thr = greedy_threshold(0.7)
     cc1 = ChoiceCheck(f"rollout ego l1 ({opponent}, n={n})", max_frac=MAX_EXCUSED["l1"])
     cc2 = ChoiceCheck(f"rollout opponent {opp_key} ({opponent}, n={n})", max_frac=MAX_EXCUSED[opp_key])
+    mode = "self" if opponent == "other" else opponent  # the draw layout of a net opponent
     for t in range(T):
-        u = coracle.philox_batch(n, 0, seed, k0 + t)
+        ex, rnd1, ex2, rnd2 = mo.qnet_policy_draws(lambda c: coracle.philox_batch(n, 0, seed, c), k0 + t, mode)
         q = mo.qnet_reference(nets["l1"], obs_in, bf16=True)
-        greedy = u[:, 0].astype(np.uint64) < thr
-        exp1 = np.where(greedy, q.argmax(1), (u[:, 1].astype(np.uint64) * 5) >> 32)
+        greedy = ex < thr
+        exp1 = np.where(greedy, q.argmax(1), rnd1)
         cc1.check(traj["a1"][t], exp1, greedy, q, f"step {t}")
         if opponent == "none":
             assert (traj["a2"][t] == -1).all()
+        elif opponent == "uniform":
+            assert (traj["a2"][t] == rnd2).all()
         else:
-            rnd2 = (u[:, 3].astype(np.uint64) * 5) >> 32
-            if opponent == "uniform":
-                assert (traj["a2"][t] == rnd2).all()
-            else:
-                q2 = mo.qnet_reference(nets[opp_key], obs_in, bf16=True, swap=True)
-                g2 = u[:, 2].astype(np.uint64) < thr
-                cc2.check(traj["a2"][t], np.where(g2, q2.argmax(1), rnd2), g2, q2, f"step {t}")
+            q2 = mo.qnet_reference(nets[opp_key], obs_in, bf16=True, swap=True)
+            g2 = ex2 < thr
+            cc2.check(traj["a2"][t], np.where(g2, q2.argmax(1), rnd2), g2, q2, f"step {t}")
         # the transition, with the actions the kernel took
         o_obs, o_rew, o_done, o_coll, _, o_fobs, err = coracle.step(
             envs, traj["a1"][t], traj["a2"][t], autoreset=True, final_obs=True)
@@ -286,16 +285,17 @@ def test_rollout_qnet_full_size(torch, coracle, nets, opponent):
     stats = (ret_sum0.copy(), counts0.copy())
     cc1 = ChoiceCheck(f"full-size ego l1 ({opponent})", max_frac=MAX_EXCUSED["l1"])
     cc2 = ChoiceCheck(f"full-size opponent {opp_key} ({opponent})", max_frac=MAX_EXCUSED[opp_key])
+    words = lambda c: np.stack([coracle.philox_batch(1, int(gi), seed, c)[0] for gi in idx_np])  # noqa: E731
+    mode = "none" if opponent == "none" else "self"
     for t in range(T):
-        u = np.stack([coracle.philox_batch(1, int(gi), seed, k0 + t)[0] for gi in idx_np])
+        ex, rnd1, ex2, rnd2 = mo.qnet_policy_draws(words, k0 + t, mode)
         q = mo.qnet_reference(nets["l1"], obs_in, bf16=True)
-        greedy = u[:, 0].astype(np.uint64) < thr
-        exp1 = np.where(greedy, q.argmax(1), (u[:, 1].astype(np.uint64) * 5) >> 32)
+        greedy = ex < thr
+        exp1 = np.where(greedy, q.argmax(1), rnd1)
         cc1.check(sub["a1"][t], exp1, greedy, q, f"step {t}")
-        rnd2 = (u[:, 3].astype(np.uint64) * 5) >> 32
         if opponent in ("self", "other"):
             q2 = mo.qnet_reference(nets[opp_key], obs_in, bf16=True, swap=True)
-            g2 = u[:, 2].astype(np.uint64) < thr
+            g2 = ex2 < thr
             cc2.check(sub["a2"][t], np.where(g2, q2.argmax(1), rnd2), g2, q2, f"step {t}")
         o_obs, o_rew, o_done, o_coll, _, o_fobs, err = coracle.step(
             envs, sub["a1"][t], sub["a2"][t], autoreset=True, final_obs=True, stats=stats)
