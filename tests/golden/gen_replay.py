@@ -202,6 +202,78 @@ def run_hdqn(hdqn_mod, env, steps, opp_random, seed):
             "ep_reward": np.asarray(reward_list, np.float64), "ep_win": np.asarray(win_list, np.bool_)}
 
 
+def _load_net(net, sd):
+    """The reference Net's parameters from a state dict of numpy arrays (weights-only data)."""
+    import torch
+
+    net.load_state_dict({k: torch.from_numpy(np.asarray(v, np.float32)) for k, v in sd.items()})
+
+
+def run_q_eval_main(main_mod, env, episodes, seed, weights):
+    """main.py's q_eval log (:189-228) from its own DQN: dqn.choose_action(state) (:195, the seeded
+    np.random drives its epsilon-greedy branch), env.step, the :218-220 break, then
+    q_eval_value = dqn.eval_net.forward(torch.Tensor(state))[action] (:221; .cuda() dropped: no GPU
+    here) on the state the last step acted on and its action. eval_net carries the shipped
+    checkpoint the bench uses (tests/golden/dqn_checkpoints.npz, l1). Records per episode the
+    logged value, that state and that action, and every action taken."""
+    import torch
+
+    np.random.seed(seed)
+    dqn = main_mod.DQN()
+    _load_net(dqn.eval_net, weights)
+    q_list, s_list, a_list, acts = [], [], [], []
+    with contextlib.redirect_stdout(io.StringIO()):
+        for _ in range(episodes):
+            state = env.reset()
+            while True:
+                action = int(dqn.choose_action(state))
+                acts.append(action)
+                next_state, rewards, done, info = env.step(action, None)  # Strategy_OP "L0"
+                if done:
+                    break
+                state = next_state
+            q = dqn.eval_net.forward(torch.Tensor(state))[action]  # :221
+            q_list.append(float(q))
+            s_list.append(np.asarray(state, np.float64))
+            a_list.append(action)
+    return {"q_eval": np.asarray(q_list, np.float32), "state": np.stack(s_list), "action": np.asarray(a_list, np.int8),
+            "actions": np.asarray(acts, np.int8)}
+
+
+def run_q_eval_hdqn(hdqn_mod, env, episodes, seed, meta_sd):
+    """hdqn.py's q_eval log (:276-333): the loop of main() with its own Goal_DQN choosing the goals
+    (upper.choose_goal at :283 and :303, seeded np.random) and seeded actions standing in for the
+    lower-level net, then q_eval_value = upper.meta_eval_net.forward(torch.Tensor(state))[goal] (:330)
+    with state the terminal observation (state = next_state, :320) and goal the :303 choice on it.
+    meta_sd: seeded Net(10, 3) weights (no h-DQN checkpoint ships with the reference)."""
+    import torch
+
+    np.random.seed(seed)
+    rng = np.random.default_rng(seed)
+    upper = hdqn_mod.Goal_DQN()
+    _load_net(upper.meta_eval_net, meta_sd)
+    q_list, s_list, g_list, acts = [], [], [], []
+    with contextlib.redirect_stdout(io.StringIO()):
+        for _ in range(episodes):
+            state = env.reset()
+            done = False
+            while not done:
+                goal = upper.choose_goal(state)  # :283
+                while not done:
+                    acts.append(int(rng.integers(0, 5)))
+                    next_state, rewards, done, info = env.step(acts[-1], None)
+                    goal = upper.choose_goal(next_state)  # :303
+                    state = next_state  # :320
+                    if done or goal == hdqn_mod.goal_status(state):  # :322
+                        break
+            q = upper.meta_eval_net.forward(torch.Tensor(state))[goal]  # :330
+            q_list.append(float(q))
+            s_list.append(np.asarray(state, np.float64))
+            g_list.append(int(goal))
+    return {"q_eval": np.asarray(q_list, np.float32), "state": np.stack(s_list), "goal": np.asarray(g_list, np.int8),
+            "actions": np.asarray(acts, np.int8)}
+
+
 def main():
     sys.path.insert(0, HERE)
     from gen_golden import load_reference_env
@@ -232,6 +304,21 @@ def main():
               "main wins", int(res["main_win"].sum()), "hdqn wins", int(res["hdqn_win"].sum()),
               "filtered != total", int((res["main_reward"] != res["hdqn_reward"]).sum()))
     out.update({f"GS_{k}": v for k, v in goal_status_rows(hdqn_mod).items()})
+    # q_eval as the scripts log it (main.py:221, hdqn.py:330), from the reference's own nets
+    ck = np.load(os.path.join(HERE, "dqn_checkpoints.npz"))
+    l1 = {k.split("/", 1)[1]: ck[k] for k in ck.files if k.startswith("l1/")}
+    res = run_q_eval_main(main_mod, env, 40, 51, l1)
+    out.update({f"QM_{k}": v for k, v in res.items()})
+    print("QM episodes", len(res["q_eval"]), "mean q_eval", float(res["q_eval"].mean()))
+    mrng = np.random.default_rng(52)
+    meta_sd = {}
+    for name, (o, i) in zip(("fc1", "fc2", "out"), [(200, 10), (100, 200), (3, 100)]):
+        meta_sd[f"{name}.weight"] = mrng.uniform(-i ** -0.5, i ** -0.5, (o, i)).astype(np.float32)
+        meta_sd[f"{name}.bias"] = mrng.uniform(-i ** -0.5, i ** -0.5, o).astype(np.float32)
+    res = run_q_eval_hdqn(hdqn_mod, env, 40, 53, meta_sd)
+    out.update({f"QH_{k}": v for k, v in res.items()})
+    out.update({f"QH_net_{k}": v for k, v in meta_sd.items()})
+    print("QH episodes", len(res["q_eval"]), "mean q_eval", float(res["q_eval"].mean()))
     np.savez_compressed(OUT, **out)
     print("wrote", OUT, os.path.getsize(OUT), "bytes")
 

@@ -189,3 +189,55 @@ def test_stats_reduce_restatement_order():
         for k, col in enumerate((0, 1, 2, 7)):
             ref = scalar(rec[:, col].tolist())
             assert np.float64(sums[k]).view(np.uint64) == np.float64(ref).view(np.uint64), (n, k)
+
+
+def test_q_eval_golden_semantics():
+    """The q_eval the scripts log (tests/golden/gen_replay.py ran the reference's own loops):
+    main.py:221 evaluates eval_net on the state the episode's last step acted on, at that step's
+    action; hdqn.py:330 evaluates meta_eval_net on the terminal state, at the goal chosen on it.
+    Replaying the recorded actions through the oracle env finds exactly those states, and the
+    oracle's fp32 Net (merge_oracle.qnet_reference) gives the logged values -- the quantities the
+    config-5 and h-DQN kernels add to mg_episode_stats.q_eval (checked on the GPU against the
+    bf16-emulated nets, tests/choice_check.check_q_eval)."""
+    import os
+
+    import numpy as np
+
+    import merge_oracle as mo
+    from conftest import ROOT
+
+    g = np.load(os.path.join(ROOT, "tests", "golden", "replay_golden.npz"))
+    ck = np.load(os.path.join(ROOT, "tests", "golden", "dqn_checkpoints.npz"))
+    l1 = {k.split("/", 1)[1]: ck[k] for k in ck.files if k.startswith("l1/")}
+    # main.py: the pre-terminal state and the last action
+    env, k, pre, last = mo.PyMergeEnv(), 0, [], []
+    for _ in range(len(g["QM_q_eval"])):
+        state = env.reset()
+        while True:
+            a = int(g["QM_actions"][k])
+            k += 1
+            nxt, _, done, _ = env.step(a, None)
+            if done:
+                break
+            state = nxt
+        pre.append(state)
+        last.append(a)
+    assert k == len(g["QM_actions"])
+    np.testing.assert_allclose(np.asarray(pre, float), g["QM_state"], rtol=0, atol=1e-9)
+    np.testing.assert_array_equal(last, g["QM_action"])
+    q = mo.qnet_reference(l1, g["QM_state"].astype(np.float32), bf16=False)
+    np.testing.assert_allclose(q[np.arange(len(last)), g["QM_action"]], g["QM_q_eval"], rtol=1e-5, atol=1e-6)
+    # hdqn.py: the terminal state and the goal chosen on it
+    meta = {k[len("QH_net_"):]: g[k] for k in g.files if k.startswith("QH_net_")}
+    env, k, term = mo.PyMergeEnv(), 0, []
+    for _ in range(len(g["QH_q_eval"])):
+        env.reset()
+        done = False
+        while not done:
+            nxt, _, done, _ = env.step(int(g["QH_actions"][k]), None)
+            k += 1
+        term.append(nxt)
+    assert k == len(g["QH_actions"])
+    np.testing.assert_allclose(np.asarray(term, float), g["QH_state"], rtol=0, atol=1e-9)
+    qh = mo.qnet_reference(meta, g["QH_state"].astype(np.float32), bf16=False)
+    np.testing.assert_allclose(qh[np.arange(len(term)), g["QH_goal"]], g["QH_q_eval"], rtol=1e-5, atol=1e-6)
