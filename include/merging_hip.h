@@ -390,8 +390,10 @@ typedef struct mg_hdqn_traj {
  * ABI 17 rejects a launch without it). goal [n] int8 holds each env's current goal across launches (< 0: none
  * yet -- chosen by the meta-net at the first step). Random draws: Philox4x32-10 with key seed,
  * counter (env_offset + i, first_step + t) for the action and next goal (x, y, z, w = explore,
- * action, explore, goal) and counter ((env_offset + i) ^ 2^63, first_step + t) for a fresh goal
- * (x, y) and the uniform opponent (z); a launch's first fresh goals use step first_step - 1.
+ * action, explore, goal) and stream B, counter ((env_offset + i) ^ 2^63, c), for a fresh goal's
+ * explore / goal draws of step k: with the uniform opponent (mode 1) words (x, y) of c = k, its
+ * action from z; otherwise (ABI 20) one call per two steps, c = k div 2, words (x, y) on even k
+ * and (z, w) on odd k. A launch's first fresh goals use step first_step - 1.
  * Greedy when the explore draw < greedy_threshold (np.random.randn() <= EPISILO, :84, :168).
  * traj as mg_rollout_qnet; opponent_mode 0 (None, Strategy_OP "L0", :261, :294-296), 1 (uniform),
  * 2 (Strategy_OP "selfplay", :262-264: upper_op = upper, lower_op = lower, so the same two

@@ -2058,6 +2058,29 @@ __device__ __forceinline__ uint4 philox_env_step(uint64_t gi, uint64_t step, uin
                        static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32));
 }
 
+// The fresh-goal draws (explore, goal) of step k from stream B (counter gi ^ 2^63). Every opponent
+// but the uniform one uses two words of B per step, so one call serves two steps (ABI 20): call
+// k div 2, words (x, y) on even steps and (z, w) on odd ones; `keep` carries the odd step's pair
+// from the even step (fresh: compute the call, as at a launch's first step). The uniform opponent
+// also draws its action from B (word z of call k), one call per step.
+template <int OPP>
+__device__ __forceinline__ uint2 fresh_goal_words(uint64_t gi, uint64_t k, uint64_t seed, bool fresh, uint2& keep,
+                                                  uint32_t& opp_word) {
+  if constexpr (OPP == 1) {
+    const uint4 u = philox_env_step(gi ^ (uint64_t{1} << 63), k, seed);
+    opp_word = u.z;
+    return make_uint2(u.x, u.y);
+  } else {
+    opp_word = 0u;
+    if ((k & 1) == 0 || fresh) {
+      const uint4 u = philox_env_step(gi ^ (uint64_t{1} << 63), k >> 1, seed);
+      keep = make_uint2(u.z, u.w);
+      return (k & 1) ? keep : make_uint2(u.x, u.y);
+    }
+    return keep;
+  }
+}
+
 // lower-net input of one env: goal state [goal] + state (hdqn.py:291), features 0..10, zero at
 // 11..12 and the bias inputs 1.0 at 13..15; swap: [goal] + state[5:] + state[:5] (the
 // opponent's goal state, :299)
@@ -2224,6 +2247,7 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
   // on in a later launch continues the loops already in flight correctly
   const bool outer = R.ext_acc != nullptr;
   double acc[2] = {0.0, 0.0};
+  uint2 kb[2] = {make_uint2(0u, 0u), make_uint2(0u, 0u)};  // each group's odd-step fresh-goal words
   auto finish_outer = [&](int g, int t, double& ac) __attribute__((always_inline)) {
     const int j = g * kHHalf + 64 * ew + lane;
     const int64_t i = base + j;
@@ -2292,7 +2316,9 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
 #pragma unroll
     for (int k = 0; k < kObs / 2; ++k) t2[k] = make_float2(static_cast<float>(o[2 * k]), static_cast<float>(o[2 * k + 1]));
     const uint64_t gi = static_cast<uint64_t>(R.env_offset + i);
-    const uint4 fb = philox_env_step(gi ^ (uint64_t{1} << 63), R.first_step - 1, R.seed);
+    uint2 unused_keep;
+    uint32_t unused_word;
+    const uint2 fb = fresh_goal_words<OPP>(gi, R.first_step - 1, R.seed, true, unused_keep, unused_word);
     b_df[j] = draw_byte(fb.x, fb.y, R.greedy_thr, R.num_goals);
     b_goal[j] = live[g] ? static_cast<uint8_t>(R.goal[i]) : 0;
     if (outer && live[g]) acc[g] = R.ext_acc[i];
@@ -2312,9 +2338,11 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
       const int64_t wbase = base + g * kHHalf + 64 * ew;
       const uint64_t gi = static_cast<uint64_t>(R.env_offset + i), k = R.first_step + t;
       const uint4 ua = philox_env_step(gi, k, R.seed);
-      const uint4 ub = philox_env_step(gi ^ (uint64_t{1} << 63), k, R.seed);
+      uint32_t opp_word;
+      const uint2 ub = g == 0 ? fresh_goal_words<OPP>(gi, k, R.seed, t == 0, kb[0], opp_word)
+                              : fresh_goal_words<OPP>(gi, k, R.seed, t == 0, kb[1], opp_word);
       const int a1 = static_cast<uint64_t>(ua.x) < R.greedy_thr ? static_cast<int>(b_act[j]) : action_from_u32(ua.y);
-      int a2 = OPP == 1 ? action_from_u32(ub.z) : MG_ACTION_NONE;
+      int a2 = OPP == 1 ? action_from_u32(opp_word) : MG_ACTION_NONE;
       uint4 uc = make_uint4(0u, 0u, 0u, 0u);
       if constexpr (kOpNets) {  // the self-play opponent's epsilon-greedy action (:300)
         uc = philox_env_step(gi ^ (uint64_t{1} << 62), k, R.seed);

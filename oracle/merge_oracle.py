@@ -456,6 +456,21 @@ def qnet_policy_draws(words, step, opponent):
     return u[:, 0], (u[:, 1] * 5) >> 32, u[:, 2], (u[:, 3] * 5) >> 32
 
 
+def hdqn_fresh_draws(words, step, opponent):
+    """The fresh-goal draws (explore, goal word) of mg_rollout_hdqn at global step `step` from stream
+    B (counter gi ^ 2^63; merging_hip.hip fresh_goal_words, ABI 20), restated: words(c) -> [n, 4]
+    uint32 words of counter (gi ^ 2^63, c). Every opponent but "uniform": one call per two steps --
+    call step div 2, words (x, y) on even steps, (z, w) on odd ones. "uniform": call `step`, (x, y),
+    and z is the opponent's action word. Returns (explore, goal word, uniform-opponent word or None);
+    `step` is taken mod 2^64 (a launch at step 0 draws its first goals at step 2^64 - 1)."""
+    step %= 1 << 64
+    if opponent == "uniform":
+        u = words(step)
+        return u[:, 0], u[:, 1], u[:, 2]
+    u = words(step >> 1)
+    return (u[:, 2], u[:, 3], None) if step & 1 else (u[:, 0], u[:, 1], None)
+
+
 # --------------------------------------------------------------------------- replay memory oracle
 
 def goal_status64(obs):

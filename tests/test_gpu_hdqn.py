@@ -233,11 +233,12 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
         ring.store_rollout(torch.from_numpy(obs_first).to(dev), tr, skip_ego_won=False, goal=tr["goal"],
                            next_goal=tr["next_goal"], reward=tr["reward"])
         # the launch's first goals: carried over, or a fresh choice with step k0 - 1's draw
+        fresh_words = lambda c: coracle.philox_batch(n, fresh_off, seed, c)  # noqa: E731
         if goal_prev is None:
-            fb = coracle.philox_batch(n, fresh_off, seed, k0 - 1)
+            fx, fy, _ = mo.hdqn_fresh_draws(fresh_words, k0 - 1, opponent)
             qm = mo.qnet_reference(meta_sd, obs, bf16=True)
-            exp = np.where(fb[:, 0] < thr, qm.argmax(1), _pick(fb[:, 1], NUM_GOALS))
-            cc_g.check(g["goal"][0], exp, fb[:, 0] < thr, qm, f"launch {launch} first goals")
+            exp = np.where(fx < thr, qm.argmax(1), _pick(fy, NUM_GOALS))
+            cc_g.check(g["goal"][0], exp, fx < thr, qm, f"launch {launch} first goals")
         else:
             assert (g["goal"][0] == goal_prev).all(), launch
         if selfplay:  # the opponent's first goal (:285): carried over, or fresh with step k0 - 1's draw
@@ -254,7 +255,7 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
         for t in range(T):
             k = k0 + t
             ua = coracle.philox_batch(n, 0, seed, k)
-            ub = coracle.philox_batch(n, fresh_off, seed, k)
+            ubx, uby, _ = mo.hdqn_fresh_draws(fresh_words, k, opponent)
             goal_t = g["goal"][t].astype(np.int64)
             x = np.concatenate([goal_t[:, None].astype(np.float32), obs], axis=1)  # [goal] + state
             q1 = mo.qnet_reference(lower_sd, x, bf16=True)
@@ -302,8 +303,8 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
                                   rew_all[t][None], d[None], fo_all[t][None], ~brk[None],
                                   reward=acc.astype(np.float32)[None], meta_goal=g["next_goal"][t][None])
             acc[brk] = 0.0
-            gf = ub[:, 0] < thr
-            fresh = np.where(gf, np.where(d, reset_goal, q2.argmax(1)), _pick(ub[:, 1], NUM_GOALS))
+            gf = ubx < thr
+            fresh = np.where(gf, np.where(d, reset_goal, q2.argmax(1)), _pick(uby, NUM_GOALS))
             exp_next = np.where(brk, fresh, g2)
             nxt = g["goal"][t + 1] if t + 1 < T else env.hdqn_goal.cpu().numpy().astype(np.int64)
             cc_g.check(nxt, exp_next, brk & gf & ~d, q2, f"fresh goal, launch {launch} step {t}")
@@ -411,13 +412,14 @@ def test_fused_hdqn_rollout_full_size(coracle, nets):
     sub = {k: tr[k][:, idx].cpu().numpy() for k in ("a1", "done", "obs", "rew", "final_observation", "goal",
                                                        "next_goal", "reward")}
     thr = greedy_threshold()
-    fresh = _philox_words(idx_np.astype(np.uint64) ^ np.uint64(1 << 63), seed, k0 - 1)
+    fresh_words = lambda c: _philox_words(idx_np.astype(np.uint64) ^ np.uint64(1 << 63), seed, c)  # noqa: E731
+    fx, fy, _ = mo.hdqn_fresh_draws(fresh_words, k0 - 1, "none")
     qm = mo.qnet_reference(meta_sd, obs, bf16=True)
-    exp0 = np.where(fresh[:, 0] < thr, qm.argmax(1), _pick(fresh[:, 1], NUM_GOALS))
-    cc_g.check(sub["goal"][0], exp0, fresh[:, 0] < thr, qm, "first goals")
+    exp0 = np.where(fx < thr, qm.argmax(1), _pick(fy, NUM_GOALS))
+    cc_g.check(sub["goal"][0], exp0, fx < thr, qm, "first goals")
     for t in range(T):
         ua = _philox_words(idx_np, seed, k0 + t)
-        ub = _philox_words(idx_np.astype(np.uint64) ^ np.uint64(1 << 63), seed, k0 + t)
+        ubx, uby, _ = mo.hdqn_fresh_draws(fresh_words, k0 + t, "none")
         goal_t = sub["goal"][t].astype(np.int64)
         q1 = mo.qnet_reference(lower_sd, np.concatenate([goal_t[:, None].astype(np.float32), obs], axis=1), bf16=True)
         greedy = ua[:, 0] < thr
@@ -442,8 +444,8 @@ def test_fused_hdqn_rollout_full_size(coracle, nets):
         qe_abs += np.where(d, np.abs(q2).max(1), 0.0)
         np.testing.assert_array_equal(sub["reward"][t], (g2 == _status(obs64)).astype(np.float32))
         brk = d | (g2 == _status(s2_64))
-        gf = ub[:, 0] < thr
-        exp_next = np.where(brk, np.where(gf, np.where(d, reset_goal, q2.argmax(1)), _pick(ub[:, 1], NUM_GOALS)), g2)
+        gf = ubx < thr
+        exp_next = np.where(brk, np.where(gf, np.where(d, reset_goal, q2.argmax(1)), _pick(uby, NUM_GOALS)), g2)
         nxt = sub["goal"][t + 1] if t + 1 < T else env.hdqn_goal[idx].cpu().numpy()
         cc_g.check(nxt, exp_next, brk & gf & ~d, q2, f"fresh goal, step {t}")
         obs = sub["obs"][t]
