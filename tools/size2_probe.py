@@ -31,10 +31,7 @@ def run(mode, E, torch, launches=240):
             env.step_random(seed, step_idx=k)
             env.reset(phase == j)
             k += 1
-    while k < 1024:  # bench.py's burn_in: fused rollouts, then single launches
-        env.rollout_random(16, seed, first_step=k, final_observation=False, won_mask=False)
-        k += 16
-    for _ in range(1072):
+    for _ in range(1072):  # bench.py's burn-in for this leg: 1,072 single launches (--burn-in 0)
         env.step_random(seed, step_idx=k)
         k += 1
     timer = KernelTimer(launches)
