@@ -65,6 +65,11 @@ def parse():
     ap.add_argument("--burn-in", type=int, default=0,
                     help="untimed steps as 16-step fused rollouts before the burn-in launches (faster "
                          "to run, but the window after them starts in the rollout kernel's regime)")
+    ap.add_argument("--stagger", type=int, default=0,
+                    help="before the burn-in, S one-step launches each followed by a reset of the envs with "
+                         "index % S == j: first-episode phases spread over S steps instead of all envs "
+                         "starting together (tools/size2_probe.py: the finishing rate, and with it the "
+                         "per-launch time past the Infinity Cache, otherwise oscillates for thousands of steps)")
     ap.add_argument("--burn-in-launches", type=int, default=1072,
                     help="untimed one-step launches before the warm-up: the steady state (episodes "
                          "need >= 106 steps, the mean is ~210) reached by the timed kernel itself")
@@ -174,6 +179,18 @@ def load_valu():
     return out
 
 
+def stagger(env, S: int, seed: int, first_step: int, torch) -> int:
+    """S untimed one-step launches, after launch j a reset of the envs with index % S == j; returns
+    the next step index (see --stagger)."""
+    if S <= 0:
+        return first_step
+    phase = torch.arange(env.num_envs, device=env.device) % S
+    for j in range(S):
+        env.step_random(seed, step_idx=first_step + j)
+        env.reset(phase == j)
+    return first_step + S
+
+
 def burn_in(env, steps: int, seed: int, first_step: int) -> int:
     """Untimed fused rollouts until `steps` env-steps have passed; returns the next step index."""
     k = first_step
@@ -210,7 +227,7 @@ def size2_leg(args, torch, env=None):
     prealloc = env is not None
     if env is None:
         env = size2_env(args, torch)
-    k = burn_in(env, args.burn_in, args.seed, 0)
+    k = burn_in(env, args.burn_in, args.seed, stagger(env, args.stagger, args.seed, 0, torch))
     for _ in range(max(5, args.burn_in_launches)):
         env.step_random(args.seed, step_idx=k)
         k += 1
@@ -667,7 +684,7 @@ def main():
     step = lambda k: env.step_random(args.seed, opponent_random=True, step_idx=k)  # noqa: E731
 
     # steady state first: every env past its first episodes, some finishing at every step
-    k0 = burn_in(env, args.burn_in, args.seed, 0)
+    k0 = burn_in(env, args.burn_in, args.seed, stagger(env, args.stagger, args.seed, 0, torch))
     for k in range(k0, k0 + args.burn_in_launches):
         step(k)
     k0 += args.burn_in_launches
