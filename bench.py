@@ -65,7 +65,7 @@ def parse():
     ap.add_argument("--burn-in", type=int, default=0,
                     help="untimed steps as 16-step fused rollouts before the burn-in launches (faster "
                          "to run, but the window after them starts in the rollout kernel's regime)")
-    ap.add_argument("--stagger", type=int, default=0,
+    ap.add_argument("--stagger", type=int, default=256,
                     help="before the burn-in, S one-step launches each followed by a reset of the envs with "
                          "index % S == j: first-episode phases spread over S steps instead of all envs "
                          "starting together (tools/size2_probe.py: the finishing rate, and with it the "
@@ -233,23 +233,17 @@ def size2_leg(args, torch, env=None):
         k += 1
     env.clear_statistics()
     # One event pair per window of 20 launches, averaged over all of them, with the host's enqueue
-    # time of each window beside it. Placed after the Q-net / h-DQN legs, the first timed window
-    # once measured 453 us per launch and the next four 107-114 (r03e): a one-time stall of ~7 ms
-    # at the first window, not a slow placement (the same arena is 107 us from the second window
-    # on, and eight arenas allocated side by side all time 101-112 us, tools/placement_probe.py).
-    # Hence, as in the main timed loop: the collector off and one rehearsal window first.
+    # time of each window beside it. Rounds 2-3 saw the first window slow (one ~7 ms stall in r03e;
+    # 109 vs 98-103 us per launch in the r03 driver run) and timed a rehearsal window first. The
+    # rocprofv3 trace of r04a shows no gap between dispatches and no single long one: per-launch
+    # times rise and fall smoothly with the number of envs finishing in the launch (~1 us per 1,000
+    # finishes past the Infinity Cache, tools/size2_probe.py), which oscillates for thousands of
+    # steps when every env starts its first episode together. --stagger spreads those starts, and
+    # the rehearsal is gone.
     win = 20
     nwin = max(1, args.size2_steps // win)
     gc.disable()
-    torch.cuda.synchronize()
-    r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    r0.record()
-    for j in range(win):
-        env.step_random(args.seed, step_idx=k + j)
-    r1.record()
-    torch.cuda.synchronize()
-    rehearsal_us = round(r0.elapsed_time(r1) / win * 1e3, 1)
-    k += win
+    rehearsal_us = None
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(nwin + 1)]
     host = []
     torch.cuda.synchronize()
