@@ -234,20 +234,22 @@ def size2_leg(args, torch, env=None):
     env.clear_statistics()
     # One event pair per window of 20 launches, averaged over all of them, with the host's enqueue
     # time of each window beside it. Rounds 2-3 saw the first window slow (one ~7 ms stall in r03e;
-    # 109 vs 98-103 us per launch in the r03 driver run) and timed a rehearsal window first. The
-    # rocprofv3 trace of r04a shows no gap between dispatches and no single long one: per-launch
-    # times rise and fall smoothly with the number of envs finishing in the launch (~1 us per 1,000
-    # finishes past the Infinity Cache, tools/size2_probe.py), which oscillates for thousands of
-    # steps when every env starts its first episode together. --stagger spreads those starts, and
-    # the rehearsal is gone.
+    # 109 vs 98-103 us per launch in the r03 driver run) and timed a rehearsal window first. Three
+    # causes, measured in round 4 ("The 2^22 first window"): (1) per-launch
+    # times follow the number of envs finishing in the launch (~1 us per 1,000 finishes past the
+    # Infinity Cache, tools/size2_probe.py), which oscillates for thousands of steps when every env
+    # starts its first episode together -- --stagger spreads those starts; (2) a synchronize before
+    # the first window leaves the GPU idle while the host resumes (386 us before the first timed
+    # dispatch in the r04f trace, and 1.4 ms of host enqueue time in that window); (3) after such a
+    # gap the launches ramp from 95 to ~110 us over ~20 launches. So the windows follow the burn-in
+    # launches in the same queue without a synchronize: the events bracket queued kernel work only.
     win = 20
     nwin = max(1, args.size2_steps // win)
     gc.disable()
     rehearsal_us = None
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(nwin + 1)]
     host = []
-    torch.cuda.synchronize()
-    evs[0].record()
+    evs[0].record()  # behind the burn-in launches still in the queue: no idle gap before the window
     for w in range(nwin):
         h0 = time.perf_counter()
         for j in range(win):
