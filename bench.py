@@ -228,21 +228,21 @@ def size2_leg(args, torch, env=None):
     if env is None:
         env = size2_env(args, torch)
     k = burn_in(env, args.burn_in, args.seed, stagger(env, args.stagger, args.seed, 0, torch))
+    env.clear_statistics()  # ahead of the burn-in launches (see the main leg)
     for _ in range(max(5, args.burn_in_launches)):
         env.step_random(args.seed, step_idx=k)
         k += 1
-    env.clear_statistics()
     # One event pair per window of 20 launches, averaged over all of them, with the host's enqueue
     # time of each window beside it. Rounds 2-3 saw the first window slow (one ~7 ms stall in r03e;
-    # 109 vs 98-103 us per launch in the r03 driver run) and timed a rehearsal window first. Three
+    # 109 vs 98-103 us per launch in the r03 driver run) and timed a rehearsal window first. The
     # causes, measured in round 4 ("The 2^22 first window"): (1) per-launch
     # times follow the number of envs finishing in the launch (~1 us per 1,000 finishes past the
     # Infinity Cache, tools/size2_probe.py), which oscillates for thousands of steps when every env
-    # starts its first episode together -- --stagger spreads those starts; (2) a synchronize before
-    # the first window leaves the GPU idle while the host resumes (386 us before the first timed
-    # dispatch in the r04f trace, and 1.4 ms of host enqueue time in that window); (3) after such a
-    # gap the launches ramp from 95 to ~110 us over ~20 launches. So the windows follow the burn-in
-    # launches in the same queue without a synchronize: the events bracket queued kernel work only.
+    # starts its first episode together -- --stagger spreads those starts; (2) the statistics clear
+    # (any form of it) is followed by ~200 launches of up to +6 % (tools/size2_probe2.py) -- it now
+    # runs before the burn-in launches; (3) a synchronize before the first window leaves the GPU idle
+    # while the host resumes (386 us in the r04f trace) -- the windows follow the burn-in launches in
+    # the same queue, so the events bracket queued kernel work only.
     win = 20
     nwin = max(1, args.size2_steps // win)
     gc.disable()
@@ -272,7 +272,7 @@ def size2_leg(args, torch, env=None):
             "rehearsal_window_us": rehearsal_us, "arena_addr": hex(arena),
             "value": E / (kernel_ms * 1e-3), "unit": "env-steps/s", "achieved": achieved, "peak": HBM_PEAK_GBPS,
             "unit_bw": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "frac_8d": frac_8d, "traffic": load_pmc(E),
-            "episodes_completed": completed}
+            "episodes_completed": completed, "episodes_counted_since": "the clear before the burn-in launches"}
 
 
 def rollout_leg(env, args, world, dist, torch):
@@ -345,11 +345,13 @@ def qnet_leg(env, args, world, dist, torch, opponent):
                                         device=env.device)
     T, L, E = args.rollout_steps, args.qnet_launches, env.num_envs
     k = 20_000_000
+    # the leg's own episodes (main.py's logged quantities, q_eval included): cleared ahead of the
+    # warm-up launches, since a clear just before the window slows the launches after it (main leg)
+    env.clear_statistics()
     for _ in range(max(1, args.leg_warmup)):
         env.rollout_qnet(T, qnet, args.seed, opponent=opponent, first_step=k, final_observation=False,
                          won_mask=False)
         k += T
-    env.clear_statistics()  # the leg's own episodes: main.py's logged quantities, q_eval included
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     if world > 1:
@@ -380,7 +382,7 @@ def qnet_leg(env, args, world, dist, torch, opponent):
     h = torch.relu(x @ w["fc1.weight"].T + w["fc1.bias"])
     h = torch.relu(h @ w["fc2.weight"].T + w["fc2.bias"])
     greedy_cpu = (h @ w["out.weight"].T + w["out.bias"]).argmax(1)
-    summ = env.episode_summary()  # untimed: mg_stats_reduce over the records of the timed launches
+    summ = env.episode_summary()  # untimed: mg_stats_reduce over the warm-up and timed launches' records
     return {"episodes": {k: summ[k] for k in ("completed", "mean_q_eval", "mean_ep_reward_main", "win_rate_main",
                                                "collision_rate")},
             "q_eval_logged_as": "eval_net(state)[action] on each episode's last input and action (main.py:221)","kernel": f"qnet_rollout_ws_kernel<{ {'none': '0, false', 'uniform': '1, false', 'self': '2, true', 'other': '3, true'}[label] }>",
@@ -427,10 +429,10 @@ def hdqn_leg(env, args, world, dist, torch):
     meta, lower = net(10, NUM_GOALS), net(11, 5)
     T, L, E = args.rollout_steps, args.qnet_launches, env.num_envs
     k = 40_000_000
+    env.clear_statistics()  # the leg's own episodes (hdqn.py's logged quantities), ahead of the warm-up
     for _ in range(max(1, args.leg_warmup)):
         env.rollout_hdqn(T, meta, lower, args.seed, first_step=k, final_observation=False)
         k += T
-    env.clear_statistics()  # the leg's own episodes: hdqn.py's logged quantities, q_eval included
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     if world > 1:
@@ -447,7 +449,7 @@ def hdqn_leg(env, args, world, dist, torch):
     elapsed = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / L
     per_s = E * T / (kernel_ms * 1e-3)
-    summ = env.episode_summary()  # untimed: the timed launches' episodes (mg_stats_reduce)
+    summ = env.episode_summary()  # untimed: the warm-up and timed launches' episodes (mg_stats_reduce)
     episodes = {k: summ[k] for k in ("completed", "mean_q_eval", "mean_return_ego", "win_rate_hdqn", "collision_rate")}
     # untimed: one launch with Goal_DQN's columns, for the inner-loop break rate (:322)
     tr = env.rollout_hdqn(T, meta, lower, args.seed, first_step=k, final_observation=False, goal_memory=True)
@@ -681,6 +683,12 @@ def main():
 
     # steady state first: every env past its first episodes, some finishing at every step
     k0 = burn_in(env, args.burn_in, args.seed, stagger(env, args.stagger, args.seed, 0, torch))
+    # the statistics are cleared here, ahead of the burn-in launches, not just before the window: any
+    # clear is followed by ~200 launches of up to +6 % per launch (a transient after the different
+    # kernel, not the record writes: tools/size2_probe2.py, DESIGN.md section 4 "The 2^22 first
+    # window"), so the episodes reported below are those completed since this point
+    env.clear_statistics()
+    launches_since_clear = args.burn_in_launches + args.warmup + args.steps
     for k in range(k0, k0 + args.burn_in_launches):
         step(k)
     k0 += args.burn_in_launches
@@ -703,7 +711,6 @@ def main():
     wev0.elapsed_time(wev1)
     k0 += args.warmup
     graph = capture_steps(step, k0, args.steps, torch) if args.graph else None
-    env.clear_statistics()
     torch.cuda.synchronize()
 
     # Timed region: K launches back to back (one graph replay, or K host launches), bracketed by
@@ -730,7 +737,7 @@ def main():
     gc.enable()
     kernel_ms = ev0.elapsed_time(ev1) / args.steps
     k0 += args.steps
-    completed_in_window = int(env.counts[:, 0].sum())
+    completed_since_clear = int(env.counts[:, 0].sum())
     del graph
 
     # untimed: per-dispatch durations (events written by the dispatch packets themselves,
@@ -755,7 +762,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kernel_ms_max = float(t[0]), float(t[1])
 
-    # episode statistics (every episode completed since the window opened), the quantities the
+    # episode statistics (every episode completed since the clear before the burn-in launches), the quantities the
     # reference's scripts log: each rank reduces its shard on the device to 80 bytes of totals,
     # which one RCCL all-gather (xGMI) brings to every rank, outside the timed loop. The device
     # reduction and the collective are timed apart; at world size 1 there is no collective.
@@ -776,13 +783,15 @@ def main():
     else:
         episodes = gather_episode_summary(env.returns, env.counts, timings=timings)
         payload = PARTIAL_BYTES if world > 1 else 0
+    episodes["mean_q_eval"] = None  # random actions: no Q-net evaluates them (main.py:221 logs a DQN's value)
     episodes.update(allgather_ms=timings.get("allgather_ms"), reduce_ms=timings.get("reduce_ms"),
                     reduce_wall_ms=timings.get("reduce_wall_ms"),
                     reduce_how=("mg_stats_reduce, fixed order (64 B of records per env): reduce_ms = HIP events "
                                 "around its two launches, reduce_wall_ms = the Python call on the host clock"),
                     allgather_bytes_per_rank=payload,
-                    completed_in_timed_window_rank0=completed_in_window,
-                    counted_since="start of the timed window (statistics cleared after the warm-up)",
+                    completed_rank0=completed_since_clear,
+                    counted_since=(f"the statistics clear before the burn-in launches: {launches_since_clear} launches "
+                                   "(burn-in, warm-up, timed window)"),
                     logged_as=("mean_return_ego / win_rate_hdqn: hdqn.py:312, :342 (terminal observation); "
                                "mean_ep_reward_main / win_rate_main: main.py:209-211, :225 (winner-filtered "
                                "reward, pre-terminal observation); ego_first_rate: winner == 1"))

@@ -640,16 +640,32 @@ MG_HD void note_first_arrival(const mg_stats& St, int64_t i, const StepOut& r,
   }
 }
 
-// The Q value the scripts log for a finished episode (q_eval_value, main.py:221, hdqn.py:330),
-// added to the env's record (mg_episode_stats.q_eval) by the env's only writer of that field.
-MG_HD void stats_add_q_eval(const mg_stats& St, int64_t i, double q) {
-  double* f = &St.rec[i].q_eval;
-  *f = *f + q;
+// gym.vector autoreset after the episode was recorded: keep its terminal observation, reset the
+// env (merging_env.py:208-230) and put the reset observation in r.o (r0: the launch's precomputed
+// one, reset0).
+MG_HD void autoreset_env(const mg_params& P, Env& e, StepOut& r, float* final_obs_row, const Reset0* r0) {
+  if (final_obs_row) {
+#pragma unroll
+    for (int k = 0; k < kObs; ++k) final_obs_row[k] = static_cast<float>(r.o[k]);
+  }
+  e.p1 = e.p2 = P.start_point;
+  e.v1 = e.v2 = P.start_vel;
+  e.ret1 = e.ret2 = 0.0;
+  e.steps = 0;
+  e.winner = 0;
+  e.done = false;
+  if (r0) {
+#pragma unroll
+    for (int k = 0; k < kObs; ++k) r.o[k] = r0->o[k];
+    r.dx1 = r0->dx1;
+  } else {
+    reset_obs(P, r.o, &r.dx1);
+  }
 }
 
-// gym.vector autoreset: record the finished episode, keep its terminal observation, reset
-// the env (merging_env.py:208-230) and put the reset observation in r.o. sreg: statistics held
-// in registers (nullptr: read-modify-write them in memory). The episode's statistics:
+// Record the finished episode, then autoreset (autoreset_env). sreg: statistics held in registers
+// (the random rollout), nullptr: read-modify-write them in memory (the one-step kernels and the host
+// path; the Q-net kernels use finish_episode_nowait below). The episode's statistics:
 // r{1,2}_accumulate (hdqn.py's ep_reward), main.py's winner-filtered ep_reward (r1_accumulate
 // before the ego-first step while winner == 1), main.py:225's win test on the state the last step
 // acted on (r.win_pre) and hdqn.py:342's on the terminal state.
@@ -687,23 +703,7 @@ MG_HD void finish_episode(const mg_params& P, Env& e, StepOut& r,
     cp[0] = c;
     reinterpret_cast<uint2*>(cp + 1)[0] = d;
   }
-  if (final_obs_row) {
-#pragma unroll
-    for (int k = 0; k < kObs; ++k) final_obs_row[k] = static_cast<float>(r.o[k]);
-  }
-  e.p1 = e.p2 = P.start_point;
-  e.v1 = e.v2 = P.start_vel;
-  e.ret1 = e.ret2 = 0.0;
-  e.steps = 0;
-  e.winner = 0;
-  e.done = false;
-  if (r0) {  // the launch's precomputed reset observation (reset0)
-#pragma unroll
-    for (int k = 0; k < kObs; ++k) r.o[k] = r0->o[k];
-    r.dx1 = r0->dx1;
-  } else {
-    reset_obs(P, r.o, &r.dx1);
-  }
+  autoreset_env(P, e, r, final_obs_row, r0);
 }
 
 // After a step with statistics: the first-arrival bookkeeping, then autoreset where done.
@@ -713,6 +713,58 @@ MG_HD void after_step(const mg_params& P, Env& e, StepOut& r, const mg_stats& St
   const bool finish = autoreset && r.done;
   if (r.first1 && !finish) note_first_arrival(St, i, r, sreg);
   if (finish) finish_episode(P, e, r, St, final_obs_row, i, sreg, r0);
+}
+
+// Episode statistics without a load on the step path (round 4), for the batched device kernels: a
+// finishing env's record update is a handful of no-return atomics, so the lane never waits for its
+// record (finish_episode's read-modify-write stalls the wave on a global load). The env's lane is
+// the only writer of its record during a launch and atomics from one lane to one address are
+// performed in issue order, so the sums are the sequential ones, bit for bit. The one value read
+// back at an episode end is main.py's pending r1_accumulate (ret1_pending), and only when the ego
+// arrived first on an earlier step: it is held in a register `pend`, loaded at the launch start
+// for the lanes whose episode is in that state (pend_load: winner == 1, a small fraction) and set
+// on the first arrival (also stored to the record then, a store without a wait).
+__device__ __forceinline__ double pend_load(const mg_stats& St, int64_t i, const Env& e) {
+  return St.rec && e.winner == 1 ? St.rec[i].ret1_pending : 0.0;
+}
+
+__device__ __forceinline__ void finish_episode_nowait(const mg_params& P, Env& e, StepOut& r, const mg_stats& St,
+                                                      float* final_obs_row, int64_t i, double pend,
+                                                      const Reset0* r0) {
+  if (St.rec) {
+    mg_episode_stats* rec = St.rec + i;
+    const bool ego_won = e.winner == 1;
+    const bool win_hdqn = (P.end_point - e.p2) > (P.end_point - e.p1);
+    unsafeAtomicAdd(&rec->ret[0], e.ret1);
+    unsafeAtomicAdd(&rec->ret[1], e.ret2);
+    unsafeAtomicAdd(&rec->ret_main, ego_won ? (r.first1 ? r.ret_pre : pend) : e.ret1);
+    atomicAdd(&rec->episodes, 1u);
+    atomicAdd(&rec->steps, e.steps);
+    if (r.coll) atomicAdd(&rec->collisions, 1u);
+    if (ego_won) atomicAdd(&rec->ego_first, 1u);
+    if (r.win_pre) atomicAdd(&rec->win_main, 1u);
+    if (win_hdqn) atomicAdd(&rec->win_hdqn, 1u);
+  }
+  autoreset_env(P, e, r, final_obs_row, r0);
+}
+
+// after_step with the no-wait statistics; returns whether the episode finished (autoreset)
+__device__ __forceinline__ bool after_step_nowait(const mg_params& P, Env& e, StepOut& r, const mg_stats& St,
+                                                  float* final_obs_row, int64_t i, bool autoreset, double& pend,
+                                                  const Reset0* r0) {
+  const bool finish = autoreset && r.done;
+  if (finish) {
+    finish_episode_nowait(P, e, r, St, final_obs_row, i, pend, r0);
+  } else if (r.first1) {
+    pend = r.ret_pre;
+    if (St.rec) St.rec[i].ret1_pending = r.ret_pre;  // note_first_arrival
+  }
+  return finish;
+}
+
+// The Q value a finished episode adds to its record (mg_episode_stats.q_eval), without a wait
+__device__ __forceinline__ void add_q_eval_nowait(const mg_stats& St, int64_t i, double q) {
+  if (St.rec) unsafeAtomicAdd(&St.rec[i].q_eval, q);
 }
 
 // Wave-scope ordering of LDS accesses between the lanes of ONE wave (no s_barrier): the LDS
@@ -903,6 +955,8 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const Launch L) {
         if (L.O.coll) st_out(L.O.coll + i, static_cast<uint8_t>(r.coll ? 1 : 0));
       }
       won = e.winner == 1;
+      // statistics by read-modify-write: the no-wait atomics (finish_episode_nowait) measured
+      // +4 % per launch here at 2^20 (r04j), where the finishing lanes' loads hit the Infinity Cache
       after_step(P, e, r, L.St, L.O.final_obs ? L.O.final_obs + i * kObs : nullptr, i,
                  (L.flags & MG_AUTORESET) != 0, nullptr, &L.R0);
       store_env(L.S, opaque_index(i), e);
@@ -988,7 +1042,9 @@ __global__ __launch_bounds__(kBlock) void rollout_kernel(const Rollout R) {
   const bool autoreset = (R.flags & MG_AUTORESET) != 0;
 
   Env e;
-  EpStats sreg;  // A/B: -9.5 % per step in steady state (finishing lanes no longer wait on a load)
+  // statistics in registers for the launch: -9.5 % per step against the read-modify-write (the
+  // finishing lanes no longer wait on a load); the no-wait atomics measured +16 % median (r04j)
+  EpStats sreg;
   if (live) {
     e = load_env(R.S, i);
     stats_load(R.St, i, sreg);
@@ -1757,7 +1813,8 @@ template <int OPP, int N, bool CHECKED>
 __device__ __forceinline__ void qnet_policy_step_n(const QRollout& R, Env (&e)[N], StepOut (&r)[N],
                                                    int64_t i0, const bool (&live)[N], int t,
                                                    const int (&greedy1)[N], const int (&greedy2)[N],
-                                                   bool (&won)[N], const float* qrow, uint2 (&keep)[N]) {
+                                                   bool (&won)[N], const float* qrow, uint2 (&keep)[N],
+                                                   double (&pend)[N]) {
   const uint64_t step = R.first_step + t;
   int a1[N], a2[N];
 #pragma unroll
@@ -1808,10 +1865,11 @@ __device__ __forceinline__ void qnet_policy_step_n(const QRollout& R, Env (&e)[N
              f32x2{static_cast<float>(r[j].r1), static_cast<float>(r[j].r2)});
     store_step_bytes(R.T, row, a1[j], a2[j], r[j].done, r[j].coll);
     won[j] = e[j].winner == 1;
-    const bool finish = (R.flags & MG_AUTORESET) && r[j].done;
-    after_step(R.P, e[j], r[j], R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i,
-               (R.flags & MG_AUTORESET) != 0, nullptr, &R.R0);
-    if (finish && R.St.rec) stats_add_q_eval(R.St, i, qrow[64 * j * kObs + a1[j]]);  // a1 in 0..4 here
+    // the Q value the scripts log for a finished episode (q_eval_value, main.py:221); a1 in 0..4
+    // here (a bad action leaves done false)
+    if (after_step_nowait(R.P, e[j], r[j], R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i,
+                          (R.flags & MG_AUTORESET) != 0, pend[j], &R.R0))
+      add_q_eval_nowait(R.St, i, qrow[64 * j * kObs + a1[j]]);
   }
 }
 
@@ -1931,11 +1989,14 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
   StepOut r[kIlp];
   bool live0[kIlp], live1[kIlp];
   uint2 keep0[kIlp], keep1[kIlp];  // OPP 0 / 1: the odd step's two draw words (qnet_policy_step_n)
+  double pend0[kIlp], pend1[kIlp];  // main.py's pending values (pend_load, after_step_nowait)
 #pragma unroll
   for (int j = 0; j < kIlp; ++j) {
     const int la = lbase + 64 * j + lane, lb = kHalf + la;
     live0[j] = qnet_load_env(R, base + la, e0[j], tile + la * kObs);
     live1[j] = qnet_load_env(R, base + lb, e1[j], tile + lb * kObs);
+    pend0[j] = live0[j] ? pend_load(R.St, base + la, e0[j]) : 0.0;
+    pend1[j] = live1[j] ? pend_load(R.St, base + lb, e1[j]) : 0.0;
 #pragma unroll
     for (int k = 0; k < kObs; ++k) r[j].o[k] = 0.0;
   }
@@ -1955,10 +2016,10 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
       const float* qrow = tile + (local0 + lane) * kObs;
       if (g == 0)
         qnet_policy_step_n<OPP, kIlp, CHECKED>(R, e0, r, base + local0 + lane, live0, t, greedy1, greedy2, won, qrow,
-                                               keep0);
+                                               keep0, pend0);
       else
         qnet_policy_step_n<OPP, kIlp, CHECKED>(R, e1, r, base + local0 + lane, live1, t, greedy1, greedy2, won, qrow,
-                                               keep1);
+                                               keep1, pend1);
       const int64_t wbase = base + local0;
 #pragma unroll
       for (int j = 0; j < kIlp; ++j) {
@@ -2179,7 +2240,7 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
         b_g2[j] = static_cast<uint8_t>(goal2);  // for the fused ring row of step t - 1
         // the episode's q_eval (hdqn.py:330): the env wave recorded the episode in E(X, t - 1); this
         // lane is the only writer of the field, so no-return atomics keep the adds in step order
-        if (done && live && R.St.rec) unsafeAtomicAdd(&R.St.rec[i].q_eval, static_cast<double>(qe));
+        if (done && live) add_q_eval_nowait(R.St, i, static_cast<double>(qe));
       } else {
         goal_t = goal_prev >= 0 ? goal_prev : (df == kHGreedy ? gstar : df);
       }
@@ -2235,6 +2296,7 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
   const int ew = wave - 4;
   Env e[2];
   bool live[2];
+  double pend[2] = {0.0, 0.0};  // main.py's pending values (pend_load, after_step_nowait)
   int stc[2];  // goal_status of each group's current state, from its fp64 dx1 and v2
   // the fused ring row of each group's last step, completed once the Q-net waves have chosen
   // its next goal: s, s' (terminal where done), goal, action
@@ -2297,6 +2359,7 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
     double o[kObs];
     if (live[g]) {
       e[g] = load_env(R.S, i);
+      pend[g] = pend_load(R.St, i, e[g]);
       double x1, y1, x2, y2;
       lon2coord(R.P, e[g].p1, true, x1, y1);
       lon2coord(R.P, e[g].p2, false, x2, y2);
@@ -2361,7 +2424,7 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
         }
       }
       auto step = [&](Env& ev, bool lv, float (&s0)[kObs], float (&s1)[kObs], int& pg, int& pa, double& ac,
-                      int& st) __attribute__((always_inline)) {
+                      int& st, double& pd) __attribute__((always_inline)) {
         StepOut rv;  // per step: the state acted on is the env's tile row, so no observation is carried
         b_st_old[j] = static_cast<uint8_t>(st);  // status of the state acted on (:314)
         if (ring) {
@@ -2403,10 +2466,11 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
           for (int q2 = 0; q2 < kObs / 2; ++q2)
             sd[q2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(
                                                       f32x2{static_cast<float>(rv.o[2 * q2]), static_cast<float>(rv.o[2 * q2 + 1])}, bf16x2));
-          finish_episode(R.P, ev, rv, R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i, nullptr, &R.R0);
+          after_step_nowait(R.P, ev, rv, R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i, true, pd,
+                            &R.R0);
           st = goal_status(rv.dx1, ev.v2);  // the reset state the next step acts on
-        } else if (lv && rv.first1) {
-          note_first_arrival(R.St, i, rv);
+        } else if (lv) {
+          after_step_nowait(R.P, ev, rv, R.St, nullptr, i, false, pd, &R.R0);  // the first arrival, if any
         }
         const int64_t wrem = R.n - wbase;
         wave_store_obs(tile + (g * kHHalf + 64 * ew) * kObs, rv.o,
@@ -2414,9 +2478,9 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
                        wrem <= 0 ? 0 : (wrem < 64 ? static_cast<int>(wrem) : 64));
       };
       if (g == 0)
-        step(e[0], live[0], ps[0], ps2[0], pgoal[0], pact[0], acc[0], stc[0]);
+        step(e[0], live[0], ps[0], ps2[0], pgoal[0], pact[0], acc[0], stc[0], pend[0]);
       else
-        step(e[1], live[1], ps[1], ps2[1], pgoal[1], pact[1], acc[1], stc[1]);
+        step(e[1], live[1], ps[1], ps2[1], pgoal[1], pact[1], acc[1], stc[1], pend[1]);
     }
     __syncthreads();
   }

@@ -92,10 +92,11 @@ def _records_of(returns, counts):
 _SCRATCH = {}  # device -> mg_stats_reduce scratch (block partials)
 
 
-def device_totals(records):
+def device_totals(records, events=None):
     """[n, 8] f64 device records (mg_episode_stats) -> their totals as one [10] int64 device tensor,
     summed by mg_stats_reduce in its fixed order (bit-reproducible; include/merging_hip.h). Two
-    launches on the current stream, no synchronisation."""
+    launches on the current stream, no synchronisation. events: a pair of timing events recorded
+    right around the launches (the output and scratch are set up before the first)."""
     import ctypes
 
     import torch
@@ -109,19 +110,24 @@ def device_totals(records):
     scratch = _SCRATCH.get(dev)
     if scratch is None or scratch.numel() < words:  # one buffer per device, reused (stream-ordered)
         scratch = _SCRATCH[dev] = torch.empty(words, dtype=torch.int64, device=dev)
-    _native.check(_native.lib.mg_stats_reduce(
-        ctypes.c_void_p(records.data_ptr()), n, ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(scratch.data_ptr()),
-        scratch.numel() * 8, ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)), "mg_stats_reduce")
+    args = (ctypes.c_void_p(records.data_ptr()), n, ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(scratch.data_ptr()),
+            scratch.numel() * 8, ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+    if events:
+        events[0].record()
+    rc = _native.lib.mg_stats_reduce(*args)
+    if events:
+        events[1].record()
+    _native.check(rc, "mg_stats_reduce")
     return out
 
 
-def partial_stats(returns, counts, q_eval=None):
+def partial_stats(returns, counts, q_eval=None, events=None):
     """This shard's totals as one [10] int64 tensor on the stats' device: the three return sums
     (r1_accumulate, r2_accumulate, main.py's filtered ep_reward; f64, bit-preserved), the q_eval sum
     (the record's own for MergeVecEnv's views; else the q_eval [n] tensor given, or 0), then
     episodes, collisions, ego-first arrivals, steps, main.py wins, hdqn.py wins. On the GPU, for
     MergeVecEnv's record views, one mg_stats_reduce (fixed summation order, ~64 B of reads per env);
-    other tensors (gloo tests on CPU) are summed by torch."""
+    other tensors (gloo tests on CPU) are summed by torch. events: timing events for device_totals."""
     import torch
 
     if returns.shape[1] != NUM_RETURNS or counts.shape[1] != NUM_COUNTS:
@@ -129,14 +135,20 @@ def partial_stats(returns, counts, q_eval=None):
     if returns.is_cuda:
         rec = _records_of(returns, counts)
         if rec is not None:
-            return device_totals(rec)
+            return device_totals(rec, events)
     rec = _records_of(returns, counts)
     if q_eval is None and rec is not None:
         q_eval = rec[:, 7]
+    timed = events and returns.is_cuda
+    if timed:
+        events[0].record()
     r = returns.sum(0)
     q = q_eval.sum().reshape(1).to(r) if q_eval is not None else torch.zeros(1, dtype=r.dtype, device=r.device)
     c = counts.to(torch.int64).sum(0)
-    return torch.cat([torch.cat([r, q]).contiguous().view(torch.int64), c])
+    out = torch.cat([torch.cat([r, q]).contiguous().view(torch.int64), c])
+    if timed:
+        events[1].record()
+    return out
 
 
 def summarize_partials(parts):
@@ -164,8 +176,8 @@ def summarize_partials(parts):
 def gather_episode_summary(returns, counts, group=None, timings=None):
     """All-gather every rank's 80-byte partial totals and reduce them: the global summary on
     every rank (the default collective of a sharded run). timings (a dict, optional) receives
-    "reduce_ms" (this shard's reduction to its partial totals: HIP events around its launches on
-    the GPU), "reduce_wall_ms" (the same call on the host clock, synchronised: Python and launch
+    "reduce_ms" (this shard's reduction to its partial totals: HIP events right around its two
+    launches on the GPU), "reduce_wall_ms" (the same call on the host clock, synchronised: Python and launch
     overheads included) and "allgather_ms" (the collective alone; None without one, world size 1)."""
     import time
 
@@ -181,11 +193,7 @@ def gather_episode_summary(returns, counts, group=None, timings=None):
         events = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     sync()
     t0 = time.perf_counter()
-    if events:
-        events[0].record()
-    part = partial_stats(returns, counts)
-    if events:
-        events[1].record()
+    part = partial_stats(returns, counts, events=events)
     sync()
     t1 = time.perf_counter()
     world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1

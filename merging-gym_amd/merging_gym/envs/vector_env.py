@@ -122,6 +122,7 @@ class MergeVecEnv:
         # counts [N,6] i32 = episodes, collisions, ego-first arrivals, steps, main.py:225 wins,
         # hdqn.py:342 wins
         self._ep_stats = torch.zeros((n, 8), dtype=torch.float64, device=dev) if episode_stats else None
+        self._keep_pending = None  # clear_statistics' record mask
         self.returns = self._ep_stats[:, :3] if episode_stats else None
         self.ret_sum = self._ep_stats[:, :2] if episode_stats else None
         self.ret_main = self._ep_stats[:, 2] if episode_stats else None
@@ -520,9 +521,14 @@ class MergeVecEnv:
         """Zero the sums and counts (each env's pending main.py value stays: it belongs to the
         episode in progress)."""
         if self.ret_sum is not None:
-            self.returns.zero_()
-            self.counts.zero_()
-            self.q_eval.zero_()
+            # one pass over whole 64-byte records (an int64 multiply by 0 / 1 keeps ret1_pending's
+            # bits): zeroing the strided fields instead (three fills of partial lines) slowed the
+            # step launches that followed by up to 6 % until every env had finished an episode
+            # (2^22 envs, tools/size2_probe2.py, DESIGN.md section 4 "The 2^22 first window")
+            if self._keep_pending is None:
+                self._keep_pending = self._torch.tensor([0, 0, 0, 1, 0, 0, 0, 0], dtype=self._torch.int64,
+                                                        device=self._ep_stats.device)
+            self._ep_stats.view(self._torch.int64).mul_(self._keep_pending)
 
     # ------------------------------------------------------------------ checkpoint / resume
     _STATE_KEYS = ("p1", "v1", "p2", "v2", "ret1", "ret2", "tf")

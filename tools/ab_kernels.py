@@ -69,7 +69,8 @@ class Bed:
         self.params.angle0 = float(np.arctan2(1000, 30000))
         self.state = nat.State(*(x.data_ptr() for x in self.t))
         self.out = nat.Outputs(self.obs.data_ptr(), self.rew.data_ptr(), self.done.data_ptr(),
-                               self.coll.data_ptr(), None, self.fobs.data_ptr(), None, None)
+                               self.coll.data_ptr(), None,
+                               None if os.environ.get("MG_AB_NOFOBS") == "1" else self.fobs.data_ptr(), None, None)
         self.stats = (nat.Stats() if os.environ.get("MG_AB_NOSTATS") == "1"
                       else nat.Stats(self.ep_stats.data_ptr()))
         self.twon = torch.zeros((T, (n + 63) // 64), dtype=torch.int64, device=dev)

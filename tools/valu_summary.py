@@ -42,7 +42,7 @@ def main():
     ap.add_argument("--out")
     a = ap.parse_args()
     vals = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> [per-dispatch values]
-    for p in glob.glob(os.path.join(a.pmc_dir, "p*", "**", "*counter_collection.csv"), recursive=True):
+    for p in glob.glob(os.path.join(a.pmc_dir, "**", "*counter_collection.csv"), recursive=True):
         per = defaultdict(float)
         for r in csv.DictReader(open(p)):
             k = kernel_key(r["Kernel_Name"])
