@@ -456,6 +456,10 @@ def test_fused_hdqn_rollout_full_size(coracle, nets):
     np.testing.assert_array_equal(env.returns[idx].cpu().numpy(), stats[0])
     np.testing.assert_array_equal(env.counts[idx].cpu().numpy().astype(np.uint32), stats[1])
     check_q_eval(env.q_eval[idx].cpu().numpy(), qe, qe_abs, f"full-size h-DQN ({nets})")
+    # main.py's pending value where the ego has arrived first: what the next launch reads back
+    # (the no-wait statistics load it only for those envs, pend_load)
+    w1 = envs["winner"] == 1
+    np.testing.assert_array_equal(env._ep_stats[idx][:, 3].cpu().numpy()[w1], envs["ep_reward_main"][w1])
     cc_a.finish()
     cc_g.finish()
 

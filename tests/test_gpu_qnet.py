@@ -316,6 +316,10 @@ def test_rollout_qnet_full_size(torch, coracle, nets, opponent):
     np.testing.assert_array_equal(env.counts[idx].cpu().numpy().astype(np.uint32), stats[1])
     np.testing.assert_array_equal(env.returns[idx].cpu().numpy(), stats[0])
     assert stats[1][:, 0].sum() > counts0[:, 0].sum()  # episodes ended in the window
+    # main.py's pending value where the ego has arrived first: what the next launch reads back
+    # (the no-wait statistics load it only for those envs, pend_load)
+    w1 = envs["winner"] == 1
+    np.testing.assert_array_equal(env._ep_stats[idx][:, 3].cpu().numpy()[w1], envs["ep_reward_main"][w1])
     check_q_eval(env.q_eval[idx].cpu().numpy(), qe, qe_abs, f"full-size ego l1 ({opponent})")
     cc1.finish()
     if opponent in ("self", "other"):
