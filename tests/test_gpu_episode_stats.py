@@ -224,3 +224,36 @@ def test_stats_reduce_is_cheap_at_full_size():
     ms = e0.elapsed_time(e1) / 20
     print(f"mg_stats_reduce at 2^20: {ms * 1e3:.1f} us per call")
     assert ms < 0.1
+
+
+def test_clear_statistics_keeps_only_the_pending_value():
+    """MergeVecEnv.clear_statistics (one int64 pass over whole records since round 4): every sum,
+    count and q_eval becomes +0 and main.py's pending value (ret1_pending, the episode in progress)
+    keeps its bits, so the episodes that finish after the clear are recorded as without it."""
+    import torch
+
+    from merging_gym import MergeVecEnv
+
+    n = 4096
+    env = MergeVecEnv(n, device="cuda:0")
+    for k in range(400):
+        env.step_random(5, step_idx=k)
+    before = env._ep_stats.clone()
+    assert int(env.counts[:, 0].sum()) > 0 and bool((before[:, 3] != 0).any())
+    env.clear_statistics()
+    after = env._ep_stats
+    assert torch.equal(after[:, 3].view(torch.int64), before[:, 3].view(torch.int64))
+    cols = [0, 1, 2, 4, 5, 6, 7]
+    assert bool((after[:, cols].view(torch.int64) == 0).all())  # +0.0 and zero counts, bit for bit
+    # the episodes after the clear: the same records as a twin batch cleared by field
+    twin = MergeVecEnv(n, device="cuda:0")
+    for k in range(400):
+        twin.step_random(5, step_idx=k)
+    twin.returns.zero_()
+    twin.counts.zero_()
+    twin.q_eval.zero_()
+    for k in range(400, 700):
+        env.step_random(5, step_idx=k)
+        twin.step_random(5, step_idx=k)
+    assert torch.equal(env._ep_stats.view(torch.int64), twin._ep_stats.view(torch.int64))
+    assert int(env.counts[:, 0].sum()) > 0
