@@ -140,8 +140,9 @@ def cpu_baseline(seconds: float, envs: int):
                         "on done); oracle/merge_oracle.c, oracle/merge_numpy.py, oracle/merge_oracle.py"}
 
 
-def load_pmc(envs: int):
-    """HBM traffic per launch from the committed rocprofv3 PMC summary (profiles/), if any."""
+def load_pmc(envs: int, kernel: str = "step"):
+    """HBM traffic per launch from the committed rocprofv3 PMC summary (profiles/), if any: the
+    step kernel's, or with kernel="rollout" the 16-step random rollout's."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
@@ -149,6 +150,8 @@ def load_pmc(envs: int):
         row = d.get("by_envs", {}).get(str(envs))
         if row is None and int(d.get("envs", -1)) == envs:
             row = d
+        if row is not None and kernel != "step":
+            row = row.get(kernel)
         return None if row is None else row.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None
@@ -309,7 +312,11 @@ def rollout_leg(env, args, world, dist, torch):
             "value": world * E * T * L / float(t[0]), "unit": "env-steps/s",
             "ms_per_step": float(t[0]) / (L * T) * 1e3, "kernel_ms_mean": kernel_ms,
             "bytes_per_env_step": bytes_per_env_step, "achieved": achieved, "peak": HBM_PEAK_GBPS,
-            "unit_bw": "GB/s", "frac": achieved / HBM_PEAK_GBPS}
+            "unit_bw": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
+            "traffic": load_pmc(E, "rollout") if T == 16 else None,
+            "traffic_note": "HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, profiles/pmc_traffic.json); "
+                            "the algorithmic bytes leave out the statistics records (32 B read per env per "
+                            "launch)"}
 
 
 QNET_USEFUL_FLOP = 2 * (10 * 200 + 200 * 100 + 100 * 5)      # one Net forward, main.py:30-47

@@ -30,7 +30,7 @@ def load(d, counter):
                 continue
             name = r["Kernel_Name"]
             key = "reset" if "reset_kernel" in name else "observe" if "observe_kernel" in name else \
-                "step" if "step_kernel" in name else None
+                "step" if "step_kernel" in name else "rollout" if "rollout_kernel" in name else None
             if key:
                 per[key].append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
     return {k: [v for _, v in sorted(vals)] for k, vals in per.items()}
@@ -63,6 +63,13 @@ def main():
                   "ratio_to_algorithmic": total / (152.0 * n),
                   "check_observe_read_ratio": chk_r, "check_reset_write_ratio": chk_w,
                   "rule": "2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md, gfx950)"}
+        if "rollout" in f and "rollout" in w:  # T = 16: 52 B per env-step + 100 B of state per env
+            rf, rw = mean(f, "rollout"), mean(w, "rollout")
+            alg = (52.0 * 16 + 100.0) * n
+            res[n]["rollout"] = {"fetch_bytes": 2.0 * rf, "write_bytes": rw, "hbm_bytes_per_launch": 2.0 * rf + rw,
+                                 "algorithmic_bytes_per_launch": alg, "ratio_to_algorithmic": (2.0 * rf + rw) / alg,
+                                 "note": "the algorithmic bytes leave out the statistics records (32 B read per "
+                                         "env per launch, the finishing envs' 64 B written back)"}
     print(json.dumps(res, indent=1))
     if a.out:
         first = res[a.envs[0]]

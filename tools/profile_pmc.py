@@ -2,8 +2,8 @@
 
 Per env count it launches, in order: `reps` x reset_kernel (writes 50 B/env: 6 f64 + 1 u16 --
 the write calibration), `reps` x observe_kernel (reads 32 B/env of f64 -- the read
-calibration), `reps` x step_kernel<philox> (the bench kernel). tools/pmc_summary.py turns the
-counter CSVs into per-launch bytes.
+calibration), `reps` x step_kernel<philox> (the bench kernel), `reps` x rollout_kernel (T = 16,
+the bench's rollout leg). tools/pmc_summary.py turns the counter CSVs into per-launch bytes.
 """
 import argparse
 import ctypes
@@ -38,6 +38,8 @@ for n in args.envs:
         env.step_random(1, step_idx=k)
     for k in range(args.reps):
         env.step_random(2, step_idx=k)
+    for k in range(args.reps):  # the random rollout, T = 16 (its trajectory buffers allocated once)
+        env.rollout_random(16, 2, first_step=1000 + 16 * k, final_observation=False, won_mask=False)
     torch.cuda.synchronize()
     print(f"envs={n} done", flush=True)
     del env
