@@ -169,6 +169,8 @@ def load_valu():
         return {}
     out = {}
     for k, v in d.items():
+        if not isinstance(v, dict) or "insts_per_64_env_steps" not in v:
+            continue  # the file's notes and comparisons ("source", "round4_valu_before_after")
         ins = v.get("insts_per_64_env_steps", {})
         out[k] = {"valu_busy_frac": v.get("VALUBusy", 0.0) / 100.0,
                   "valu_insts_per_lane_step": ins.get("valu", 0.0),  # wave instructions per 64 env-steps
