@@ -394,7 +394,9 @@ def qnet_leg(env, args, world, dist, torch, opponent):
     summ = env.episode_summary()  # untimed: mg_stats_reduce over the warm-up and timed launches' records
     return {"episodes": {k: summ[k] for k in ("completed", "mean_q_eval", "mean_ep_reward_main", "win_rate_main",
                                                "collision_rate")},
-            "q_eval_logged_as": "eval_net(state)[action] on each episode's last input and action (main.py:221)","kernel": f"qnet_rollout_ws_kernel<{ {'none': '0, false', 'uniform': '1, false', 'self': '2, true', 'other': '3, true'}[label] }>",
+            "q_eval_logged_as": "eval_net(state)[action] on each episode's last input and action (main.py:221)",
+            "kernel": "qnet_rollout_ws_kernel<%s>" % {"none": "0, false", "uniform": "1, false", "self": "2, true",
+                                                      "other": "3, true"}[label],
             "opponent": label if label != "other" else "other net (main.py Strategy_OP L1; checkpoint l3)",
             "steps_per_launch": T, "launches": L, "dtype": "bf16 (fp32 accumulate)",
             "value": world * E * T * L / elapsed, "unit": "env-steps/s",
