@@ -84,9 +84,15 @@ MG_HD double div_const(double x, double d, double inv) {
 // 99.98 % of 2e7 samples vs glibc). Larger |theta| takes the device library's sincos.
 // The device library's sincos for |t| >= 1/16 (only reached off the live-episode range, e.g.
 // stepping far past done). Kept out of line: inlined, the compiler hoists its polynomial
-// constants into VGPRs for the whole step loop of the T-step kernels, which then spill.
-__device__ __attribute__((noinline, unused)) void sincos_cold(double t, double* s, double* c) {
-  sincos(t, s, c);
+// constants into VGPRs for the whole step loop of the T-step kernels, which then spill. Its
+// results come back by value (round 4): through pointers they were private-memory loads in the
+// caller, and the wait for those at the join after the branch -- one in-order counter for vector
+// loads and stores on gfx950 -- also waited for every store the wave had in flight, on the common
+// path too. Config 5 -1.5 to -3 % per step, the rollout and h-DQN within noise (profiles/r04/ab/r04z_*).
+__device__ __attribute__((noinline, unused)) double2 sincos_cold(double t) {
+  double s, c;
+  sincos(t, &s, &c);
+  return make_double2(s, c);
 }
 
 // the polynomial branch (|t| < 1/16)
@@ -110,7 +116,9 @@ MG_HD void arc_sincos(double t, double& s, double& c) {
     return;
   }
 #if defined(__HIP_DEVICE_COMPILE__)
-  sincos_cold(t, &s, &c);
+  const double2 sc = sincos_cold(t);
+  s = sc.x;
+  c = sc.y;
 #else
   s = std::sin(t);
   c = std::cos(t);
