@@ -1,13 +1,11 @@
-# In-process A/B of tools/variants/lib_*.so: step + rollout (interleaved record), config-5 Q-net, h-DQN.
-# Usage: TAG=r04x LIBS="tools/variants/lib_a.so tools/variants/lib_b.so" bash tools/gpu_r04ab.sh
+# r04ab: the rollout with the by-value cold sincos (lib_sc = the working tree) against the build
+# before it, longer, both orders.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-TAG=${TAG:-r04ab}
-O=gpurun_out/$TAG
+O=gpurun_out/r04ab
 mkdir -p $O
-LIBS=${LIBS:-tools/variants/lib_*.so}
-echo "== ab step/rollout" && MG_AB_FLAGS=1 timeout -k 10 300 python tools/ab_kernels.py $LIBS --rounds 6 --warm 1200 > $O/ab_rollout.log 2>&1 && tail -4 $O/ab_rollout.log \
-&& echo "== ab qnet" && timeout -k 10 300 python tools/ab_kernels.py $LIBS --qnet --rounds 5 --warm 1200 > $O/ab_qnet.log 2>&1 && tail -8 $O/ab_qnet.log \
-&& echo "== ab hdqn" && timeout -k 10 400 python tools/ab_hdqn.py $LIBS --rounds 4 > $O/ab_hdqn.log 2>&1 && tail -8 $O/ab_hdqn.log \
-&& echo "== ab ok"
+echo "== ab rollout" && MG_AB_FLAGS=1 timeout -k 10 500 python tools/ab_kernels.py tools/variants/lib_rp_base.so tools/variants/lib_sc.so tools/variants/lib_sc_split.so --rounds 12 --warm 1200 --rollouts 8 > $O/ab_rollout.log 2>&1 && tail -4 $O/ab_rollout.log | head -3 \
+&& echo "== ab rollout rev" && MG_AB_FLAGS=1 timeout -k 10 500 python tools/ab_kernels.py tools/variants/lib_sc_split.so tools/variants/lib_sc.so tools/variants/lib_rp_base.so --rounds 12 --warm 1200 --rollouts 8 > $O/ab_rollout_rev.log 2>&1 && tail -4 $O/ab_rollout_rev.log | head -3 \
+&& echo "== ab qnet" && MG_AB_FLAGS=1 timeout -k 10 400 python tools/ab_kernels.py tools/variants/lib_rp_base.so tools/variants/lib_sc.so tools/variants/lib_sc_split.so --qnet --rounds 4 --warm 1200 > $O/ab_qnet.log 2>&1 && tail -3 $O/ab_qnet.log \
+&& echo "== all ok"
