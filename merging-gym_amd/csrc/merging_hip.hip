@@ -88,7 +88,8 @@ MG_HD double div_const(double x, double d, double inv) {
 // results come back by value (round 4): through pointers they were private-memory loads in the
 // caller, and the wait for those at the join after the branch -- one in-order counter for vector
 // loads and stores on gfx950 -- also waited for every store the wave had in flight, on the common
-// path too. Config 5 -1.5 to -3 % per step, the rollout and h-DQN within noise (profiles/r04/ab/r04z_*).
+// path too. Config 5 -1.5 to -3 % per step, the rollout and h-DQN within noise (profiles/r04/ab/
+// r04z_*, and r04ab_*: the rollout in both orders, and by-value in the lockstep path only, which tied).
 __device__ __attribute__((noinline, unused)) double2 sincos_cold(double t) {
   double s, c;
   sincos(t, &s, &c);
