@@ -50,3 +50,24 @@ def test_recorded_bench_line_keeps_the_contract(path):
     if "cpu_baseline" in d:  # the default run times the oracle on the host (rank 0, N = 1)
         c = d["cpu_baseline"]
         assert c["kind"] in ("port", "reference") and c["cores"] >= 1 and c["value"] > 0 and c["sample"]
+
+
+GRIDS = sorted(glob.glob(os.path.join(ROOT, "profiles", "r04", "kernel_stats_by_grid_r04*.json")))
+
+
+@pytest.mark.skipif(not GRIDS, reason="no recorded rocprofv3 summaries")
+@pytest.mark.parametrize("path", GRIDS, ids=[os.path.basename(p) for p in GRIDS])
+def test_rocprof_step_kernel_average_agrees_with_the_bench_line(path):
+    """The committed rocprofv3 summary of a pass and that pass's bench line time the same kernel:
+    the step kernel's average at the 2^20 grid agrees with roofline.kernel_ms_mean within 5 %."""
+    tag = os.path.basename(path)[len("kernel_stats_by_grid_"):-len(".json")]
+    bench = os.path.join(ROOT, "profiles", "r04", f"bench_default_{tag}.json")
+    if not os.path.exists(bench):
+        pytest.skip(f"no bench line for {tag}")
+    d = _load(bench)
+    r = d["roofline"]
+    with open(path) as f:
+        rows = json.load(f)
+    step = [x for x in rows if x["kernel"] == r["kernel"] and x["grid_threads"] == d["config"]["envs_per_gpu"]]
+    assert step, (r["kernel"], [x["kernel"] for x in rows])
+    assert abs(step[0]["avg_us"] / (r["kernel_ms_mean"] * 1e3) - 1) < 0.05
