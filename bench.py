@@ -322,6 +322,17 @@ def rollout_leg(env, args, world, dist, torch):
 
 
 QNET_USEFUL_FLOP = 2 * (10 * 200 + 200 * 100 + 100 * 5)      # one Net forward, main.py:30-47
+# The reference evaluates a net only on choose_action's / choose_goal's greedy branch
+# (np.random.randn() <= EPISILO: P = Phi(0.7), main.py:105, hdqn.py:86, :170) plus once per finished
+# episode for the logged q_eval (main.py:221, hdqn.py:330). Round 5: useful FLOPs count exactly those
+# forwards (the kernels since round 5 compute only them, and the counts below come from the leg's
+# own episodes and goal breaks); rounds 1-4 counted one forward per net per env-step.
+
+
+def p_greedy():
+    from merging_gym.policy import greedy_threshold
+
+    return greedy_threshold() / 2.0 ** 32
 # MFMAs issued per 64-env forward (ABI 19). The 16x16 forward (self-play / other-net opponents,
 # h-DQN): layer 1 14 x 32x32x16, layers 2 and 3 (196 + 16) x 16x16x32. The 32x32 forward (config 5
 # without a net opponent): 132 x 32x32x16 (padded tiles, all-padding k-blocks skipped).
@@ -382,6 +393,11 @@ def qnet_leg(env, args, world, dist, torch, opponent):
     mfma_flop, sustained = ((QNET32_MFMA_FLOP, MFMA32_BF16_SUSTAINED_TFLOPS) if nets == 1
                             else (QNET_MFMA_FLOP, MFMA_BF16_SUSTAINED_TFLOPS))
     per_s = E * T / (kernel_ms * 1e-3)
+    summ = env.episode_summary()  # untimed: mg_stats_reduce over the warm-up and timed launches' records
+    ep_rate = summ["completed"] / (E * T * (L + max(1, args.leg_warmup)))  # episodes per env-step
+    # forwards the reference runs per env-step: the ego's greedy branch + q_eval once per episode,
+    # the opponent's greedy branch (self / other net)
+    fwd = p_greedy() * nets + ep_rate
     # BASELINE config 5: greedy-action agreement with the reference's fp32 Net on the CPU
     # (main.py:30-47, re-declared here with torch) over the envs' current observations
     sample = env.observe()[: 1 << 16].clone()
@@ -391,7 +407,6 @@ def qnet_leg(env, args, world, dist, torch, opponent):
     h = torch.relu(x @ w["fc1.weight"].T + w["fc1.bias"])
     h = torch.relu(h @ w["fc2.weight"].T + w["fc2.bias"])
     greedy_cpu = (h @ w["out.weight"].T + w["out.bias"]).argmax(1)
-    summ = env.episode_summary()  # untimed: mg_stats_reduce over the warm-up and timed launches' records
     return {"episodes": {k: summ[k] for k in ("completed", "mean_q_eval", "mean_ep_reward_main", "win_rate_main",
                                                "collision_rate")},
             "q_eval_logged_as": "eval_net(state)[action] on each episode's last input and action (main.py:221)",
@@ -401,18 +416,36 @@ def qnet_leg(env, args, world, dist, torch, opponent):
             "steps_per_launch": T, "launches": L, "dtype": "bf16 (fp32 accumulate)",
             "value": world * E * T * L / elapsed, "unit": "env-steps/s",
             "ms_per_step": elapsed / (L * T) * 1e3, "kernel_ms_mean": kernel_ms,
-            "useful_tflops": nets * QNET_USEFUL_FLOP * per_s / 1e12,
+            "reference_forwards_per_env_step": fwd,
+            "forwards_rule": ("P(greedy) = Phi(0.7) per net per env-step (main.py:105) + one per finished episode "
+                              "(q_eval, main.py:221)"),
+            "useful_tflops": fwd * QNET_USEFUL_FLOP * per_s / 1e12,
             "forward": "32x32" if nets == 1 else "16x16",
-            "mfma_tflops": nets * mfma_flop * per_s / 1e12,
+            "mfma_tflops_if_every_forward_ran": nets * mfma_flop * per_s / 1e12,
             "peak_tflops": MFMA_BF16_PEAK_TFLOPS,
-            "frac_useful": nets * QNET_USEFUL_FLOP * per_s / 1e12 / MFMA_BF16_PEAK_TFLOPS,
+            "frac_useful": fwd * QNET_USEFUL_FLOP * per_s / 1e12 / MFMA_BF16_PEAK_TFLOPS,
             "sustained_tflops": sustained,
-            "mfma_frac_of_sustained": nets * mfma_flop * per_s / 1e12 / sustained,
             "greedy_agreement_vs_fp32_cpu": float((greedy_gpu == greedy_cpu).double().mean()),
             "agreement_sample": int(x.shape[0])}
 
 
-HDQN_USEFUL_FLOP = 2 * (10 * 200 + 200 * 100 + 100 * 3) + 2 * (11 * 200 + 200 * 100 + 100 * 5)  # meta + lower
+HDQN_META_FLOP = 2 * (10 * 200 + 200 * 100 + 100 * 3)   # Goal_DQN's meta-net (hdqn.py:38-55, 10 -> 3)
+HDQN_LOWER_FLOP = 2 * (11 * 200 + 200 * 100 + 100 * 5)  # HDQN's lower-level net on [goal] + state (11 -> 5)
+
+
+def hdqn_useful_flop(p, brk, ep, opponent_nets):
+    """bf16 FLOPs per env-step of the forwards hdqn.py runs (greedy branches only): the ego's
+    choose_goal on every next state (:303) and again at each new outer iteration (:283: after a
+    goal break on the same state, after an episode end on the reset one), its choose_action every
+    step (:292), the episode's q_eval (:330); with a net opponent its choose_action every step (:300)
+    and its choose_goal at each outer iteration (:285). brk: outer iterations per env-step (goal
+    breaks and episode ends, :322), ep: episodes per env-step."""
+    meta = p * (1.0 + brk) + ep
+    lower = p
+    if opponent_nets:
+        meta += p * brk
+        lower += p
+    return meta * HDQN_META_FLOP + lower * HDQN_LOWER_FLOP
 
 
 def hdqn_leg(env, args, world, dist, torch):
@@ -462,6 +495,7 @@ def hdqn_leg(env, args, world, dist, torch):
     per_s = E * T / (kernel_ms * 1e-3)
     summ = env.episode_summary()  # untimed: the warm-up and timed launches' episodes (mg_stats_reduce)
     episodes = {k: summ[k] for k in ("completed", "mean_q_eval", "mean_return_ego", "win_rate_hdqn", "collision_rate")}
+    ep_rate = summ["completed"] / (E * T * (L + max(1, args.leg_warmup)))
     # untimed: one launch with Goal_DQN's columns, for the inner-loop break rate (:322)
     tr = env.rollout_hdqn(T, meta, lower, args.seed, first_step=k, final_observation=False, goal_memory=True)
     k += T
@@ -521,27 +555,31 @@ def hdqn_leg(env, args, world, dist, torch):
     other_ms = timed(lambda: env.rollout_hdqn(T, meta, lower, args.seed, opponent=(meta_op, lower_op),
                                               first_step=k, final_observation=False))
     other_per_s = E * T / (other_ms * 1e-3)
-    self_flop = HDQN_USEFUL_FLOP + 2 * (11 * 200 + 200 * 100 + 100 * 5)  # + the opponent's lower net
+    p = p_greedy()
+    l0_flop = hdqn_useful_flop(p, break_rate, ep_rate, False)
+    self_flop = hdqn_useful_flop(p, break_rate, ep_rate, True)  # the L0 leg's break / episode rates
     return {"kernel": "hdqn_rollout_kernel<0>", "opponent": "none", "steps_per_launch": T, "launches": L,
             "selfplay": {"kernel": "hdqn_rollout_kernel<2>", "kernel_ms_mean": self_ms,
-                         "env_steps_per_s": self_per_s, "useful_tflops_lower_bound": self_flop * self_per_s / 1e12,
-                         "frac_useful_lower_bound": self_flop * self_per_s / 1e12 / MFMA_BF16_PEAK_TFLOPS,
-                         "note": "useful FLOPs count the opponent's lower net every step, not its meta-net "
-                                 "(run only at outer-loop iterations)"},
+                         "env_steps_per_s": self_per_s, "useful_tflops": self_flop * self_per_s / 1e12,
+                         "frac_useful": self_flop * self_per_s / 1e12 / MFMA_BF16_PEAK_TFLOPS},
             "other_checkpoint": {"kernel": "hdqn_rollout_kernel<3>", "kernel_ms_mean": other_ms,
                                  "env_steps_per_s": other_per_s,
-                                 "frac_useful_lower_bound": self_flop * other_per_s / 1e12 / MFMA_BF16_PEAK_TFLOPS,
+                                 "frac_useful": self_flop * other_per_s / 1e12 / MFMA_BF16_PEAK_TFLOPS,
                                  "note": "opponent nets read from global memory (L2, fragment-major copies), not LDS"},
+            "useful_flop_rule": ("hdqn.py's forwards, greedy branches only (P = Phi(0.7)): ego meta-net per next state "
+                                 "and per outer iteration, ego lower net per step, q_eval per episode; a net opponent "
+                                 "adds its lower net per step and its meta-net per outer iteration (break and "
+                                 "episode rates of the L0 leg)"),
+            "useful_flop_per_env_step": {"L0": l0_flop, "selfplay_other": self_flop},
             "with_goal_ring": {"fused_store_ms_per_launch": fused_ms, "rollout_then_replay_store_ms": separate_ms,
                                "fused_env_steps_per_s": E * T / (fused_ms * 1e-3),
                                "separate_env_steps_per_s": E * T / (separate_ms * 1e-3),
                                "ring_capacity": 1 << 24},
             "dtype": "bf16 (fp32 accumulate)", "value": world * E * T * L / elapsed, "unit": "env-steps/s",
             "ms_per_step": elapsed / (L * T) * 1e3, "kernel_ms_mean": kernel_ms,
-            "useful_tflops": HDQN_USEFUL_FLOP * per_s / 1e12, "peak_tflops": MFMA_BF16_PEAK_TFLOPS,
-            "frac_useful": HDQN_USEFUL_FLOP * per_s / 1e12 / MFMA_BF16_PEAK_TFLOPS,
-            "mfma_tflops": 2 * QNET_MFMA_FLOP * per_s / 1e12, "sustained_tflops": MFMA_BF16_SUSTAINED_TFLOPS,
-            "mfma_frac_of_sustained": 2 * QNET_MFMA_FLOP * per_s / 1e12 / MFMA_BF16_SUSTAINED_TFLOPS,
+            "useful_tflops": l0_flop * per_s / 1e12, "peak_tflops": MFMA_BF16_PEAK_TFLOPS,
+            "frac_useful": l0_flop * per_s / 1e12 / MFMA_BF16_PEAK_TFLOPS,
+            "episodes_per_env_step": ep_rate,
             "nets": "seeded, torch.nn.Linear default init U(-1/sqrt(in), 1/sqrt(in)) (signed)",
             "goal_break_rate_per_step": break_rate, "next_goal_share": greedy_goal_spread,
             "episodes": episodes,
@@ -673,16 +711,20 @@ def main():
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
+    env_world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    device = torch.device("cuda", local % max(torch.cuda.device_count(), 1) if world > 1 else 0)
+    device = torch.device("cuda", local % max(torch.cuda.device_count(), 1) if env_world > 1 else 0)
     torch.cuda.set_device(device)
-    if world > 1:
+    backend = None
+    if env_world > 1:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=device)
         else:
             dist.init_process_group(args.dist_backend)
+        backend = dist.get_backend()
+    # the rank count and rank the process group reports (RCCL under backend "nccl" on ROCm)
+    world = dist.get_world_size() if env_world > 1 else 1
+    rank = dist.get_rank() if env_world > 1 else 0
     host_coll = world > 1 and args.dist_backend != "nccl"
 
     from merging_gym import MergeVecEnv
@@ -840,14 +882,28 @@ def main():
 
     total_env_steps = world * E * args.steps
     value = total_env_steps / elapsed
+    # the CPU baseline and the config-1 drop-in leg run on rank 0 after every rank's GPU legs, at any
+    # world size (north_star: the reference-style step timed on the box's host cores in the same run);
+    # the other ranks wait at the closing barrier. The child process never touches a GPU.
+    cpu = dropin = None
+    if world > 1:
+        dist.barrier()
+    if rank == 0 and not args.no_cpu_baseline:
+        dropin = dropin_leg(args.seed)
+        cpu = cpu_baseline(args.cpu_seconds, E)
+        cpu["ran_while"] = ("the other ranks wait at the closing barrier" if world > 1 else "alone")
     if rank == 0:
         achieved = BYTES_PER_ENV_STEP * E / (kernel_ms * 1e-3) / 1e9 if kernel_ms else None
+        # all ranks' bytes over the slowest rank's mean launch: the whole node against world x peak
+        achieved_agg = world * BYTES_PER_ENV_STEP * E / (kernel_ms_max * 1e-3) / 1e9 if kernel_ms_max else None
         pmc = load_pmc(E)
         line = {
             "metric": "env-steps/sec at batch=2^20; achieved HBM GB/s vs peak; 1/2/4/8-GPU scaling",
             "value": value,
             "unit": "env-steps/s",
             "n_gpus": world,
+            "dist": {"backend": backend, "world_size": world, "rank_printing": rank,
+                     "launcher_world_size": env_world},
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
@@ -874,6 +930,9 @@ def main():
                                         "write-back 2 B, done / collision / actions as one 4-B record); "
                                         "frac_8d: SURVEY.md 8(d)'s 136 B (fp32 returns)"),
                          "kernel_ms_mean": kernel_ms, "kernel_ms_mean_max_rank": kernel_ms_max,
+                         "achieved_aggregate": achieved_agg,
+                         "frac_aggregate": (achieved_agg / (world * HBM_PEAK_GBPS)) if achieved_agg else None,
+                         "aggregate_rule": "world x bytes per launch / the slowest rank's mean launch, vs world x peak",
                          "timing": ("HIP events recorded on the launch stream around the K timed launches "
                                     f"({'one HIP-graph replay' if args.graph else 'K host launches'}), / K"),
                          "kernel_ms_dispatch_sample": dispatch_ms, "host_enqueue_ms_per_launch": host_ms,
@@ -904,12 +963,71 @@ def main():
                     leg["valu"] = valu[key]
         if size2 is not None:
             line["size_2p22"] = size2
-        if world == 1 and not args.no_cpu_baseline:
-            line["dropin_single_env"] = dropin_leg(args.seed)
-            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, E)
-        print(json.dumps(line), flush=True)
+        if cpu is not None:
+            line["dropin_single_env"] = dropin
+            line["cpu_baseline"] = cpu
+        line["stagger"] = {"value": args.stagger, "statistics_cleared": "before the burn-in launches",
+                           "note": "--stagger 0 reproduces the round-3 start (every env's first episode together)"}
+        # the full record on an earlier line (not JSON by itself), then the compact JSON line the
+        # driver parses: it keeps only the last ~8 KB of the output
+        print("bench detail: " + json.dumps(line), flush=True)
+        print(json.dumps(compact_line(line)), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
+
+
+def compact_line(line):
+    """The bench contract's ONE JSON line, kept under ~6 KB: every leg's value, roofline fraction,
+    mean kernel time and traffic; the per-leg details (VALU counters, episode statistics, notes) are
+    on the earlier "bench detail:" line."""
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config", "dist", "build", "stagger")
+    out = {k: line[k] for k in keep if k in line}
+    rf = line["roofline"]
+    out["roofline"] = {k: rf.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel",
+                                             "bytes_per_env_step", "frac_8d", "kernel_ms_mean",
+                                             "kernel_ms_mean_max_rank", "achieved_aggregate", "frac_aggregate")}
+    cb = line.get("cpu_baseline")
+    if cb is not None:
+        out["cpu_baseline"] = ({"error": cb["error"][-300:]} if "error" in cb else
+                               {k: cb.get(k) for k in ("value", "unit", "cores", "kind", "sample", "ran_while")})
+    legs = {}
+    ep = line.get("episodes") or {}
+    legs["step_episodes"] = {k: ep.get(k) for k in ("completed", "collision_rate", "win_rate_hdqn", "allgather_ms",
+                                                   "reduce_ms")}
+    if "size_2p22" in line:
+        z = line["size_2p22"]
+        legs["size_2p22"] = {k: z.get(k) for k in ("envs", "value", "kernel_ms", "frac", "frac_8d", "traffic")}
+    if "rollout" in line:
+        z = line["rollout"]
+        legs["rollout"] = {k: z.get(k) for k in ("kernel", "value", "kernel_ms_mean", "bytes_per_env_step", "frac",
+                                                "traffic")}
+    if "replay" in line:
+        z = line["replay"]
+        legs["replay"] = {k: z.get(k) for k in ("value", "unit", "ms_per_store", "frac", "sample_128_us")}
+    for z in line.get("qnet_policy") or []:
+        legs["qnet_" + z["opponent"].split(" ")[0]] = {
+            k: z.get(k) for k in ("kernel", "value", "kernel_ms_mean", "frac_useful", "reference_forwards_per_env_step",
+                                  "greedy_agreement_vs_fp32_cpu")}
+        legs["qnet_" + z["opponent"].split(" ")[0]]["q_eval_mean"] = z["episodes"]["mean_q_eval"]
+    h = line.get("hdqn_policy")
+    if h is not None:
+        legs["hdqn_L0"] = {"kernel": h["kernel"], "value": h["value"], "kernel_ms_mean": h["kernel_ms_mean"],
+                           "frac_useful": h["frac_useful"], "goal_break_rate": h["goal_break_rate_per_step"]}
+        for key, name in (("selfplay", "hdqn_self"), ("other_checkpoint", "hdqn_other")):
+            z = h[key]
+            legs[name] = {"kernel": z["kernel"], "env_steps_per_s": z["env_steps_per_s"],
+                          "kernel_ms_mean": z["kernel_ms_mean"], "frac_useful": z["frac_useful"]}
+        legs["hdqn_goal_ring"] = {k: h["with_goal_ring"][k] for k in ("fused_env_steps_per_s",
+                                                                     "separate_env_steps_per_s")}
+    d = line.get("dropin_single_env")
+    if d is not None:
+        legs["dropin_single_env_us_per_step"] = {k: d[k]["us_per_step"] for k in ("host_dropin", "gpu_dropin",
+                                                                                   "cpu_python_port")}
+    out["legs"] = legs
+    out["detail"] = "the full record is the 'bench detail:' line above"
+    return out
 
 
 if __name__ == "__main__":

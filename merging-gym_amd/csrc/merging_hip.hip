@@ -22,6 +22,7 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -1394,8 +1395,18 @@ __device__ __forceinline__ void qnet_gather_q(const f32x4 (&acc3)[4], float (&q)
 // (each W2 fragment feeds the four column tiles' MFMAs); layer 3's k-blocks follow the last
 // k-block's layer-2 row tiles they read. Unrolled, the first MFMA into each accumulator takes an
 // inline zero and the next k-block's operands land in their final registers.
-template <int D, class Src>
+//
+// NC (round 5): the number of 16-env column tiles computed, 1..4: lanes 16 NC .. 63 get no result.
+// Column tiles are independent (each MFMA column is one env), so the envs computed get the same
+// bits as in a full forward; a pass over a compacted list of the envs whose Q the reference
+// evaluates (its greedy branch) skips the other tiles' MFMAs. NC <= 2 also skips the layer-1 half
+// xb1 and its ReLU / swap work. A compile-time count (qnet_mlp_nc dispatches): guarding each MFMA
+// with a runtime test put a scalar branch behind every MFMA and cost +66 % per h-DQN launch even
+// where every tile ran (r05a).
+template <int D, int NC = 4, class Src>
 __device__ __forceinline__ void qnet_mlp(const Src& src, bf16x8 xb0, bf16x8 xb1, float (&q)[8]) {
+  static_assert(NC >= 1 && NC <= 4, "1..4 column tiles");
+  constexpr int nc = NC;
   static_assert(kQT1 == 7 && kQT2 == 7 && kQK3 == 4 && kQFrags == 60,
                 "qfrag's consumption order assumes 7 k-blocks, 7 layer-2 row tiles and 4 layer-3 k-blocks");
   bf16x8 ring[D];
@@ -1409,10 +1420,11 @@ __device__ __forceinline__ void qnet_mlp(const Src& src, bf16x8 xb0, bf16x8 xb1,
   const f32x16 z16 = {};
   const f32x4 z4 = {};
   f32x16 c0, c1;
+  constexpr bool hi = nc > 2;  // column tiles 2 and 3: the layer-1 half xb1
   auto layer1 = [&](int s) __attribute__((always_inline)) {
     const bf16x8 a1 = take(s);
     c0 = mfma32(a1, xb0, z16);
-    c1 = mfma32(a1, xb1, z16);
+    if (hi) c1 = mfma32(a1, xb1, z16);
   };
   // packed ReLU pairs of c0 (d = 0..7) and c1 (d = 8..15)
   auto relu_d = [&](int d) __attribute__((always_inline)) {
@@ -1433,9 +1445,13 @@ __device__ __forceinline__ void qnet_mlp(const Src& src, bf16x8 xb0, bf16x8 xb1,
   };
   layer1(0);
 #pragma unroll
-  for (int d = 0; d < 16; ++d) nx[d] = relu_d(d);
+  for (int d = 0; d < 8; ++d) nx[d] = relu_d(d);
+  if (hi) {
+#pragma unroll
+    for (int d = 8; d < 16; ++d) nx[d] = relu_d(d);
+  }
   swap_u(0);
-  swap_u(1);
+  if (hi) swap_u(1);
   bf16x8 hb[4];
   operands(hb);
   f32x4 acc2[kQT2][4];
@@ -1456,11 +1472,11 @@ __device__ __forceinline__ void qnet_mlp(const Src& src, bf16x8 xb0, bf16x8 xb1,
       const bf16x8 a2 = take(s++);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        slot(acc2[t2][t], a2, hb[t], kb == 0);
+        if (t < nc) slot(acc2[t2][t], a2, hb[t], kb == 0);
         // the next k-block's operands: ReLU pairs behind row tiles 1..4, swaps behind 5 and 6
-        if (t2 >= 1 && t2 <= 4) nx[4 * (t2 - 1) + t] = relu_d(4 * (t2 - 1) + t);
+        if (t2 >= 1 && t2 <= 4 && (t2 <= 2 || hi)) nx[4 * (t2 - 1) + t] = relu_d(4 * (t2 - 1) + t);
         if (t2 == 5) permlane16_swap(nx[t], nx[4 + t]);
-        if (t2 == 6) permlane16_swap(nx[8 + t], nx[12 + t]);
+        if (t2 == 6 && hi) permlane16_swap(nx[8 + t], nx[12 + t]);
       }
     }
     operands(hb);
@@ -1468,7 +1484,7 @@ __device__ __forceinline__ void qnet_mlp(const Src& src, bf16x8 xb0, bf16x8 xb1,
   // The last k-block with layer 3 interleaved. Layer-3 k-block k3 reads row tiles 2 k3 and 2 k3 + 1;
   // the ReLU pairs of its B operands are built in the slots after each row tile's MFMAs have issued
   // (two pairs per slot), into two buffers used alternately.
-  f32x4 acc3[4];
+  f32x4 acc3[4] = {z4, z4, z4, z4};  // the tiles past nc stay zero (never read as results)
   uint32_t b3[2][4][4];
   auto pairs3 = [&](int t2, int t) __attribute__((always_inline)) {  // row tile t2 of env tile t
     const int buf = (t2 >> 1) & 1, d = 2 * (t2 & 1);
@@ -1480,8 +1496,8 @@ __device__ __forceinline__ void qnet_mlp(const Src& src, bf16x8 xb0, bf16x8 xb1,
     const bf16x8 a2 = take(s++);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      slot(acc2[t2][t], a2, hb[t], false);
-      if (p >= 0) pairs3(p, t);
+      if (t < nc) slot(acc2[t2][t], a2, hb[t], false);
+      if (p >= 0 && t < nc) pairs3(p, t);
     }
   };
   auto layer3 = [&](int k3, int p) __attribute__((always_inline)) {
@@ -1491,8 +1507,8 @@ __device__ __forceinline__ void qnet_mlp(const Src& src, bf16x8 xb0, bf16x8 xb1,
     for (int t = 0; t < 4; ++t) {
       if (2 * k3 + 1 >= kQT2) b3[buf][t][2] = b3[buf][t][3] = 0u;  // row tile 7 does not exist
       const bf16x8 b = __builtin_bit_cast(bf16x8, u32x4{b3[buf][t][0], b3[buf][t][1], b3[buf][t][2], b3[buf][t][3]});
-      slot(acc3[t], a3, b, k3 == 0);
-      if (p >= 0) pairs3(p, t);
+      if (t < nc) slot(acc3[t], a3, b, k3 == 0);
+      if (p >= 0 && t < nc) pairs3(p, t);
     }
   };
   static_assert(kQT2 == 7 && kQK3 == 4, "the tail below is written for 7 row tiles, 4 layer-3 k-blocks");
@@ -1510,9 +1526,34 @@ __device__ __forceinline__ void qnet_mlp(const Src& src, bf16x8 xb0, bf16x8 xb1,
   qnet_gather_q(acc3, q);
 }
 
+// qnet_mlp on nc (1..4, wave-uniform) column tiles: one instance per count. Every call site inlines
+// all four, so the kernels keep one or two call sites (a pass loop), not one per pass. A weight
+// fragment feeds nc MFMAs, so the fewer the column tiles the less of a fragment's load latency its
+// MFMAs cover: the ring deepens as nc falls (D(nc) fragments in flight, D the full forward's; the
+// fewer accumulators of a narrow instance leave the registers for it).
+template <int D, class Src>
+__device__ __forceinline__ void qnet_mlp_nc(const Src& src, bf16x8 xb0, bf16x8 xb1, float (&q)[8], int nc) {
+  switch (nc) {
+    case 1:
+      qnet_mlp<4 * D, 1>(src, xb0, xb1, q);
+      break;
+    case 2:
+      qnet_mlp<2 * D, 2>(src, xb0, xb1, q);
+      break;
+    case 3:
+      qnet_mlp<D + D / 2, 3>(src, xb0, xb1, q);
+      break;
+    default:
+      qnet_mlp<D, 4>(src, xb0, xb1, q);
+  }
+}
+
 // the forward of a net in LDS
 __device__ __forceinline__ void qnet_mlp_swp(const uint8_t* net, bf16x8 xb0, bf16x8 xb1, float (&q)[8]) {
   qnet_mlp<kQLdsAhead>(qnet_lds(net), xb0, xb1, q);
+}
+__device__ __forceinline__ void qnet_mlp_swp_nc(const uint8_t* net, bf16x8 xb0, bf16x8 xb1, float (&q)[8], int nc) {
+  qnet_mlp_nc<kQLdsAhead>(qnet_lds(net), xb0, xb1, q, nc);
 }
 
 // Q-values of this lane's env (rows 0..7) from the block's f32 observation tile in LDS.
@@ -1743,6 +1784,15 @@ __global__ __launch_bounds__(64) void qnet_fragments_kernel(const uint8_t* packe
   if (i < kQNetBytes / 16) reinterpret_cast<u32x4*>(frags)[i] = reinterpret_cast<const u32x4*>(packed)[i];
 }
 
+// This lane's rank among the set lanes of a ballot (lanes below it whose bit is set).
+__device__ __forceinline__ int lane_rank(uint64_t m) {
+  return static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u)));
+}
+
+// 16-env column tiles of a forward over n (1..64) compacted items
+__device__ __forceinline__ int col_tiles(int n) { return (n + 15) >> 4; }
+
 __device__ __forceinline__ int argmax_first(const float (&q)[8], int out_dim) {
   int best = 0;
   float v = q[0];
@@ -1785,6 +1835,10 @@ __global__ __launch_bounds__(kBlock) void qnet_forward_kernel(const uint8_t* net
   }
 }
 
+// may_finish_next's constants (below)
+struct FinishBound {
+  float smin, smax, g;  // min / max of action_dict, the MPC's speed gain per step
+};
 struct QRollout {
   mg_params P;
   Reset0 R0;
@@ -1802,7 +1856,54 @@ struct QRollout {
   int32_t num_steps;
   int32_t out_dim;
   uint32_t flags;
+  FinishBound fin;  // may_finish_next's constants
 };
+
+// Whether env e's next step can end its episode, for ANY pair of actions (a conservative superset of
+// env_step's done, tests/test_may_finish.py): main.py:221 logs eval_net(state)[action] of an
+// episode's last step whatever branch chose the action, so the config-5 kernels evaluate the net for
+// these envs even where the ego explores. From the state a step acts on (o: its fp32 observation;
+// every margin below is >= 0.25 m, far above the fp32 rounding of o):
+//   timeout   the step count reaches timeout_steps (env_clock);
+//   arrival   a car can pass END_POINT within the step and that ends the episode (the other car
+//             already won, or both arrive): p' = p + dT v' with v' between v and the action's target
+//             speed, so END_POINT - p < dT max(v, smax) + 0.5;
+//   collision the boxes can overlap afterwards. Laterally trunc(y1) - trunc(y2) <= 4 needs
+//             y1 - y2 < 5 (y1 >= y2 on the two arcs), and a step moves each y by at most
+//             |sin theta| dT v' < 0.3 m there. Longitudinally |t1 - t2| <= 8 needs |x1 - x2| < 9, and a
+//             step changes x1 - x2 by at most dT |v1' - v2'| (+ 0.2 % for the arc): the MPC moves each
+//             speed by g (s - v), g = dT z0 / z'n = 1/15 (mpc_acc), so |v1' - v2'| <= |v1 - v2| +
+//             g (max(smax, v1, v2) - min(smin, v1, v2)).
+// Flags ~2.2 % of env-steps in uniform random play (tests/test_may_finish.py).
+MG_HD bool may_finish_next(const mg_params& P, const Env& e, const obs_t (&o)[kObs], const FinishBound& B) {
+  if (static_cast<int32_t>(e.steps) + 1 >= P.timeout_steps) return true;
+  const float dt = static_cast<float>(P.dT);
+  const bool ego = o[3] < dt * fmaxf(o[4], B.smax) + 0.5f;  // o[3] = END_POINT - p1, o[4] = v1
+  const bool opp = o[8] < dt * fmaxf(o[9], B.smax) + 0.5f;  // o[8] = END_POINT - p2, o[9] = v2
+  const bool arrive = e.winner == 1 ? opp : (e.winner == 2 ? ego : (ego && opp));
+  const float spread = fmaxf(B.smax, fmaxf(o[4], o[9])) - fminf(B.smin, fminf(o[4], o[9]));
+  const float rel = dt * (fabsf(o[2]) + B.g * spread) + 0.5f;  // o[2] = v2 - v1
+  const bool coll = -o[1] < 5.75f && fabsf(o[0]) < 9.0f + rel;  // o[1] = y2 - y1, o[0] = x2 - x1
+  return arrive || coll;
+}
+
+// The need bits of env gi's step `step` for the config-5 Q-net waves (opponent modes 2 / 3): bit 0
+// the ego's forward (its greedy draw, or may_finish_next while statistics are kept), bit 1 the
+// opponent's (its greedy draw). u: the step's Philox words (qnet_policy_step_n's stream).
+__device__ __forceinline__ uint8_t qnet_need_bits(const QRollout& R, const uint4& u, bool live, const Env& e,
+                                                  const obs_t (&o)[kObs]) {
+  if (!live) return 0;
+  const bool fin = R.St.rec != nullptr && (R.flags & MG_AUTORESET) && may_finish_next(R.P, e, o, R.fin);
+  return static_cast<uint8_t>(((static_cast<uint64_t>(u.x) < R.greedy_thr || fin) ? 1 : 0) |
+                              (static_cast<uint64_t>(u.z) < R.opp_greedy_thr ? 2 : 0));
+}
+
+__device__ __forceinline__ uint4 qnet_draws(const QRollout& R, int64_t i, uint64_t step) {
+  const uint64_t gi = static_cast<uint64_t>(R.env_offset + i);
+  return philox4x32_10(make_uint4(static_cast<uint32_t>(gi), static_cast<uint32_t>(gi >> 32),
+                                  static_cast<uint32_t>(step), static_cast<uint32_t>(step >> 32)),
+                       static_cast<uint32_t>(R.seed), static_cast<uint32_t>(R.seed >> 32));
+}
 
 
 // One epsilon-greedy step (main.py:99-112) of the N envs i0 + 64 j of one env-wave lane given their
@@ -1823,7 +1924,7 @@ __device__ __forceinline__ void qnet_policy_step_n(const QRollout& R, Env (&e)[N
                                                    int64_t i0, const bool (&live)[N], int t,
                                                    const int (&greedy1)[N], const int (&greedy2)[N],
                                                    bool (&won)[N], const float* qrow, uint2 (&keep)[N],
-                                                   double (&pend)[N]) {
+                                                   double (&pend)[N], uint4 (&un)[N], uint8_t* need) {
   const uint64_t step = R.first_step + t;
   int a1[N], a2[N];
 #pragma unroll
@@ -1854,10 +1955,7 @@ __device__ __forceinline__ void qnet_policy_step_n(const QRollout& R, Env (&e)[N
         a2[j] = MG_ACTION_NONE;
       }
     } else {
-      const uint4 u = philox4x32_10(
-          make_uint4(static_cast<uint32_t>(gi), static_cast<uint32_t>(gi >> 32),
-                     static_cast<uint32_t>(step), static_cast<uint32_t>(step >> 32)),
-          static_cast<uint32_t>(R.seed), static_cast<uint32_t>(R.seed >> 32));
+      const uint4 u = un[j];  // drawn one phase ahead, with the need bits the Q-net waves compacted by
       a1[j] = (static_cast<uint64_t>(u.x) < R.greedy_thr) ? greedy1[j] : action_from_u32(u.y);
       a2[j] = (static_cast<uint64_t>(u.z) < R.opp_greedy_thr) ? greedy2[j] : action_from_u32(u.w);
     }
@@ -1879,6 +1977,15 @@ __device__ __forceinline__ void qnet_policy_step_n(const QRollout& R, Env (&e)[N
     if (after_step_nowait(R.P, e[j], r[j], R.St, R.T.final_obs ? R.T.final_obs + row * kObs : nullptr, i,
                           (R.flags & MG_AUTORESET) != 0, pend[j], &R.R0))
       add_q_eval_nowait(R.St, i, qrow[64 * j * kObs + a1[j]]);
+  }
+  if constexpr (OPP >= 2) {  // the next step's draws and need bits, for Q(X, t + 1)
+    if (t + 1 < R.num_steps) {
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        un[j] = qnet_draws(R, i0 + 64 * j, step + 1);
+        need[64 * j] = qnet_need_bits(R, un[j], live[j], e[j], r[j].o);
+      }
+    }
   }
 }
 
@@ -1944,6 +2051,12 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
   __shared__ __attribute__((aligned(16))) uint8_t lds_net2[OPP == 3 ? kQNetBytes : 16];
   __shared__ __attribute__((aligned(16))) float tile[kEnvs * kObs];
   __shared__ uint8_t greedy[2][kEnvs];
+  // OPP 2 / 3 (round 5): per Q-net wave the compacted items of a phase (env e of the wave's 128 |
+  // 0x80 the opponent's view); greedy[1][j] holds env j's need bits (qnet_need_bits) when a phase begins
+  __shared__ uint8_t qlist[OPP >= 2 ? 4 : 1][OPP >= 2 ? 256 : 1];
+  // OPP 2: each listed item's layer-1 B fragment halves (the view it needs), staged by the env's own
+  // lane, so one forward can hold both views' items (one net) and reads its inputs lane-linearly
+  __shared__ __attribute__((aligned(16))) u32x4 qstage[OPP == 2 ? 4 : 1][OPP == 2 ? 256 : 1][2];
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int64_t base = static_cast<int64_t>(blockIdx.x) * kEnvs;
@@ -1964,6 +2077,92 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
     // registers apart -- in one loop the env state sat beside the accumulators and spilled)
     __syncthreads();
     for (int p = 0; p < phases; ++p) {
+      if constexpr (OPP >= 2) {
+        // Only the forwards the reference evaluates (round 5): choose_action runs the net on its
+        // greedy branch only (main.py:105-107), and :221 evaluates it on an episode's last step.
+        // The wave's 128 envs of the group are compacted by their need bits into one list, the
+        // opponent's items (swapped view) first, and each view's items run through the forward 64
+        // at a time on col_tiles(count) column tiles. The ego's q[0..4] go into the env's tile row
+        // for q_eval, after every read of that row (the opponent items come first).
+        if (p < 2 * R.num_steps) {
+          static_assert(kTiles == 2, "the list holds the wave's two 64-env tiles");
+          const int gb = (p & 1) * kHalf;
+          auto row_of = [&](int e) __attribute__((always_inline)) { return gb + (4 * ((e >> 6) & 1) + wave) * 64 + (e & 63); };
+          uint8_t* list = qlist[wave];
+          const int nb0 = greedy[1][row_of(lane)], nb1 = greedy[1][row_of(64 + lane)];
+          const uint64_t mo0 = __ballot(nb0 & 2), mo1 = __ballot(nb1 & 2);
+          const uint64_t me0 = __ballot(nb0 & 1), me1 = __ballot(nb1 & 1);
+          const int Lo0 = __popcll(mo0), Lo = Lo0 + __popcll(mo1);
+          const int Le0 = __popcll(me0), Ln = Lo + Le0 + __popcll(me1);
+          if (nb0 & 2) list[lane_rank(mo0)] = static_cast<uint8_t>(0x80 | lane);
+          if (nb1 & 2) list[Lo0 + lane_rank(mo1)] = static_cast<uint8_t>(0x80 | 64 | lane);
+          if (nb0 & 1) list[Lo + lane_rank(me0)] = static_cast<uint8_t>(lane);
+          if (nb1 & 1) list[Lo + Le0 + lane_rank(me1)] = static_cast<uint8_t>(64 | lane);
+          if constexpr (OPP == 2) {
+            // the same net for both views: stage every item's fragments from its env's lane (both
+            // views of the row from one read), then run the whole list 64 items per forward
+            auto stage = [&](int row, int nb, int po, int pe) __attribute__((always_inline)) {
+              float f[kObs];
+#pragma unroll
+              for (int k = 0; k < kObs / 2; ++k) {
+                const f32x2 t2 = reinterpret_cast<const f32x2*>(tile + row * kObs)[k];
+                f[2 * k] = t2[0];
+                f[2 * k + 1] = t2[1];
+              }
+              auto pk = [](float a, float b) { return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2)); };
+              if (nb & 2) {  // the opponent's view state[5:] + state[:5] (main.py:199)
+                qstage[wave][po][0] = u32x4{pk(f[5], f[6]), pk(f[7], f[8]), pk(f[9], f[0]), pk(f[1], f[2])};
+                qstage[wave][po][1] = u32x4{pk(f[3], f[4]), 0u, 0x3F800000u, 0x3F803F80u};
+              }
+              if (nb & 1) {
+                qstage[wave][pe][0] = u32x4{pk(f[0], f[1]), pk(f[2], f[3]), pk(f[4], f[5]), pk(f[6], f[7])};
+                qstage[wave][pe][1] = u32x4{pk(f[8], f[9]), 0u, 0x3F800000u, 0x3F803F80u};
+              }
+            };
+            stage(row_of(lane), nb0, lane_rank(mo0), Lo + lane_rank(me0));
+            stage(row_of(64 + lane), nb1, Lo0 + lane_rank(mo1), Lo + Le0 + lane_rank(me1));
+          }
+          wave_lds_sync();
+          const int r = lane & 31, h = lane >> 5;
+#pragma unroll 1
+          for (int c0 = 0; c0 < Ln;) {
+            // OPP 3: a forward holds one net's items (the opponent's net for the first Lo), built from
+            // the tile rows with the view uniform per forward (a view chosen per lane by selects on
+            // the features cost +35 % per launch, r05f q1 / q2). OPP 2: staged fragments, any mix.
+            const bool opp = c0 < Lo;
+            const int end = (OPP == 3 && opp) ? Lo : Ln;
+            const int cnt = end - c0 < 64 ? end - c0 : 64;
+            auto input = [&](int it) __attribute__((always_inline)) {
+              if constexpr (OPP == 2)
+                return __builtin_bit_cast(bf16x8, qstage[wave][c0 + (it < cnt ? it : 0)][h]);
+              const float* row = tile + row_of(list[c0 + (it < cnt ? it : 0)]) * kObs;
+              return opp ? qnet_input(row, true, h) : qnet_input(row, false, h);
+            };
+            const int e_out = list[c0 + (lane < cnt ? lane : 0)];  // read ahead: its wait hides under the forward
+            float q[8];
+            qnet_mlp_swp_nc((OPP == 3 && opp) ? lds_net2 : lds_net, input(r), input(32 + r), q, col_tiles(cnt));
+            if (lane < cnt) {
+              const int e = e_out;
+              const int row = row_of(e);
+              const uint8_t a = static_cast<uint8_t>(argmax_first(q, R.out_dim));
+              if (e & 0x80) {
+                greedy[1][row] = a;
+              } else {
+                greedy[0][row] = a;
+                // eval_net(state)[0..4] into the row the env wave reads at an episode end (main.py:221)
+                float* qr = tile + row * kObs;
+                reinterpret_cast<f32x2*>(qr)[0] = f32x2{q[0], q[1]};
+                reinterpret_cast<f32x2*>(qr)[1] = f32x2{q[2], q[3]};
+                qr[4] = q[4];
+              }
+            }
+            wave_lds_sync();
+            c0 += cnt;
+          }
+        }
+        __syncthreads();
+        continue;
+      }
       if (p < 2 * R.num_steps) {
 #pragma unroll 1
         for (int tt = 0; tt < kTiles; ++tt) {
@@ -1999,6 +2198,7 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
   bool live0[kIlp], live1[kIlp];
   uint2 keep0[kIlp], keep1[kIlp];  // OPP 0 / 1: the odd step's two draw words (qnet_policy_step_n)
   double pend0[kIlp], pend1[kIlp];  // main.py's pending values (pend_load, after_step_nowait)
+  uint4 un0[kIlp], un1[kIlp];       // OPP 2 / 3: each env's draws of its next step (one phase ahead)
 #pragma unroll
   for (int j = 0; j < kIlp; ++j) {
     const int la = lbase + 64 * j + lane, lb = kHalf + la;
@@ -2006,6 +2206,18 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
     live1[j] = qnet_load_env(R, base + lb, e1[j], tile + lb * kObs);
     pend0[j] = live0[j] ? pend_load(R.St, base + la, e0[j]) : 0.0;
     pend1[j] = live1[j] ? pend_load(R.St, base + lb, e1[j]) : 0.0;
+    if constexpr (OPP >= 2) {  // step 0's draws and need bits (the observation as the tile row holds it)
+      obs_t o0[kObs], o1[kObs];
+#pragma unroll
+      for (int k = 0; k < kObs; ++k) {
+        o0[k] = tile[la * kObs + k];
+        o1[k] = tile[lb * kObs + k];
+      }
+      un0[j] = qnet_draws(R, base + la, R.first_step);
+      un1[j] = qnet_draws(R, base + lb, R.first_step);
+      greedy[1][la] = qnet_need_bits(R, un0[j], live0[j], e0[j], o0);
+      greedy[1][lb] = qnet_need_bits(R, un1[j], live1[j], e1[j], o1);
+    }
 #pragma unroll
     for (int k = 0; k < kObs; ++k) r[j].o[k] = 0.0;
   }
@@ -2023,12 +2235,13 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
       bool won[kIlp];
       // wave-uniform branch: each group's envs stay in named registers
       const float* qrow = tile + (local0 + lane) * kObs;
+      uint8_t* need = &greedy[1][local0 + lane];
       if (g == 0)
         qnet_policy_step_n<OPP, kIlp, CHECKED>(R, e0, r, base + local0 + lane, live0, t, greedy1, greedy2, won, qrow,
-                                               keep0, pend0);
+                                               keep0, pend0, un0, need);
       else
         qnet_policy_step_n<OPP, kIlp, CHECKED>(R, e1, r, base + local0 + lane, live1, t, greedy1, greedy2, won, qrow,
-                                               keep1, pend1);
+                                               keep1, pend1, un1, need);
       const int64_t wbase = base + local0;
 #pragma unroll
       for (int j = 0; j < kIlp; ++j) {
@@ -3226,9 +3439,12 @@ const char* mg_last_error(void) { return g_err; }
 // The compiler that built this library (its hipcc version decides the inline-asm permlane hazard
 // padding of qnet_gather_q, which hipcc 7.2's builtins miscompiled): printed in the GPU test log
 // header and the bench line.
+#ifndef MG_SRC_SHA
+#define MG_SRC_SHA "unknown"  // merging_gym/build.py passes the sha256 of source + header + flags
+#endif
 const char* mg_build_info(void) {
   return "clang " __clang_version__ "; HIP " MG_STR(HIP_VERSION_MAJOR) "." MG_STR(HIP_VERSION_MINOR) "."
-         MG_STR(HIP_VERSION_PATCH) "; ABI " MG_STR(MG_ABI_VERSION) "; gfx950, -ffp-contract=off";
+         MG_STR(HIP_VERSION_PATCH) "; ABI " MG_STR(MG_ABI_VERSION) "; gfx950, -ffp-contract=off; src " MG_SRC_SHA;
 }
 
 void mg_params_default(mg_params* p) {
@@ -3433,6 +3649,14 @@ int mg_rollout_qnet(const mg_params* params, const mg_state* state, const mg_tra
   R.num_steps = num_steps;
   R.out_dim = out_dim;
   R.flags = flags;
+  double smin = params->action_speed[0], smax = smin;
+  for (int a = 1; a < MG_NUM_ACTIONS; ++a) {
+    smin = std::min(smin, params->action_speed[a]);
+    smax = std::max(smax, params->action_speed[a]);
+  }
+  // rounded outward by a margin: the bound only has to contain every speed a step reaches
+  R.fin = FinishBound{static_cast<float>(smin) - 0.5f, static_cast<float>(smax) + 0.5f,
+                      static_cast<float>(params->dT * params->qp_z0 / params->qp_nz) * 1.01f};
   const int64_t block_envs = opponent_mode == 3 ? qws_envs<3>() : qws_envs<0>();
   const unsigned blocks = static_cast<unsigned>((n + block_envs - 1) / block_envs);
   hipStream_t st = static_cast<hipStream_t>(stream);

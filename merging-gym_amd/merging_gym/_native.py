@@ -166,7 +166,25 @@ def _load(path=LIB_PATH):
     return lib
 
 
-lib = _load()
+def _checked_path() -> str:
+    """The in-tree library, built from this tree's source (build.is_current: the sha256 it carries).
+    A stale one is rebuilt where hipcc exists, else refused; MERGING_HIP_LIB (a variant build for
+    tools/ab_*.py) is taken as given."""
+    if "MERGING_HIP_LIB" in os.environ:
+        return LIB_PATH
+    from . import build
+
+    if os.path.exists(build.SRC) and os.path.exists(LIB_PATH) and not build.is_current(LIB_PATH):
+        try:
+            build.hipcc()
+        except FileNotFoundError:
+            raise ImportError(f"{LIB_PATH} was built from another source (src {build.embedded_sha(LIB_PATH)}, "
+                              f"tree {build.source_sha()}) and hipcc is not available to rebuild it")
+        build.build()
+    return LIB_PATH
+
+
+lib = _load(_checked_path())
 
 
 def check(rc: int, what: str) -> None:

@@ -2,10 +2,14 @@
 
 hipcc --offload-arch=gfx950, -ffp-contract=off (the step's fp64 arithmetic must not be
 fused: positions and arrival tests are compared bit-for-bit with the reference's floats).
+The library carries the sha256 of the source, header and flags it was built from (mg_build_info);
+build() recompiles when that differs from the tree's, and merging_gym._native refuses (or rebuilds)
+a stale in-tree library at import.
 """
 
 from __future__ import annotations
 
+import hashlib
 import os
 import shutil
 import subprocess
@@ -29,12 +33,43 @@ def hipcc() -> str:
     raise FileNotFoundError("hipcc not found (ROCm not installed?)")
 
 
+HEADER = os.path.join(INCLUDE, "merging_hip.h")
+
+
+def source_sha(src: str = SRC, header: str = HEADER) -> str:
+    """sha256 (first 16 hex digits) of the kernel source, the C-ABI header and the compiler flags:
+    embedded in the library (mg_build_info "src <sha>") so a build can be matched to its tree."""
+    h = hashlib.sha256()
+    for path in (src, header):
+        with open(path, "rb") as f:
+            h.update(f.read())
+    h.update(" ".join(HIPCC_FLAGS).encode())
+    return h.hexdigest()[:16]
+
+
+def embedded_sha(lib_path: str) -> str | None:
+    """The source sha a built library carries (mg_build_info's "src <sha>"), read from its bytes
+    without loading it; None for a library built before round 5."""
+    try:
+        with open(lib_path, "rb") as f:
+            data = f.read()
+    except OSError:
+        return None
+    i = data.find(b"; src ")
+    return data[i + 6:i + 22].decode("ascii", "replace") if i >= 0 else None
+
+
+def is_current(lib_path: str = OUT, sha: str | None = None) -> bool:
+    """The library at lib_path was built from this tree's source and header (by content, not mtime)."""
+    return embedded_sha(lib_path) == (sha or source_sha())
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
-    deps = [SRC, os.path.join(INCLUDE, "merging_hip.h"), __file__]
-    if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
+    sha = source_sha()
+    if not force and os.path.exists(OUT) and is_current(OUT, sha):
         return OUT
     tmp = OUT + ".tmp"
-    cmd = [hipcc(), *HIPCC_FLAGS, "-I", INCLUDE, "-o", tmp, SRC]
+    cmd = [hipcc(), *HIPCC_FLAGS, f'-DMG_SRC_SHA="{sha}"', "-I", INCLUDE, "-o", tmp, SRC]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd)

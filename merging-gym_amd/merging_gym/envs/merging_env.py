@@ -214,7 +214,11 @@ class MergeEnv(_EnvBase):
     (bench.py `dropin_single_env`): the host path ~7 us, the GPU path ~28 us (a launch plus a stream
     synchronisation per step), the reference-style Python step ~11 us. backend "gpu" (or any
     `device` given): the same step as a batch of one env in the step kernel (mg_step). Both give the
-    same doubles bit for bit. Batches belong in MergeVecEnv, which is GPU-only.
+    same doubles bit for bit on every state a live episode reaches; past about 2,875 m (|theta| >=
+    1/16, cars driving on long after the end point) sin / cos come from glibc on the host and from
+    the device library on the GPU, and the observation may differ there by an ulp (positions,
+    speeds, rewards and flags stay equal; tests/test_host_step.py). Batches belong in MergeVecEnv,
+    which is GPU-only.
     """
 
     def __init__(self, device=None, zero_copy: bool = True, backend: str | None = None):

@@ -24,6 +24,8 @@ return `infos` as N per-env dicts with the last observation of a finished env in
 of later gym versions' batched infos), so no host loop over N envs runs per step; the terminal
 observations are also under `info["terminal_observation"]` (the same [N,10] tensor). Observations,
 rewards and dones are device tensors, and `step` takes both players' action arrays.
+`gym_vector()` gives the gym 0.20 protocol itself (step_async / step_wait, numpy outputs, per-env
+infos; envs/gym_vector.py) for callers written against it.
 """
 
 from __future__ import annotations
@@ -452,6 +454,14 @@ class MergeVecEnv:
         if goal_memory:
             out.update(ext_reward=hb["ext_reward"], no_break=hb["no_break"])
         return out
+
+    def gym_vector(self, obs_dtype=None):
+        """gym 0.20's VectorEnv protocol over this env (envs/gym_vector.py): step_async / step_wait,
+        numpy outputs and per-env infos with "terminal_observation". The device-tensor API above stays
+        the fast path."""
+        from .gym_vector import GymVectorEnv
+
+        return GymVectorEnv(self, obs_dtype)
 
     def observe(self):
         """Observation of the current state without stepping (merging_env.py:118-132)."""

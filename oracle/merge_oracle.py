@@ -436,6 +436,79 @@ def qnet_reference(weights, obs, bf16: bool = True, swap: bool = False):
     return h.numpy()
 
 
+def _bf16(a):
+    """fp32 -> bf16 (round to nearest even) -> back, as v_cvt_pk_bf16_f32 / static_cast<__bf16>."""
+    import torch
+
+    return torch.as_tensor(np.asarray(a, np.float32)).to(torch.bfloat16).to(torch.float32).numpy()
+
+
+def _bias_parts(b):
+    """merging_hip.hip qnet_pack_kernel's three-way split b = hi + mid + lo of an fp32 bias into bf16
+    parts (the padded K slots whose input is 1.0)."""
+    b = np.asarray(b, np.float32)
+    hi = _bf16(b)
+    r = (b - hi).astype(np.float32)
+    mid = _bf16(r)
+    lo = _bf16((r - mid).astype(np.float32))
+    return hi, mid, lo
+
+
+def qnet_reference_blocked(weights, x, swap: bool = False, block: int = 32):
+    """The Net forward as the kernels' MFMAs compute it (round 5; tests/test_gpu_qnet.py pins it bit
+    for bit to mg_qnet_forward): bf16 operands, fp32 accumulators, and each MFMA adding the EXACT sum
+    of its K products to the accumulator with ONE rounding to fp32. The K blocks follow the packed
+    layout (merging_hip.hip qfrag / qnet_unit1 / qnet_unit2; the order within a block does not matter
+    for an exact sum):
+      layer 1   one 32x32x16 MFMA over the 16 input slots: features 0..in-1, b1's three bf16 parts at
+                slots 13..15 (inputs 1.0);
+      layer 2   hidden-1 units in blocks of `block` (32: the 16x16x32 forward of the net-opponent and
+                h-DQN kernels and mg_qnet_forward; 16: the 32x32x16 forward of config 5 without a net
+                opponent), b2's parts at units 200..202 (outputs 1.0), accumulated block by block from 0;
+      layer 3   hidden-2 units likewise, b3's parts at units 100..102.
+    ReLU after the bf16 rounding of each hidden accumulator (v_cvt_pk_bf16_f32 then max_i16(., 0)).
+    Exact sums in long double (64-bit significand: products of bf16 pairs carry 16 bits, so a block
+    is exact unless its terms span > 2^40 in magnitude). x: [n, in] fp32 (10 or 11 features);
+    swap feeds x[5:] + x[:5] (in 10 only). Returns q [n, out] fp32."""
+    x = np.asarray(x, np.float32)
+    if swap:
+        x = np.concatenate([x[:, 5:], x[:, :5]], axis=1)
+    n, din = x.shape
+    ld = np.longdouble
+    w1, w2, w3 = (np.asarray(weights[k], np.float32) for k in ("fc1.weight", "fc2.weight", "out.weight"))
+    b1, b2, b3 = (np.asarray(weights[k], np.float32) for k in ("fc1.bias", "fc2.bias", "out.bias"))
+
+    def matrix(w, b, kin, kpad, ones_at):
+        # [out, kpad] bf16 values as long double: weights, then the bias parts in slots ones_at..+2
+        m = np.zeros((w.shape[0], kpad), ld)
+        m[:, :kin] = _bf16(w).astype(ld)
+        for j, part in enumerate(_bias_parts(b)):
+            m[:, ones_at + j] = part.astype(ld)
+        return m
+
+    def layer(h, m, blk):
+        acc = np.zeros((h.shape[0], m.shape[0]), np.float32)
+        for k0 in range(0, m.shape[1], blk):
+            s = h[:, k0:k0 + blk].astype(ld) @ m[:, k0:k0 + blk].T  # exact: see the docstring
+            acc = (acc.astype(ld) + s).astype(np.float32)
+        return acc
+
+    def hidden(acc, width, ones_at):
+        h = np.zeros((acc.shape[0], width), np.float32)
+        h[:, :acc.shape[1]] = np.maximum(_bf16(acc), 0.0)  # -0.0 -> +0.0 as max_i16
+        h[:, ones_at:ones_at + 3] = 1.0
+        return h
+
+    xin = np.zeros((n, 16), np.float32)
+    xin[:, :din] = _bf16(x)
+    xin[:, 13:16] = 1.0
+    a1 = layer(xin, matrix(w1, b1, din, 16, 13), 16)
+    h1 = hidden(a1, 224, 200)
+    a2 = layer(h1, matrix(w2, b2, 200, 224, 200), block)
+    h2 = hidden(a2, 128, 100)
+    return layer(h2, matrix(w3, b3, 100, 128, 100), block)
+
+
 def qnet_policy_draws(words, step, opponent):
     """The epsilon-greedy draws of mg_rollout_qnet at global step `step` (merging_hip.hip
     qnet_policy_step_n, ABI 20), restated: words(c) -> [n, 4] uint32 Philox4x32-10 words of counter

@@ -15,6 +15,8 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LINES = sorted(glob.glob(os.path.join(ROOT, "profiles", "r04", "bench_default_r04*.json")) +
                glob.glob(os.path.join(ROOT, "profiles", "r04", "bench_k20_r04*.json")))
+# round 5: the compact last line (bench.compact_line), incl. the multi-rank rehearsals
+LINES5 = sorted(glob.glob(os.path.join(ROOT, "profiles", "r05", "bench_*.json")))
 
 TOP = {"metric": str, "value": float, "unit": str, "n_gpus": int, "steps": int, "warmup": int,
        "ms_per_step": float, "higher_is_better": bool, "scaling": str, "dtype": str, "data": str,
@@ -71,3 +73,96 @@ def test_rocprof_step_kernel_average_agrees_with_the_bench_line(path):
     step = [x for x in rows if x["kernel"] == r["kernel"] and x["grid_threads"] == d["config"]["envs_per_gpu"]]
     assert step, (r["kernel"], [x["kernel"] for x in rows])
     assert abs(step[0]["avg_us"] / (r["kernel_ms_mean"] * 1e3) - 1) < 0.05
+
+
+def check_line(d):
+    """The round-5 contract of a bench line at any world size: the driver's keys, the rank count the
+    process group reported, the roofline with its all-rank aggregate, and -- at every world size
+    (north_star: the reference-style step on the box's host cores in the same run) -- the CPU
+    baseline with its core count."""
+    for k, t in TOP.items():
+        assert k in d, k
+        assert isinstance(d[k], (int, float) if t is float else t), (k, type(d[k]))
+    n = d["n_gpus"]
+    assert n >= 1 and d["dist"]["world_size"] == n, d.get("dist")
+    if n > 1:
+        assert d["dist"]["backend"] in ("nccl", "gloo"), d["dist"]
+    r = d["roofline"]
+    for k in ("achieved", "peak", "frac", "kernel_ms_mean_max_rank", "achieved_aggregate", "frac_aggregate"):
+        assert isinstance(r.get(k), (int, float)), k
+    per_launch = r["bytes_per_env_step"] * d["config"]["envs_per_gpu"]
+    assert math.isclose(r["achieved_aggregate"], n * per_launch / (r["kernel_ms_mean_max_rank"] * 1e-3) / 1e9,
+                        rel_tol=1e-6)
+    assert math.isclose(d["value"], d["config"]["global_envs"] / (d["ms_per_step"] * 1e-3), rel_tol=1e-6)
+    c = d.get("cpu_baseline")
+    assert c is not None, "no cpu_baseline"
+    assert c["kind"] in ("port", "reference") and c["cores"] >= 1 and c["value"] > 0 and c["sample"]
+
+
+def _synthetic(n, with_cpu=True):
+    ms = 0.03
+    line = {"metric": "m", "value": n * (1 << 20) / (ms * 1e-3), "unit": "env-steps/s", "n_gpus": n, "steps": 20,
+            "warmup": 5, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f64", "data": "synthetic", "dist": {"backend": "nccl" if n > 1 else None, "world_size": n},
+            "config": {"workload": "w", "envs_per_gpu": 1 << 20, "global_envs": n << 20},
+            "roofline": {"bound": "hbm", "achieved": 6000.0, "peak": 8000.0, "unit": "GB/s", "frac": 0.75,
+                         "bytes_per_env_step": 152, "kernel_ms_mean": 0.026, "kernel_ms_mean_max_rank": 0.027}}
+    r = line["roofline"]
+    r["achieved_aggregate"] = n * 152 * (1 << 20) / (0.027e-3) / 1e9
+    r["frac_aggregate"] = r["achieved_aggregate"] / (n * 8000.0)
+    if with_cpu:
+        line["cpu_baseline"] = {"value": 1.6e8, "unit": "env-steps/s", "cores": 16, "kind": "port", "sample": "s"}
+    return line
+
+
+def test_multi_rank_line_without_cpu_baseline_is_rejected():
+    check_line(_synthetic(8))
+    check_line(_synthetic(1))
+    with pytest.raises(AssertionError, match="cpu_baseline"):
+        check_line(_synthetic(8, with_cpu=False))
+    bad = _synthetic(8)
+    bad["dist"]["world_size"] = 1  # n_gpus must be the process group's rank count
+    with pytest.raises(AssertionError):
+        check_line(bad)
+    bad = _synthetic(8)
+    del bad["roofline"]["achieved_aggregate"]
+    with pytest.raises(AssertionError):
+        check_line(bad)
+
+
+@pytest.mark.skipif(not LINES5, reason="no recorded round-5 bench lines")
+@pytest.mark.parametrize("path", LINES5, ids=[os.path.basename(p) for p in LINES5])
+def test_recorded_round5_line(path):
+    with open(path) as f:
+        text = f.read().strip().splitlines()[-1]
+    assert len(text) < 6144, len(text)  # the driver keeps ~8 KB of the output's tail
+    d = json.loads(text)
+    check_line(d)
+    if "legs" in d and d["n_gpus"] == 1:
+        for leg in ("rollout", "replay", "qnet_none", "qnet_self", "qnet_other", "hdqn_L0", "hdqn_self", "hdqn_other"):
+            assert leg in d["legs"], leg
+
+
+def test_compact_line_of_a_full_record_is_small():
+    """bench.compact_line keeps every leg's headline figures under 6 KB, from the largest recorded
+    round-4 record (all legs, VALU blocks and episode details)."""
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    full = json.loads(open(os.path.join(ROOT, "profiles", "r04", "bench_default_r04af.json")).read().strip()
+                      .splitlines()[-1])
+    full.setdefault("dist", {"backend": None, "world_size": 1})
+    for leg in full["qnet_policy"]:
+        leg.setdefault("reference_forwards_per_env_step", None)
+    h = full["hdqn_policy"]
+    for key in ("selfplay", "other_checkpoint"):
+        h[key].setdefault("frac_useful", h[key].get("frac_useful_lower_bound"))
+    out = json.dumps(bench.compact_line(full))
+    assert len(out) < 6144, len(out)
+    d = json.loads(out)
+    for leg in ("rollout", "replay", "qnet_none", "qnet_self", "qnet_other", "hdqn_L0", "hdqn_self", "hdqn_other",
+                "size_2p22"):
+        assert leg in d["legs"], leg
+    assert d["roofline"]["frac"] == full["roofline"]["frac"] and d["cpu_baseline"]["cores"] == 16

@@ -227,6 +227,49 @@ def test_host_step_equals_kernel():
     assert hb.flags[:, 2].any() and hb.flags[:, 3].any() and np.isfinite(hb.fobs).any()
 
 
+@pytest.mark.gpu
+def test_host_step_equals_kernel_past_the_polynomial_range():
+    """Far past the end point (|theta| >= 1/16: positions beyond ~2,875 m, reached by cars that keep
+    driving after a finished episode without autoreset) sin / cos leave the shared polynomial: glibc
+    on the host, the device library on the GPU. The state, rewards and flags stay bit-equal (they do
+    not depend on sin / cos there: the cars are far apart), and the observations agree to 1 fp32 ulp
+    (the doubles differ by at most an ulp before the fp32 rounding)."""
+    import torch
+
+    from merging_gym import _native
+
+    n = 1 << 14
+    rng = np.random.default_rng(10)
+    hb = HostBatch(n)
+    hb.s["p1"][:] = rng.uniform(2800, 20000, n)
+    hb.s["p2"][:] = rng.uniform(-3000, 20000, n)
+    hb.s["v1"][:] = rng.uniform(0, 45, n)
+    hb.s["v2"][:] = rng.uniform(0, 45, n)
+    hb.tf[:] = (rng.integers(0, 2600, n) | (rng.integers(0, 3, n) << 13)).astype(np.uint16)
+    a1 = rng.integers(0, 5, n).astype(np.int8)
+    a2 = rng.integers(-1, 5, n).astype(np.int8)
+    dev = {k: torch.from_numpy(v.copy()).cuda() for k, v in hb.s.items()}
+    dtf = torch.from_numpy(hb.tf.view(np.int16).copy()).cuda()
+    d = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    dstate = _native.State(*(d(dev[k]) for k in ("p1", "v1", "p2", "v2", "ret1", "ret2")), d(dtf))
+    dobs = torch.zeros((n, 10), dtype=torch.float32, device="cuda")
+    drew = torch.zeros((n, 2), dtype=torch.float32, device="cuda")
+    dflags = torch.zeros((n, 4), dtype=torch.uint8, device="cuda")
+    dout = _native.Outputs(d(dobs), d(drew), None, None, None, None, None, None, None, d(dflags))
+    da1, da2 = torch.from_numpy(a1).cuda(), torch.from_numpy(a2).cuda()
+    rc = _native.lib.mg_step(ctypes.byref(hb.params), ctypes.byref(dstate), d(da1), d(da2), ctypes.byref(dout),
+                             None, n, 0, None)
+    _native.check(rc, "mg_step")
+    torch.cuda.synchronize()
+    hb.step(a1, a2, autoreset=False, stats=False)
+    for k in hb.s:
+        np.testing.assert_array_equal(dev[k].cpu().numpy().view(np.uint64), hb.s[k].view(np.uint64), err_msg=k)
+    np.testing.assert_array_equal(dtf.cpu().numpy().view(np.uint16), hb.tf)
+    np.testing.assert_array_equal(dflags.cpu().numpy(), hb.flags)
+    np.testing.assert_array_equal(drew.cpu().numpy().view(np.uint32), hb.rew.view(np.uint32))
+    np.testing.assert_array_max_ulp(dobs.cpu().numpy(), hb.obs, maxulp=1)
+
+
 def test_host_collision_test_over_the_whole_plane(coracle):
     """The step's collision test takes integer lateral edges where they equal the fp64 ones (y >= 8,
     merging_hip.hip vehicles_collide) and the fp64 form elsewhere. Pairs of cars placed over the
