@@ -54,7 +54,8 @@ def test_recorded_bench_line_keeps_the_contract(path):
         assert c["kind"] in ("port", "reference") and c["cores"] >= 1 and c["value"] > 0 and c["sample"]
 
 
-GRIDS = sorted(glob.glob(os.path.join(ROOT, "profiles", "r04", "kernel_stats_by_grid_r04*.json")))
+GRIDS = sorted(glob.glob(os.path.join(ROOT, "profiles", "r04", "kernel_stats_by_grid_r04*.json")) +
+               glob.glob(os.path.join(ROOT, "profiles", "r05", "kernel_stats_by_grid_r05*.json")))
 
 
 @pytest.mark.skipif(not GRIDS, reason="no recorded rocprofv3 summaries")
@@ -63,7 +64,9 @@ def test_rocprof_step_kernel_average_agrees_with_the_bench_line(path):
     """The committed rocprofv3 summary of a pass and that pass's bench line time the same kernel:
     the step kernel's average at the 2^20 grid agrees with roofline.kernel_ms_mean within 5 %."""
     tag = os.path.basename(path)[len("kernel_stats_by_grid_"):-len(".json")]
-    bench = os.path.join(ROOT, "profiles", "r04", f"bench_default_{tag}.json")
+    rnd = os.path.basename(os.path.dirname(path))
+    # round 4: the default bench line of the same pass; round 5: the profiled run's own line
+    bench = os.path.join(ROOT, "profiles", rnd, f"bench_default_{tag}.json" if rnd == "r04" else f"prof_bench_{tag}.json")
     if not os.path.exists(bench):
         pytest.skip(f"no bench line for {tag}")
     d = _load(bench)

@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 
 import merge_oracle as mo
-from choice_check import ChoiceCheck, check_q_eval
+from choice_check import ChoiceCheck, check_q_eval, order_matched_q
 
 pytestmark = pytest.mark.gpu
 
@@ -196,6 +196,7 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
     envs = mo.oracle_envs_from(coracle, env)
     stats = (env.returns.cpu().numpy().copy(), env.counts.cpu().numpy().astype(np.uint32))
     qe, qe_abs = env.q_eval.cpu().numpy().copy(), np.zeros(n)  # hdqn.py:330's q_eval per episode
+    qe_pin = qe.copy()  # the same sums of the kernel-order Q-values (choice_check.order_matched_q)
     obs = env.observe().cpu().numpy().copy()
     obs64 = coracle.observe(envs)  # the fp64 state goal_status reads
     kind = _kind(opponent)
@@ -290,6 +291,8 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
             qg = q2[np.arange(n), g2]
             qe += np.where(d, qg, 0.0)
             qe_abs += np.where(d, np.abs(q2).max(1), 0.0)
+            if d.any():
+                qe_pin += np.where(d, order_matched_q(meta, meta_sd, s2, "16x16")[np.arange(n), g2], 0.0)
             # :314 on the state acted on and :322 on the next state, in fp64 as the reference
             np.testing.assert_array_equal(g["reward"][t], (g2 == _status(obs64)).astype(np.float32))
             # the goal of the next step: kept, or fresh once reached / after an episode end
@@ -351,7 +354,7 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
     # the episode statistics the launch's finishing envs recorded (both scripts' logged values)
     np.testing.assert_array_equal(env.returns.cpu().numpy(), stats[0])
     np.testing.assert_array_equal(env.counts.cpu().numpy().astype(np.uint32), stats[1])
-    check_q_eval(env.q_eval.cpu().numpy(), qe, qe_abs, f"fused h-DQN {opponent} n={n}")
+    check_q_eval(env.q_eval.cpu().numpy(), qe, qe_abs, f"fused h-DQN {opponent} n={n}", pinned=qe_pin)
     cc_a.finish()
     cc_g.finish()
     if selfplay:
@@ -395,6 +398,7 @@ def test_fused_hdqn_rollout_full_size(coracle, nets):
     envs = mo.oracle_envs_from(coracle, env, idx)
     stats = (env.returns[idx].cpu().numpy().copy(), env.counts[idx].cpu().numpy().astype(np.uint32))
     qe, qe_abs = env.q_eval[idx].cpu().numpy().copy(), np.zeros(len(idx_np))
+    qe_pin = qe.copy()
     obs = env.observe()[idx].cpu().numpy().copy()
     obs64 = coracle.observe(envs)
     reset_goal = meta.reset_argmax()
@@ -442,6 +446,8 @@ def test_fused_hdqn_rollout_full_size(coracle, nets):
         qg = q2[np.arange(len(idx_np)), g2]  # hdqn.py:330
         qe += np.where(d, qg, 0.0)
         qe_abs += np.where(d, np.abs(q2).max(1), 0.0)
+        if d.any():
+            qe_pin += np.where(d, order_matched_q(meta, meta_sd, s2, "16x16")[np.arange(len(idx_np)), g2], 0.0)
         np.testing.assert_array_equal(sub["reward"][t], (g2 == _status(obs64)).astype(np.float32))
         brk = d | (g2 == _status(s2_64))
         gf = ubx < thr
@@ -455,7 +461,7 @@ def test_fused_hdqn_rollout_full_size(coracle, nets):
         np.testing.assert_array_equal(src[idx].cpu().numpy(), envs[name], err_msg=name)
     np.testing.assert_array_equal(env.returns[idx].cpu().numpy(), stats[0])
     np.testing.assert_array_equal(env.counts[idx].cpu().numpy().astype(np.uint32), stats[1])
-    check_q_eval(env.q_eval[idx].cpu().numpy(), qe, qe_abs, f"full-size h-DQN ({nets})")
+    check_q_eval(env.q_eval[idx].cpu().numpy(), qe, qe_abs, f"full-size h-DQN ({nets})", pinned=qe_pin)
     # main.py's pending value where the ego has arrived first: what the next launch reads back
     # (the no-wait statistics load it only for those envs, pend_load)
     w1 = envs["winner"] == 1

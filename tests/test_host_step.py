@@ -261,7 +261,7 @@ def test_host_step_equals_kernel_past_the_polynomial_range():
                              None, n, 0, None)
     _native.check(rc, "mg_step")
     torch.cuda.synchronize()
-    hb.step(a1, a2, autoreset=False, stats=False)
+    hb.step(a1, a2, autoreset=False)
     for k in hb.s:
         np.testing.assert_array_equal(dev[k].cpu().numpy().view(np.uint64), hb.s[k].view(np.uint64), err_msg=k)
     np.testing.assert_array_equal(dtf.cpu().numpy().view(np.uint16), hb.tf)
