@@ -3208,7 +3208,7 @@ void mpc_qp_constants(double t, double* nz_out, double* z0_out, double* vsmall_o
 
 // ============================================================================ statistics reduction
 // The per-env 64-byte records (mg_episode_stats) summed to one mg_stats_totals in a FIXED order, so
-// the fp64 sums are reproducible bit for bit (oracle/merge_numpy.py stats_reduce restates it):
+// the fp64 sums are reproducible bit for bit (oracle/merge_oracle.py stats_reduce_fixed restates it):
 //   pass 1 (block b of kRedThreads threads, kRedEnvs envs): thread t adds the records of envs
 //          b kRedEnvs + j kRedThreads + t, j = 0..kRedPer-1, in j order onto -0.0 (the additive
 //          identity), then the block folds its kRedThreads values in halves (v[t] += v[t + o],

@@ -348,6 +348,37 @@ def test_rollout_equals_step_sequence(torch, n, T):
     assert b._step_idx == 180 + T
 
 
+def test_rollout_longer_than_one_launch_is_chunked_bit_exactly(torch):
+    """rollout_random splits a rollout longer than mg_rollout_random's 65,535-step limit into
+    consecutive launches that write slices of the same buffers (_traj_slice's row strides). T =
+    65,535 + 37 steps of 96 envs against the same steps as one-step launches: the rows around the
+    chunk boundary (obs, flags, final observations, won bits, rewards), the final state and the
+    statistics records bit for bit."""
+    from merging_gym import MergeVecEnv
+
+    n, T, seed, k0 = 96, 65535 + 37, 91, 120
+    a = MergeVecEnv(n, device="cuda:0", won_mask=True)
+    b = MergeVecEnv(n, device="cuda:0")
+    for k in range(k0):
+        a.step_random(seed, step_idx=k)
+        b.step_random(seed, step_idx=k)
+    traj = b.rollout_random(T, seed, first_step=k0)
+    torch.cuda.synchronize()
+    check = set(range(65530, T)) | {0, 1}
+    for t in range(T):
+        obs, rew, done, info = a.step_random(seed, step_idx=k0 + t)
+        if t in check:
+            assert torch.equal(traj["obs"][t], obs), t
+            assert torch.equal(traj["rew"][t], rew), t
+            assert torch.equal(traj["done"][t], done) and torch.equal(traj["collision"][t], info["collision"]), t
+            assert torch.equal(traj["a1"][t], a.a1_buf) and torch.equal(traj["a2"][t], a.a2_buf), t
+            assert torch.equal(traj["final_observation"][t][done], info["final_observation"][done]), t
+            assert torch.equal(traj["won_mask"][t], a.won_mask), t
+    for name in ("p1", "v1", "p2", "v2", "ret1", "ret2", "tf", "returns", "counts", "_ep_stats"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+    assert b._step_idx == k0 + T and int(b.counts[:, 0].sum()) > 20000  # ~300 episodes per env
+
+
 def test_config4_size_and_64bit_env_index(torch, coracle):
     """Config 4's global batch (2^23 envs) stepped on one GPU: step-count bookkeeping over the
     whole batch and oracle replays at both ends of the index range; then a small shard whose
