@@ -1895,7 +1895,22 @@ __device__ __forceinline__ uint8_t qnet_need_bits(const QRollout& R, const uint4
   if (!live) return 0;
   const bool fin = R.St.rec != nullptr && (R.flags & MG_AUTORESET) && may_finish_next(R.P, e, o, R.fin);
   return static_cast<uint8_t>(((static_cast<uint64_t>(u.x) < R.greedy_thr || fin) ? 1 : 0) |
-                              (static_cast<uint64_t>(u.z) < R.opp_greedy_thr ? 2 : 0));
+                              (static_cast<uint64_t>(u.z) < R.opp_greedy_thr ? 2 : 0) | (fin ? 4 : 0));
+}
+
+// Where the Q-net waves find them: OPP 2 reads both bits from greedy[1][j]; OPP 3 (round 5, the
+// waves split by net) gives each net's waves a byte of their own -- greedy[0][j] the ego's (bit 0
+// need, bit 1 may finish), greedy[1][j] the opponent's (bit 0 its greedy draw, bit 1 may finish) --
+// which those waves then overwrite with the greedy actions, so no byte is shared between waves.
+template <int OPP>
+__device__ __forceinline__ void qnet_put_need(uint8_t* g0, uint8_t* g1, uint8_t b) {
+  if constexpr (OPP == 3) {
+    const uint8_t fin = static_cast<uint8_t>((b >> 1) & 2);
+    *g0 = static_cast<uint8_t>((b & 1) | fin);
+    *g1 = static_cast<uint8_t>(((b >> 1) & 1) | fin);
+  } else {
+    *g1 = b;
+  }
 }
 
 __device__ __forceinline__ uint4 qnet_draws(const QRollout& R, int64_t i, uint64_t step) {
@@ -1924,7 +1939,8 @@ __device__ __forceinline__ void qnet_policy_step_n(const QRollout& R, Env (&e)[N
                                                    int64_t i0, const bool (&live)[N], int t,
                                                    const int (&greedy1)[N], const int (&greedy2)[N],
                                                    bool (&won)[N], const float* qrow, uint2 (&keep)[N],
-                                                   double (&pend)[N], uint4 (&un)[N], uint8_t* need) {
+                                                   double (&pend)[N], uint4 (&un)[N], uint8_t* need0,
+                                                   uint8_t* need1) {
   const uint64_t step = R.first_step + t;
   int a1[N], a2[N];
 #pragma unroll
@@ -1983,7 +1999,7 @@ __device__ __forceinline__ void qnet_policy_step_n(const QRollout& R, Env (&e)[N
 #pragma unroll
       for (int j = 0; j < N; ++j) {
         un[j] = qnet_draws(R, i0 + 64 * j, step + 1);
-        need[64 * j] = qnet_need_bits(R, un[j], live[j], e[j], r[j].o);
+        qnet_put_need<OPP>(need0 + 64 * j, need1 + 64 * j, qnet_need_bits(R, un[j], live[j], e[j], r[j].o));
       }
     }
   }
@@ -2028,6 +2044,21 @@ __device__ __forceinline__ bool qnet_load_env(const QRollout& R, int64_t i, Env&
 // keeps a second net in LDS: with the 16x16 layouts (2 x 59,392 B, ABI 19) the two nets, the
 // 1,024-env tile and the greedy bytes take 161,792 B, so it runs ILP 2 like the others (the
 // 32x32 layouts, 2 x 60,496 B, did not fit and ran ILP 1 on 512-env blocks: 1 % slower).
+// The items a Q-net wave runs itself out of a list of n (round 5): all of them, or 192 (three full
+// forwards) when 1..16 remain past those, which then run on the env wave of the same index.
+__device__ __forceinline__ int qws_own_items(int n) { return n > 192 && n <= 192 + 16 ? 192 : n; }
+__device__ __forceinline__ void qws_publish_tail(int (&qt)[4], int p, int nq, int nn, int nf) {
+  if ((threadIdx.x & 63) == 0) {
+    qt[1] = nq;
+    qt[2] = nn;
+    qt[3] = nf;
+    __hip_atomic_store(&qt[0], p, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+}
+__device__ __forceinline__ void qws_wait(const int* flag, int p) {
+  while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != p) __builtin_amdgcn_s_sleep(1);
+}
+
 template <int OPP>
 constexpr int qws_ilp() { return kQWsIlp; }
 template <int OPP>
@@ -2057,6 +2088,15 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
   // OPP 2: each listed item's layer-1 B fragment halves (the view it needs), staged by the env's own
   // lane, so one forward can hold both views' items (one net) and reads its inputs lane-linearly
   __shared__ __attribute__((aligned(16))) u32x4 qstage[OPP == 2 ? 4 : 1][OPP == 2 ? 256 : 1][2];
+  // OPP 3: phase p once opponent wave h has read every tile row an ego wave will overwrite with
+  // Q-values (the may-finish rows, which it lists first)
+  __shared__ int qrows_read[2];
+  // OPP 2 / 3: a Q-net wave's list tail -- its items past three full forwards, when at most 16 -- runs
+  // on env wave w (the same index) after that wave's step, so the Q-net waves' phase ends after three
+  // forwards instead of three and a narrow fourth (whose weight stream costs half a full one). Wave w
+  // publishes {phase, items it runs, list length, may-finish items} once its list (and OPP 2's staged
+  // fragments) are in LDS; the phase word last, with release order.
+  __shared__ int qtail[OPP >= 2 ? 4 : 1][4];
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int64_t base = static_cast<int64_t>(blockIdx.x) * kEnvs;
@@ -2070,6 +2110,8 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
     qnet_to_lds(R.net, lds_net);
   }
   if constexpr (OPP == 3) qnet_to_lds(R.opp_net, lds_net2);
+  if (tid < 2) qrows_read[tid] = -1;
+  if (OPP >= 2 && tid < 4) qtail[tid][0] = -1;
   const int phases = 2 * R.num_steps + 1;
   if (qwave) {
     // Q-net waves: the barrier count matches the env waves' loop below, phase for phase
@@ -2077,7 +2119,94 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
     // registers apart -- in one loop the env state sat beside the accumulators and spilled)
     __syncthreads();
     for (int p = 0; p < phases; ++p) {
-      if constexpr (OPP >= 2) {
+      if constexpr (OPP == 3) {
+        // Only the forwards the reference evaluates (round 5; OPP 2 below for the common part), with
+        // the waves split by net: waves 0-1 run the opponent's net, 2-3 the ego's, each over 256 of
+        // the group's 512 envs (rows rb + e). One net per wave keeps the view uniform and gives each
+        // wave ~194 items = three full 64-item forwards and a narrow one; split by env instead, each
+        // wave ran both nets on ~97 items apiece (two forwards per net, the second three tiles wide).
+        // An ego wave writes eval_net(state)[0..4] into the tile rows of its may-finish items only (an
+        // episode can end only there, main.py:221) and only once the opponent wave of the same rows
+        // has read them: that wave lists those items first and publishes the phase in
+        // qrows_read[hw] after their forward; the ego wave lists them last.
+        if (p < 2 * R.num_steps) {
+          static_assert(kHalf == 512, "two waves per net, 256 envs each");
+          const bool oppw = wave < 2;
+          const int hw = wave & 1;
+          const int rb = (p & 1) * kHalf + 256 * hw;
+          uint8_t* gout = greedy[oppw ? 1 : 0] + rb;
+          uint8_t* list = qlist[wave];
+          uint64_t mn[4], mf[4];
+          int nn = 0, nf = 0;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int nb = gout[64 * k + lane];
+            mn[k] = __ballot(nb & 1);
+            mf[k] = __ballot((nb & 3) == 3);
+            nn += __popcll(mn[k]);
+            nf += __popcll(mf[k]);
+          }
+          int of = oppw ? 0 : nn - nf, on = oppw ? nf : 0;  // may-finish items first / last
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint64_t mo = mn[k] & ~mf[k];
+            if ((mf[k] >> lane) & 1)
+              list[of + lane_rank(mf[k])] = static_cast<uint8_t>(64 * k + lane);
+            else if ((mo >> lane) & 1)
+              list[on + lane_rank(mo)] = static_cast<uint8_t>(64 * k + lane);
+            of += __popcll(mf[k]);
+            on += __popcll(mo);
+          }
+          wave_lds_sync();
+          const int nq = qws_own_items(nn);
+          qws_publish_tail(qtail[wave], p, nq, nn, nf);
+          if (oppw && nf == 0 && lane == 0) __hip_atomic_store(&qrows_read[hw], p, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          const int fin0 = nn - nf;  // an ego wave's first may-finish item
+          const int r = lane & 31, h = lane >> 5;
+          const uint8_t* net = oppw ? lds_net2 : lds_net;
+          // the tile rows of a chunk's items (column envs r and 32 + r, and this lane's result row),
+          // read one chunk ahead: a forward's inputs then wait for one LDS read, not two
+          auto rows_of = [&](int c, int& ra, int& rc, int& ro) __attribute__((always_inline)) {
+            const int n = nn - c < 64 ? nn - c : 64;
+            ra = rb + list[c + (r < n ? r : 0)];
+            rc = rb + list[c + (32 + r < n ? 32 + r : 0)];
+            ro = rb + list[c + (lane < n ? lane : 0)];
+          };
+          int ra, rc, row;
+          rows_of(0, ra, rc, row);
+#pragma unroll 1
+          for (int c0 = 0; c0 < nq;) {
+            const int cnt = nq - c0 < 64 ? nq - c0 : 64;
+            auto input = [&](int j) __attribute__((always_inline)) {
+              const float* rw = tile + j * kObs;
+              return oppw ? qnet_input(rw, true, h) : qnet_input(rw, false, h);
+            };
+            const bf16x8 x0 = input(ra), x1 = input(rc);
+            const int rcur = row;
+            if (c0 + cnt < nq) rows_of(c0 + cnt, ra, rc, row);
+            float q[8];
+            qnet_mlp_swp_nc(net, x0, x1, q, col_tiles(cnt));
+            if (lane < cnt) gout[rcur - rb] = static_cast<uint8_t>(argmax_first(q, R.out_dim));
+            if (oppw) {  // (nf > nq: the env wave running the tail publishes it)
+              if (c0 < nf && c0 + cnt >= nf && lane == 0)  // the forward has consumed its rows
+                __hip_atomic_store(&qrows_read[hw], p, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else if (c0 + cnt > fin0) {
+              qws_wait(&qrows_read[hw], p);
+              if (lane < cnt && c0 + lane >= fin0) {
+                float* qr = tile + rcur * kObs;
+                reinterpret_cast<f32x2*>(qr)[0] = f32x2{q[0], q[1]};
+                reinterpret_cast<f32x2*>(qr)[1] = f32x2{q[2], q[3]};
+                qr[4] = q[4];
+              }
+            }
+            wave_lds_sync();
+            c0 += cnt;
+          }
+        }
+        __syncthreads();
+        continue;
+      }
+      if constexpr (OPP == 2) {
         // Only the forwards the reference evaluates (round 5): choose_action runs the net on its
         // greedy branch only (main.py:105-107), and :221 evaluates it on an episode's last step.
         // The wave's 128 envs of the group are compacted by their need bits into one list, the
@@ -2098,7 +2227,7 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
           if (nb1 & 2) list[Lo0 + lane_rank(mo1)] = static_cast<uint8_t>(0x80 | 64 | lane);
           if (nb0 & 1) list[Lo + lane_rank(me0)] = static_cast<uint8_t>(lane);
           if (nb1 & 1) list[Lo + Le0 + lane_rank(me1)] = static_cast<uint8_t>(64 | lane);
-          if constexpr (OPP == 2) {
+          {
             // the same net for both views: stage every item's fragments from its env's lane (both
             // views of the row from one read), then run the whole list 64 items per forward
             auto stage = [&](int row, int nb, int po, int pe) __attribute__((always_inline)) {
@@ -2123,24 +2252,20 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
             stage(row_of(64 + lane), nb1, Lo0 + lane_rank(mo1), Lo + Le0 + lane_rank(me1));
           }
           wave_lds_sync();
+          const int nq = qws_own_items(Ln);
+          qws_publish_tail(qtail[wave], p, nq, Ln, 0);
           const int r = lane & 31, h = lane >> 5;
 #pragma unroll 1
-          for (int c0 = 0; c0 < Ln;) {
-            // OPP 3: a forward holds one net's items (the opponent's net for the first Lo), built from
-            // the tile rows with the view uniform per forward (a view chosen per lane by selects on
-            // the features cost +35 % per launch, r05f q1 / q2). OPP 2: staged fragments, any mix.
-            const bool opp = c0 < Lo;
-            const int end = (OPP == 3 && opp) ? Lo : Ln;
-            const int cnt = end - c0 < 64 ? end - c0 : 64;
+          for (int c0 = 0; c0 < nq;) {
+            // staged fragments, any mix of views (a view chosen per lane by selects on the features
+            // cost +35 % per launch, r05f q1 / q2)
+            const int cnt = nq - c0 < 64 ? nq - c0 : 64;
             auto input = [&](int it) __attribute__((always_inline)) {
-              if constexpr (OPP == 2)
-                return __builtin_bit_cast(bf16x8, qstage[wave][c0 + (it < cnt ? it : 0)][h]);
-              const float* row = tile + row_of(list[c0 + (it < cnt ? it : 0)]) * kObs;
-              return opp ? qnet_input(row, true, h) : qnet_input(row, false, h);
+              return __builtin_bit_cast(bf16x8, qstage[wave][c0 + (it < cnt ? it : 0)][h]);
             };
             const int e_out = list[c0 + (lane < cnt ? lane : 0)];  // read ahead: its wait hides under the forward
             float q[8];
-            qnet_mlp_swp_nc((OPP == 3 && opp) ? lds_net2 : lds_net, input(r), input(32 + r), q, col_tiles(cnt));
+            qnet_mlp_swp_nc(lds_net, input(r), input(32 + r), q, col_tiles(cnt));
             if (lane < cnt) {
               const int e = e_out;
               const int row = row_of(e);
@@ -2215,8 +2340,8 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
       }
       un0[j] = qnet_draws(R, base + la, R.first_step);
       un1[j] = qnet_draws(R, base + lb, R.first_step);
-      greedy[1][la] = qnet_need_bits(R, un0[j], live0[j], e0[j], o0);
-      greedy[1][lb] = qnet_need_bits(R, un1[j], live1[j], e1[j], o1);
+      qnet_put_need<OPP>(&greedy[0][la], &greedy[1][la], qnet_need_bits(R, un0[j], live0[j], e0[j], o0));
+      qnet_put_need<OPP>(&greedy[0][lb], &greedy[1][lb], qnet_need_bits(R, un1[j], live1[j], e1[j], o1));
     }
 #pragma unroll
     for (int k = 0; k < kObs; ++k) r[j].o[k] = 0.0;
@@ -2235,13 +2360,14 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
       bool won[kIlp];
       // wave-uniform branch: each group's envs stay in named registers
       const float* qrow = tile + (local0 + lane) * kObs;
-      uint8_t* need = &greedy[1][local0 + lane];
+      uint8_t* need0 = &greedy[0][local0 + lane];
+      uint8_t* need1 = &greedy[1][local0 + lane];
       if (g == 0)
         qnet_policy_step_n<OPP, kIlp, CHECKED>(R, e0, r, base + local0 + lane, live0, t, greedy1, greedy2, won, qrow,
-                                               keep0, pend0, un0, need);
+                                               keep0, pend0, un0, need0, need1);
       else
         qnet_policy_step_n<OPP, kIlp, CHECKED>(R, e1, r, base + local0 + lane, live1, t, greedy1, greedy2, won, qrow,
-                                               keep1, pend1, un1, need);
+                                               keep1, pend1, un1, need0, need1);
       const int64_t wbase = base + local0;
 #pragma unroll
       for (int j = 0; j < kIlp; ++j) {
@@ -2254,6 +2380,58 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
       wave_store_obs_n<kIlp>(tile + local0 * kObs, r,
                              R.T.obs ? R.T.obs + (static_cast<int64_t>(t) * R.n + wbase) * kObs : nullptr,
                              wrows);
+    }
+    if constexpr (OPP >= 2) {
+      // Q-net wave ew's list tail for Q(group p & 1, step p / 2), as that wave would run it (qtail)
+      if (p < 2 * R.num_steps) {
+        qws_wait(&qtail[ew][0], p);
+        const int nq = qtail[ew][1], nn = qtail[ew][2];
+        if (nn > nq) {
+          const int cnt = nn - nq;  // 1..16: one column tile
+          const uint8_t* list = qlist[ew];
+          const int r32 = lane & 31, h = lane >> 5;
+          const int it = nq + (r32 < cnt ? r32 : 0), io = nq + (lane < cnt ? lane : 0);
+          float q[8];
+          if constexpr (OPP == 3) {
+            const bool oppw = ew < 2;
+            const int hw = ew & 1, nf = qtail[ew][3];
+            const int rb = (p & 1) * kHalf + 256 * hw;
+            const float* rw = tile + (rb + list[it]) * kObs;
+            const int row = rb + list[io];
+            const bf16x8 x = oppw ? qnet_input(rw, true, h) : qnet_input(rw, false, h);
+            qnet_mlp<2 * kQLdsAhead, 1>(qnet_lds(oppw ? lds_net2 : lds_net), x, x, q);
+            if (lane < cnt) greedy[oppw ? 1 : 0][row] = static_cast<uint8_t>(argmax_first(q, R.out_dim));
+            if (oppw) {
+              if (nf > nq && lane == 0) __hip_atomic_store(&qrows_read[hw], p, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else if (nn - nf < nn) {  // may-finish items, listed last
+              qws_wait(&qrows_read[hw], p);
+              if (lane < cnt && io >= nn - nf) {
+                float* qr = tile + row * kObs;
+                reinterpret_cast<f32x2*>(qr)[0] = f32x2{q[0], q[1]};
+                reinterpret_cast<f32x2*>(qr)[1] = f32x2{q[2], q[3]};
+                qr[4] = q[4];
+              }
+            }
+          } else {
+            const bf16x8 x = __builtin_bit_cast(bf16x8, qstage[ew][it][h]);
+            qnet_mlp<2 * kQLdsAhead, 1>(qnet_lds(lds_net), x, x, q);
+            if (lane < cnt) {
+              const int e = list[io];
+              const int row = (p & 1) * kHalf + (4 * ((e >> 6) & 1) + ew) * 64 + (e & 63);
+              const uint8_t a = static_cast<uint8_t>(argmax_first(q, R.out_dim));
+              if (e & 0x80) {
+                greedy[1][row] = a;
+              } else {
+                greedy[0][row] = a;
+                float* qr = tile + row * kObs;
+                reinterpret_cast<f32x2*>(qr)[0] = f32x2{q[0], q[1]};
+                reinterpret_cast<f32x2*>(qr)[1] = f32x2{q[2], q[3]};
+                qr[4] = q[4];
+              }
+            }
+          }
+        }
+      }
     }
     __syncthreads();
   }
@@ -2402,6 +2580,8 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
   // OPP 2 / 3: the opponent's greedy action, current goal and fresh-goal draw
   constexpr bool kOpNets = OPP >= 2;  // the opponent acts through h-DQN nets
   __shared__ uint8_t b_aop[kOpNets ? kHEnvs : 1], b_gop[kOpNets ? kHEnvs : 1], b_dfo[kOpNets ? kHEnvs : 1];
+  // the opponent meta-net's compacted items per Q-net wave and their goals (round 5)
+  __shared__ uint8_t b_olist[kOpNets ? 4 : 1][64], b_gos[kOpNets ? kHEnvs : 1];
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int64_t base = static_cast<int64_t>(blockIdx.x) * kHEnvs;
@@ -2470,18 +2650,39 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
       if constexpr (kOpNets) {  // upper_op.choose_goal(swapped state) at a new outer iteration (:285)
         const int gop_prev = static_cast<int8_t>(b_gop[j]);
         const bool fresh_op = t > 0 ? brk : gop_prev < 0;
-        int gop_star = 0;
-        if (__ballot(live && fresh_op) != 0) {  // on the state acted on at step t (reset obs after an end)
-          float q[8];
-          const bf16x8 x0 = qnet_input(tile + (row0 + r) * kObs, true, h);
-          const bf16x8 x1 = qnet_input(tile + (row0 + 32 + r) * kObs, true, h);
-          if constexpr (OPP == 3)
-            qnet_mlp<kQGlobalAhead>(qnet_global(R.meta_op), x0, x1, q);  // the opponent's own Goal_DQN (:267)
-          else
-            qnet_mlp_swp(lds_meta, x0, x1, q);
-          gop_star = argmax_first(q, R.num_goals);
-        }
         const int dfo = b_dfo[j];
+        // Only where the reference evaluates it (round 5): at a new outer iteration, on the greedy
+        // branch (:86-92) -- about a quarter of the envs. The wave's items are compacted into one
+        // forward on 32 envs (two column tiles) when they fit, else the full 64; the other passes
+        // run at three quarters or more and stay uncompacted (a forward's weight stream costs as
+        // much as two column tiles, so a narrower pass than two tiles' saving does not pay).
+        const bool need_o = live && fresh_op && dfo == kHGreedy;
+        const uint64_t mo = __ballot(need_o);
+        int gop_star = 0;
+        if (mo != 0) {  // on the state acted on at step t (reset obs after an end)
+          const int L = __popcll(mo);
+          uint8_t* list = b_olist[wave];
+          if (need_o) list[lane_rank(mo)] = static_cast<uint8_t>(lane);
+          wave_lds_sync();
+          const int ea = list[r < L ? r : 0], ec = list[32 + r < L ? 32 + r : 0], eo = list[lane < L ? lane : 0];
+          float q[8];
+          const bf16x8 x0 = qnet_input(tile + (row0 + ea) * kObs, true, h);
+          const bf16x8 x1 = qnet_input(tile + (row0 + ec) * kObs, true, h);
+          if constexpr (OPP == 3) {  // the opponent's own Goal_DQN (:267)
+            if (L <= 32)
+              qnet_mlp<2 * kQGlobalAhead, 2>(qnet_global(R.meta_op), x0, x1, q);
+            else
+              qnet_mlp<kQGlobalAhead>(qnet_global(R.meta_op), x0, x1, q);
+          } else {
+            if (L <= 32)
+              qnet_mlp<2 * kQLdsAhead, 2>(qnet_lds(lds_meta), x0, x1, q);
+            else
+              qnet_mlp_swp(lds_meta, x0, x1, q);
+          }
+          if (lane < L) b_gos[row0 + eo] = static_cast<uint8_t>(argmax_first(q, R.num_goals));
+          wave_lds_sync();
+          gop_star = b_gos[j];  // this env's item where need_o
+        }
         gop_t = fresh_op ? (dfo == kHGreedy ? gop_star : dfo) : gop_prev;
       }
       if (t < T) {

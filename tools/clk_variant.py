@@ -3,7 +3,10 @@ each wave of blocks 0..63 stamps s_memtime at the start of every phase and just 
 closing barrier into a device array that mg_debug_clocks copies out. Applied as text edits to a
 source file (the shipped one or an older one):
 
-    python tools/clk_variant.py SRC OUT.so
+    python tools/clk_variant.py SRC OUT.so [0|1|base|q5|q5base]
+
+(0 / 1 / base: the h-DQN kernel's phases, with the round-5 or round-4 forward marks; q5 / q5base:
+the config-5 kernel's, working tree or round-4 source.)
 """
 import os
 import subprocess
@@ -20,8 +23,94 @@ __device__ unsigned g_mg_clk[64 * 8 * 64 * 16];
   g_mg_clk[((blockIdx.x * 8 + (threadIdx.x >> 6)) * 64 + p) * 16 + (ev)] = static_cast<unsigned>(__builtin_amdgcn_s_memtime()); } while (0)
 extern "C" int mg_debug_clocks(void* dst) { return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_mg_clk), sizeof(g_mg_clk)); }
 '''
-# the round-5 Q-net waves' passes: a mark after each forward (2 + 2 stage + chunk parity) and after
-# each scatter (3 + ...)
+# config-5 (qnet_rollout_ws_kernel): phase marks of both roles, and a mark pair around each forward
+# of the Q-net waves (the k-th forward of a phase: 2 + k before, 8 + k after, k < 6)
+Q5_EDITS = [
+    ("""    __syncthreads();
+    for (int p = 0; p < phases; ++p) {
+      if constexpr (OPP == 3) {""",
+     """    __syncthreads();
+    for (int p = 0; p < phases; ++p) {
+      MG_CLK(0);
+      int fidx = 0;
+      if constexpr (OPP == 3) {"""),
+    ("""        __syncthreads();
+        continue;
+      }""",
+     """        MG_CLK(1);
+        __syncthreads();
+        continue;
+      }""", 2),
+    ("""            qnet_mlp_swp_nc(net, input(r), input(32 + r), q, col_tiles(cnt));""",
+     """            if (fidx < 6) MG_CLK(2 + fidx);
+            qnet_mlp_swp_nc(net, input(r), input(32 + r), q, col_tiles(cnt));
+            asm volatile("" :: "v"(q[0]), "v"(q[1]), "v"(q[2]), "v"(q[4]));
+            if (fidx < 6) MG_CLK(8 + fidx);
+            ++fidx;"""),
+    ("""            qnet_mlp_swp_nc((OPP == 3 && opp) ? lds_net2 : lds_net, input(r), input(32 + r), q, col_tiles(cnt));""",
+     """            if (fidx < 6) MG_CLK(2 + fidx);
+            qnet_mlp_swp_nc((OPP == 3 && opp) ? lds_net2 : lds_net, input(r), input(32 + r), q, col_tiles(cnt));
+            asm volatile("" :: "v"(q[0]), "v"(q[1]), "v"(q[2]), "v"(q[4]));
+            if (fidx < 6) MG_CLK(8 + fidx);
+            ++fidx;"""),
+]
+Q5_BASE_EDITS = [
+    ("""    __syncthreads();
+    for (int p = 0; p < phases; ++p) {
+      if (p < 2 * R.num_steps) {""",
+     """    __syncthreads();
+    for (int p = 0; p < phases; ++p) {
+      MG_CLK(0);
+      if (p < 2 * R.num_steps) {"""),
+    ("""            qnet_forward_swp(OPP == 3 ? lds_net2 : lds_net, tile, row0, true, q);""",
+     """            MG_CLK(2 + 2 * tt);
+            qnet_forward_swp(OPP == 3 ? lds_net2 : lds_net, tile, row0, true, q);
+            asm volatile("" :: "v"(q[0]), "v"(q[1]), "v"(q[2]), "v"(q[4]));
+            MG_CLK(8 + 2 * tt);"""),
+    ("""          else
+            qnet_forward_swp(lds_net, tile, row0, false, q);""",
+     """          else {
+            MG_CLK(3 + 2 * tt);
+            qnet_forward_swp(lds_net, tile, row0, false, q);
+            asm volatile("" :: "v"(q[0]), "v"(q[1]), "v"(q[2]), "v"(q[4]));
+            MG_CLK(9 + 2 * tt);
+          }"""),
+]
+Q5_COMMON = [
+    ("""      __syncthreads();
+    }
+    return;
+  }
+  // env lane:""",
+     """      MG_CLK(1);
+      __syncthreads();
+    }
+    return;
+  }
+  // env lane:"""),
+    ("""  for (int p = 0; p < phases; ++p) {
+    if (p > 0) {
+      const int g = (p - 1) & 1, t = (p - 1) >> 1;
+      const int local0""",
+     """  for (int p = 0; p < phases; ++p) {
+    MG_CLK(0);
+    if (p > 0) {
+      const int g = (p - 1) & 1, t = (p - 1) >> 1;
+      const int local0"""),
+    ("""    __syncthreads();
+  }
+#pragma unroll
+  for (int j = 0; j < kIlp; ++j) {
+    const int la""",
+     """    MG_CLK(1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int j = 0; j < kIlp; ++j) {
+    const int la"""),
+]
+# the round-5 h-DQN Q-net waves' passes (not kept): a mark pair around each forward (2 + 2 stage +
+# chunk parity before, 8 + ... after)
 NEW_EDITS = [
     ("""        if (glob)
           qnet_mlp_nc<kQGlobalAhead>(qnet_global(stage == 1 ? R.meta_op : R.lower_op), x0, x1, q, col_tiles(cnt));
@@ -90,8 +179,11 @@ EDITS = [
 def main(src, out, marks="0"):
     s = open(src).read()
     s = s.replace('#include "merging_hip.h"\n', '#include "merging_hip.h"\n' + HDR, 1)
-    for a, b in EDITS + {"0": [], "1": NEW_EDITS, "base": BASE_EDITS}[marks]:
-        assert s.count(a) == 1, a[:80]
+    sets = {"0": EDITS, "1": EDITS + NEW_EDITS, "base": EDITS + BASE_EDITS,
+            "q5": Q5_COMMON + Q5_EDITS, "q5base": Q5_COMMON + Q5_BASE_EDITS}
+    for e in sets[marks]:
+        a, b, n = e if len(e) == 3 else (*e, 1)
+        assert s.count(a) == n, a[:80]
         s = s.replace(a, b)
     tmp = out + ".hip"
     open(tmp, "w").write(s)
