@@ -2082,8 +2082,9 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
   __shared__ __attribute__((aligned(16))) uint8_t lds_net2[OPP == 3 ? kQNetBytes : 16];
   __shared__ __attribute__((aligned(16))) float tile[kEnvs * kObs];
   __shared__ uint8_t greedy[2][kEnvs];
-  // OPP 2 / 3 (round 5): per Q-net wave the compacted items of a phase (env e of the wave's 128 |
-  // 0x80 the opponent's view); greedy[1][j] holds env j's need bits (qnet_need_bits) when a phase begins
+  // OPP 2 / 3 (round 5): per Q-net wave the compacted items of a phase -- OPP 2: env e of the wave's
+  // 128 | 0x80 the opponent's view; OPP 3: env e of the wave's 256 (one net per wave). When a phase
+  // begins the greedy bytes hold the need bits (qnet_need_bits, qnet_put_need)
   __shared__ uint8_t qlist[OPP >= 2 ? 4 : 1][OPP >= 2 ? 256 : 1];
   // OPP 2: each listed item's layer-1 B fragment halves (the view it needs), staged by the env's own
   // lane, so one forward can hold both views' items (one net) and reads its inputs lane-linearly
