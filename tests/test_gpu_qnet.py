@@ -127,14 +127,20 @@ def test_qnet_forward_hdqn_nets(torch, coracle, in_dim, out_dim):
         qnet.forward(torch.zeros((4, in_dim + 1), device="cuda:0"))
 
 
-@pytest.mark.parametrize("opponent,n", [("none", 4096), ("uniform", 4096), ("self", 4096), ("none", 1000),
-                                        ("uniform", 1001), ("self", 577), ("other", 4096), ("other", 577)])
-def test_rollout_qnet_policy_and_transitions(torch, coracle, nets, opponent, n):
+@pytest.mark.parametrize("opponent,n,sync", [("none", 4096, False), ("uniform", 4096, False), ("self", 4096, False),
+                                             ("none", 1000, False), ("uniform", 1001, False), ("self", 577, False),
+                                             ("other", 4096, False), ("other", 577, False), ("other", 4096, True),
+                                             ("self", 4096, True)])
+def test_rollout_qnet_policy_and_transitions(torch, coracle, nets, opponent, n, sync):
     """Every action is the epsilon-greedy choice (Philox draws exact, greedy = argmax of the
     bf16 reference except near-ties) and every transition equals the CPU oracle's. The odd
     sizes leave partial waves / a partial block and unaligned trajectory rows. "other" is
     main.py's default Strategy_OP "L1" (:161-168): the opponent is another shipped checkpoint
-    (l3) acting on the swapped observation, the kernel instance with both nets in LDS."""
+    (l3) acting on the swapped observation, the kernel instance with both nets in LDS.
+    sync: every env's clock three steps short of the timeout, so that whole waves' items are
+    may-finish ones at once -- the round-5 lists' extremes: an ego wave whose every item writes its
+    Q-values into the tile rows, and opponent lists whose may-finish items reach the tail that the
+    env waves run (they then publish the rows-read flag the ego waves wait for)."""
     from merging_gym import MergeVecEnv
     from merging_gym.policy import QNet, greedy_threshold
 
@@ -143,6 +149,10 @@ def test_rollout_qnet_policy_and_transitions(torch, coracle, nets, opponent, n):
     env = MergeVecEnv(n, device="cuda:0")
     for k in range(200):  # mid-episode start: episodes end inside the window (autoreset, q_eval)
         env.step_random(seed + 1, step_idx=k)
+    if sync:  # the clock's bits of the packed time / flags word (MG_TF_*)
+        m = env._nat.TF_STEPS_MASK
+        env.tf.copy_((env.tf & ~m) | 2498)
+        assert bool((env.steps == 2498).all())
     envs = coracle.new_envs(n)
     for name, src in (("pos1", env.p1), ("vel1", env.v1), ("pos2", env.p2), ("vel2", env.v2),
                       ("r1_acc", env.ret1), ("r2_acc", env.ret2)):
