@@ -2608,37 +2608,46 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
       const int j = row0 + lane;
       const int64_t i = base + j;
       const bool live = i < R.n;
+      // This env's bytes for the phase, read together before the meta forward and held across it
+      // (round 5: read where used, after the forward, each put an LDS round trip on the Q-net
+      // waves' chain -- the goal logic took ~1.1 k cycles per phase, tools/clk_segments.py)
       const int goal_prev = static_cast<int8_t>(b_goal[j]);
+      const int dg = b_dg[j], df = b_df[j], st_new = b_st_new[j], st_old = b_st_old[j];
+      const bool done = t > 0 && b_done[j] != 0;
+      int gop_prev = 0, dfo = 0;
+      if constexpr (kOpNets) {
+        gop_prev = static_cast<int8_t>(b_gop[j]);
+        dfo = b_dfo[j];
+      }
+      asm volatile("" ::"v"(dg), "v"(df), "v"(st_new), "v"(st_old), "v"(gop_prev), "v"(dfo));
       int goal_t;
       const bool need_meta = t > 0 || __ballot(live && goal_prev < 0) != 0;
       int gstar = 0;
       float qe = 0.f;  // meta_eval_net(terminal state)[goal chosen on it], logged at an episode end (:330)
       if (need_meta) {  // meta-net on the next state of step t - 1 (on s_0 for a launch's first goals)
+        // both sources read at once, the terminal observation's bf16 pairs chosen where the episode
+        // ended (one LDS round trip, not the done byte's and then the row's)
         const bool d0 = t > 0 && b_done[row0 + r], d1 = t > 0 && b_done[row0 + 32 + r];
-        const bf16x8 x0 = d0 ? qnet_input_pairs(side + (row0 + r) * 5, h)
-                             : qnet_input(tile + (row0 + r) * kObs, false, h);
-        const bf16x8 x1 = d1 ? qnet_input_pairs(side + (row0 + 32 + r) * 5, h)
-                             : qnet_input(tile + (row0 + 32 + r) * kObs, false, h);
+        const bf16x8 p0 = qnet_input_pairs(side + (row0 + r) * 5, h), p1 = qnet_input_pairs(side + (row0 + 32 + r) * 5, h);
+        const bf16x8 o0 = qnet_input(tile + (row0 + r) * kObs, false, h);
+        const bf16x8 o1 = qnet_input(tile + (row0 + 32 + r) * kObs, false, h);
+        const bf16x8 x0 = d0 ? p0 : o0, x1 = d1 ? p1 : o1;
         float q[8];
         qnet_mlp_swp(lds_meta, x0, x1, q);
         gstar = argmax_first(q, R.num_goals);
-        const int dg = b_dg[j];
         const int g2 = dg == kHGreedy ? gstar : dg;
 #pragma unroll
         for (int k = 0; k < 8; ++k) qe = k == g2 ? q[k] : qe;
       }
-      const int df = b_df[j];
       bool brk = false;  // step t - 1 left the inner loop (:322): a new outer iteration starts
       if (t > 0) {  // hdqn.py:303-322 for step t - 1
-        const int dg = b_dg[j];
         const int goal2 = dg == kHGreedy ? gstar : dg;
-        const bool done = b_done[j] != 0;
-        brk = done || goal2 == b_st_new[j];
+        brk = done || goal2 == st_new;
         goal_t = done ? (df == kHGreedy ? R.reset_goal : df) : (brk ? (df == kHGreedy ? gstar : df) : goal2);
         if (live) {
           const int64_t row = static_cast<int64_t>(t - 1) * R.n + i;
           if (R.H.next_goal) st_out(R.H.next_goal + row, static_cast<float>(goal2));
-          if (R.H.reward) st_out(R.H.reward + row, goal2 == b_st_old[j] ? 1.0f : 0.0f);
+          if (R.H.reward) st_out(R.H.reward + row, goal2 == st_old ? 1.0f : 0.0f);
         }
         b_g2[j] = static_cast<uint8_t>(goal2);  // for the fused ring row of step t - 1
         // the episode's q_eval (hdqn.py:330): the env wave recorded the episode in E(X, t - 1); this
@@ -2649,9 +2658,7 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
       }
       int gop_t = 0;
       if constexpr (kOpNets) {  // upper_op.choose_goal(swapped state) at a new outer iteration (:285)
-        const int gop_prev = static_cast<int8_t>(b_gop[j]);
         const bool fresh_op = t > 0 ? brk : gop_prev < 0;
-        const int dfo = b_dfo[j];
         // Only where the reference evaluates it (round 5): at a new outer iteration, on the greedy
         // branch (:86-92) -- about a quarter of the envs. The wave's items are compacted into one
         // forward on 32 envs (two column tiles) when they fit, else the full 64; the other passes
@@ -2694,14 +2701,20 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
           if (live && R.H.goal_op) st_out(R.H.goal_op + static_cast<int64_t>(t) * R.n + i, static_cast<float>(gop_t));
         }
         wave_lds_sync();  // the wave's goals are in LDS before the lanes read their column envs'
+        const bf16x8 xe0 = qnet_input_goal(tile + (row0 + r) * kObs, b_goal[row0 + r], h);
+        const bf16x8 xe1 = qnet_input_goal(tile + (row0 + 32 + r) * kObs, b_goal[row0 + 32 + r], h);
+        // the opponent's inputs too, before the ego's forward (held across it)
+        bf16x8 xo0 = xe0, xo1 = xe1;
+        if constexpr (kOpNets) {
+          xo0 = qnet_input_goal(tile + (row0 + r) * kObs, b_gop[row0 + r], h, true);
+          xo1 = qnet_input_goal(tile + (row0 + 32 + r) * kObs, b_gop[row0 + 32 + r], h, true);
+        }
         float q[8];
-        qnet_mlp_swp(lds_lower, qnet_input_goal(tile + (row0 + r) * kObs, b_goal[row0 + r], h),
-                     qnet_input_goal(tile + (row0 + 32 + r) * kObs, b_goal[row0 + 32 + r], h), q);
+        qnet_mlp_swp(lds_lower, xe0, xe1, q);
         b_act[j] = static_cast<uint8_t>(argmax_first(q, MG_NUM_ACTIONS));
         if constexpr (kOpNets) {  // lower_op.choose_action([goal_op] + swapped state) (:299-300)
           float qo[8];
-          const bf16x8 x0 = qnet_input_goal(tile + (row0 + r) * kObs, b_gop[row0 + r], h, true);
-          const bf16x8 x1 = qnet_input_goal(tile + (row0 + 32 + r) * kObs, b_gop[row0 + 32 + r], h, true);
+          const bf16x8 x0 = xo0, x1 = xo1;
           if constexpr (OPP == 3)
             qnet_mlp<kQGlobalAhead>(qnet_global(R.lower_op), x0, x1, qo);  // the opponent's own HDQN (:268)
           else

@@ -162,6 +162,47 @@ BASE_EDITS = [
           MG_CLK(13);
           b_aop[j] = static_cast<uint8_t>(argmax_first(qo, MG_NUM_ACTIONS));"""),
 ]
+# the h-DQN Q-net waves as kept in round 5 (opponent meta-net pass compacted): a mark at each
+# boundary of the phase's segments -- 2 / 8 around the meta forward (its inputs before 2), 3 after
+# the goal logic, 9 after the opponent meta pass, 6 / 12 around the lower forward, 7 / 13 around the
+# opponent's lower forward
+NOW_EDITS = [
+    ("""        float q[8];
+        qnet_mlp_swp(lds_meta, x0, x1, q);
+        gstar = argmax_first(q, R.num_goals);""",
+     """        float q[8];
+        MG_CLK(2);
+        qnet_mlp_swp(lds_meta, x0, x1, q);
+        asm volatile("" :: "v"(q[0]), "v"(q[1]), "v"(q[2]));
+        MG_CLK(8);
+        gstar = argmax_first(q, R.num_goals);"""),
+    ("""      int gop_t = 0;
+      if constexpr (kOpNets) {  // upper_op.choose_goal""",
+     """      int gop_t = 0;
+      MG_CLK(3);
+      if constexpr (kOpNets) {  // upper_op.choose_goal"""),
+    ("""        gop_t = fresh_op ? (dfo == kHGreedy ? gop_star : dfo) : gop_prev;
+      }""",
+     """        gop_t = fresh_op ? (dfo == kHGreedy ? gop_star : dfo) : gop_prev;
+      }
+      MG_CLK(9);"""),
+    ("""        float q[8];
+        qnet_mlp_swp(lds_lower, xe0, xe1, q);""",
+     """        float q[8];
+        MG_CLK(6);
+        qnet_mlp_swp(lds_lower, xe0, xe1, q);"""),
+    ("""        b_act[j] = static_cast<uint8_t>(argmax_first(q, MG_NUM_ACTIONS));""",
+     """        asm volatile("" :: "v"(q[0]), "v"(q[1]), "v"(q[2]));
+        MG_CLK(12);
+        b_act[j] = static_cast<uint8_t>(argmax_first(q, MG_NUM_ACTIONS));"""),
+    ("""          const bf16x8 x0 = xo0, x1 = xo1;""",
+     """          const bf16x8 x0 = xo0, x1 = xo1;
+          MG_CLK(7);"""),
+    ("""          b_aop[j] = static_cast<uint8_t>(argmax_first(qo, MG_NUM_ACTIONS));""",
+     """          asm volatile("" :: "v"(qo[0]), "v"(qo[1]), "v"(qo[2]));
+          MG_CLK(13);
+          b_aop[j] = static_cast<uint8_t>(argmax_first(qo, MG_NUM_ACTIONS));"""),
+]
 EDITS = [
     # h-DQN Q-net waves
     ("    for (int p = 0; p < phases; ++p) {\n      const int g = p & 1, t = p >> 1;\n      const int row0 = g * kHHalf + 64 * wave;",
@@ -180,7 +221,7 @@ def main(src, out, marks="0"):
     s = open(src).read()
     s = s.replace('#include "merging_hip.h"\n', '#include "merging_hip.h"\n' + HDR, 1)
     sets = {"0": EDITS, "1": EDITS + NEW_EDITS, "base": EDITS + BASE_EDITS,
-            "q5": Q5_COMMON + Q5_EDITS, "q5base": Q5_COMMON + Q5_BASE_EDITS}
+            "q5": Q5_COMMON + Q5_EDITS, "q5base": Q5_COMMON + Q5_BASE_EDITS, "hnow": EDITS + NOW_EDITS}
     for e in sets[marks]:
         a, b, n = e if len(e) == 3 else (*e, 1)
         assert s.count(a) == n, a[:80]
