@@ -2619,7 +2619,6 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
         gop_prev = static_cast<int8_t>(b_gop[j]);
         dfo = b_dfo[j];
       }
-      asm volatile("" ::"v"(dg), "v"(df), "v"(st_new), "v"(st_old), "v"(gop_prev), "v"(dfo));
       int goal_t;
       const bool need_meta = t > 0 || __ballot(live && goal_prev < 0) != 0;
       int gstar = 0;
@@ -2632,6 +2631,8 @@ __global__ __launch_bounds__(512, 2) void hdqn_rollout_kernel(const HRollout R) 
         const bf16x8 o0 = qnet_input(tile + (row0 + r) * kObs, false, h);
         const bf16x8 o1 = qnet_input(tile + (row0 + 32 + r) * kObs, false, h);
         const bf16x8 x0 = d0 ? p0 : o0, x1 = d1 ? p1 : o1;
+        // the bytes above arrive with the inputs (one wait), not after the forward
+        asm volatile("" ::"v"(dg), "v"(df), "v"(st_new), "v"(st_old), "v"(gop_prev), "v"(dfo));
         float q[8];
         qnet_mlp_swp(lds_meta, x0, x1, q);
         gstar = argmax_first(q, R.num_goals);
