@@ -203,6 +203,24 @@ NOW_EDITS = [
           MG_CLK(13);
           b_aop[j] = static_cast<uint8_t>(argmax_first(qo, MG_NUM_ACTIONS));"""),
 ]
+# the same segments for the lower passes listed by the env waves (r05zh): marks around the ego's and
+# the opponent's listed forwards
+LIST_EDITS = NOW_EDITS[:3] + [
+    ("""          if (nqe > 0) {
+            float q[8];""",
+     """          MG_CLK(6);
+          if (nqe > 0) {
+            float q[8];"""),
+    ("""          if (nqo > 0) {  // lower_op.choose_action""",
+     """          MG_CLK(12);
+          MG_CLK(7);
+          if (nqo > 0) {  // lower_op.choose_action"""),
+    ("""            if (lane < nqo) b_aop[row0 + loo] = static_cast<uint8_t>(argmax_first(qo, MG_NUM_ACTIONS));
+          }""",
+     """            if (lane < nqo) b_aop[row0 + loo] = static_cast<uint8_t>(argmax_first(qo, MG_NUM_ACTIONS));
+          }
+          MG_CLK(13);"""),
+]
 EDITS = [
     # h-DQN Q-net waves
     ("    for (int p = 0; p < phases; ++p) {\n      const int g = p & 1, t = p >> 1;\n      const int row0 = g * kHHalf + 64 * wave;",
@@ -221,7 +239,7 @@ def main(src, out, marks="0"):
     s = open(src).read()
     s = s.replace('#include "merging_hip.h"\n', '#include "merging_hip.h"\n' + HDR, 1)
     sets = {"0": EDITS, "1": EDITS + NEW_EDITS, "base": EDITS + BASE_EDITS,
-            "q5": Q5_COMMON + Q5_EDITS, "q5base": Q5_COMMON + Q5_BASE_EDITS, "hnow": EDITS + NOW_EDITS}
+            "q5": Q5_COMMON + Q5_EDITS, "q5base": Q5_COMMON + Q5_BASE_EDITS, "hnow": EDITS + NOW_EDITS, "hlist": EDITS + LIST_EDITS}
     for e in sets[marks]:
         a, b, n = e if len(e) == 3 else (*e, 1)
         assert s.count(a) == n, a[:80]
