@@ -574,12 +574,11 @@ class MergeVecEnv:
         self._step_idx = int(sd["step_idx"])
         if self.ret_sum is not None:
             self._load_episode_stats(sd)
-        if "hdqn_goal" in sd:
-            self.hdqn_goal = self._torch.as_tensor(sd["hdqn_goal"]).to(self.device, self._torch.int8).clone()
-        if "hdqn_goal_op" in sd:
-            self.hdqn_goal_op = self._torch.as_tensor(sd["hdqn_goal_op"]).to(self.device, self._torch.int8).clone()
-        if "hdqn_ext" in sd:
-            self.hdqn_ext = self._torch.as_tensor(sd["hdqn_ext"]).to(self.device, self._torch.float64).clone()
+        # rollout_hdqn's carried state as it was when the checkpoint was taken: absent = none yet (the
+        # next launch chooses every env's first goals), not whatever a later launch left here
+        for name, dtype in (("hdqn_goal", self._torch.int8), ("hdqn_goal_op", self._torch.int8),
+                            ("hdqn_ext", self._torch.float64)):
+            setattr(self, name, self._torch.as_tensor(sd[name]).to(self.device, dtype).clone() if name in sd else None)
 
     def _load_episode_stats(self, sd):
         """The 64-byte records of a checkpoint. ABI <= 16 checkpoints kept 'ret_sum' / 'counts'
