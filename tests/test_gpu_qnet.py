@@ -218,7 +218,7 @@ def test_rollout_qnet_policy_and_transitions(torch, coracle, nets, opponent, n, 
         cc2.finish()
 
 
-@pytest.mark.parametrize("opponent", ["none", "self"])
+@pytest.mark.parametrize("opponent", ["none", "self", "other"])
 def test_rollout_qnet_invalid_greedy_actions(torch, coracle, nets, opponent):
     """A net with 8 outputs (out_dim <= 8 is allowed) picks actions 5-7, which the reference's
     action_dict rejects with a KeyError after the clock (and the ego, for a bad action2) has
@@ -228,14 +228,19 @@ def test_rollout_qnet_invalid_greedy_actions(torch, coracle, nets, opponent):
     from merging_gym import MergeVecEnv
     from merging_gym.policy import QNet
 
-    sd = dict(nets["l1"])
-    w3, b3 = sd["out.weight"], sd["out.bias"]
-    # output 5 = action 2's row with a slightly larger bias: it wins wherever action 2 would
-    # (most greedy choices of this checkpoint); outputs 6-7 never win
-    sd["out.weight"] = np.concatenate([w3, w3[[2, 0, 1]]])
-    sd["out.bias"] = np.concatenate([b3, [b3[2] + 0.01, b3[0] - 100.0, b3[1] - 100.0]]).astype(np.float32)
-    qnet = QNet.from_state_dict(sd, device="cuda:0")
+    def widened(key):
+        sd = dict(nets[key])
+        w3, b3 = sd["out.weight"], sd["out.bias"]
+        # output 5 = action 2's row with a slightly larger bias: it wins wherever action 2 would
+        # (most greedy choices of this checkpoint); outputs 6-7 never win
+        sd["out.weight"] = np.concatenate([w3, w3[[2, 0, 1]]])
+        sd["out.bias"] = np.concatenate([b3, [b3[2] + 0.01, b3[0] - 100.0, b3[1] - 100.0]]).astype(np.float32)
+        return QNet.from_state_dict(sd, device="cuda:0")
+
+    qnet = widened("l1")
     assert qnet.out_dim == 8
+    if opponent == "other":  # the net-split kernel (round 5) with the other checkpoint widened alike
+        opponent = widened("l3")
     n, T, seed, k0 = 1000, 16, 23, 300
     env = MergeVecEnv(n, device="cuda:0")
     for k in range(40):
