@@ -3,6 +3,11 @@
     python bench.py [--gpus N --steps K --warmup W --envs E]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU)
 
+With --gpus N > 1 and no launcher (no WORLD_SIZE in the environment) bench.py starts the N one-GPU
+ranks itself as child processes, before anything in the parent touches HIP, and exits with the
+worst rank's status; fewer visible GPUs than N is an error under RCCL. Every rank checks that its
+process group (and one all-reduce over it) has exactly N ranks.
+
 A step = one launch of mg_step_random over this rank's 2^20 envs: Philox actions for both
 players drawn on the device, the full reference step (merging_env.py:138-195), autoreset,
 episode statistics. Envs are sharded across ranks (rank r owns global envs [r E, (r+1) E),
@@ -22,7 +27,8 @@ or a HIP-graph replay with --graph 1.
 Rank 0 prints ONE JSON line: value = env-steps/s over all ranks (max-over-ranks time),
 roofline = algorithmic bytes per launch / mean kernel time (HIP events on the launch stream)
 against the 8 TB/s HBM3E peak, size_2p22 = the same kernel at 2^22 envs (past the 256 MiB
-Infinity Cache, N = 1 only), cpu_baseline = the CPU restatements on the host cores (N = 1 only).
+Infinity Cache, N = 1 only), cpu_baseline = the CPU restatements on the host cores (rank 0, at every
+world size, after the GPU legs; the other ranks wait at the closing barrier).
 """
 
 from __future__ import annotations
@@ -693,6 +699,90 @@ def _native_build_info():
     return _native.build_info()
 
 
+DEVICE_COUNT_ENV = "MG_BENCH_DEVICE_COUNT"   # overrides the probe (tests of the launch decision)
+SELF_LAUNCH_ENV = "MG_BENCH_SELF_LAUNCHED"  # set in the ranks a self-launch starts
+
+
+def visible_gpu_count() -> int:
+    """GPUs the ranks could use, counted in a child process (torch.cuda.device_count() there), so that
+    the launching process itself never imports torch or loads HIP before it starts the ranks."""
+    if DEVICE_COUNT_ENV in os.environ:
+        return int(os.environ[DEVICE_COUNT_ENV])
+    import subprocess
+
+    out = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                         capture_output=True, text=True, timeout=900)
+    if out.returncode != 0:
+        raise SystemExit(f"bench.py: counting GPUs failed (rc {out.returncode}): {out.stderr[-400:]}")
+    return int(out.stdout.strip().splitlines()[-1])
+
+
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_envs(args, environ, ngpu: int, port: int) -> list:
+    """The environment of each rank of a self-launch (--gpus N > 1 without a launcher's WORLD_SIZE):
+    the variables torchrun would set, one GPU per rank. Under RCCL (backend nccl) every rank needs a
+    GPU of its own, so fewer than N visible GPUs is an error; a gloo rehearsal may share them."""
+    n = args.gpus
+    if ngpu < 1:
+        raise SystemExit(f"bench.py --gpus {n}: no GPU visible")
+    if args.dist_backend == "nccl" and ngpu < n:
+        raise SystemExit(f"bench.py --gpus {n}: only {ngpu} GPU(s) visible; RCCL needs one per rank "
+                         "(--dist-backend gloo rehearses N ranks on fewer GPUs)")
+    out = []
+    for r in range(n):
+        e = dict(environ)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), **{SELF_LAUNCH_ENV: "1"})
+        out.append(e)
+    return out
+
+
+def self_launch(args, argv, popen=None, script=None) -> int:
+    """Start N one-GPU ranks of this script (same arguments) as child processes and wait for them:
+    rank 0 prints the JSON line on the shared stdout; when a rank fails the others are stopped. Returns
+    the worst exit status (the first nonzero one in rank order). Runs before anything in this process
+    imports torch or loads HIP, and replaces no process (children only)."""
+    import signal
+    import subprocess
+
+    popen = popen or subprocess.Popen
+    envs = rank_envs(args, os.environ, visible_gpu_count(), free_port())
+    cmd = [sys.executable, "-u", script or os.path.abspath(__file__), *argv]
+    procs = [popen(cmd, env=e) for e in envs]
+
+    def stop(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+
+    old = signal.signal(signal.SIGTERM, lambda *a: (stop(), sys.exit(143)))
+    first_bad = None
+    try:
+        rcs = [None] * len(procs)
+        while any(rc is None for rc in rcs):
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    rcs[i] = p.poll()
+                    if rcs[i] not in (None, 0) and first_bad is None:
+                        first_bad = rcs[i]
+                        print(f"bench.py: rank {i} exited with {rcs[i]}; stopping the others", file=sys.stderr)
+                        stop()  # a failed rank would leave the others at a barrier
+            time.sleep(0.05)
+    finally:
+        signal.signal(signal.SIGTERM, old)
+        stop()
+    if first_bad is None:
+        return 0
+    return first_bad if first_bad > 0 else 128 - first_bad  # killed by signal s: 128 + s, as a shell reports
+
+
 def sync_spin():
     """hipDeviceScheduleSpin for this process, before the HIP context exists: a synchronize then
     spins on the host instead of yielding, so the host thread that issues the timed launches is
@@ -707,24 +797,42 @@ def sync_spin():
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # the driver's 1-GPU form (python3 bench.py --gpus N) asked for N GPUs: start N ranks here,
+        # before this process touches HIP (sync_spin below already does)
+        sys.exit(self_launch(args, sys.argv[1:]))
+    env_world = int(os.environ.get("WORLD_SIZE", "1"))
+    if env_world != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} under a launcher with WORLD_SIZE={env_world}")
+    launcher = ("self" if os.environ.get(SELF_LAUNCH_ENV) == "1" else "external") if env_world > 1 else None
     spin_rc = sync_spin() if args.sync_spin else None
     import torch
     import torch.distributed as dist
 
-    env_world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    device = torch.device("cuda", local % max(torch.cuda.device_count(), 1) if env_world > 1 else 0)
+    ndev = torch.cuda.device_count()
+    if env_world > 1 and args.dist_backend == "nccl" and local >= ndev:
+        raise SystemExit(f"rank with LOCAL_RANK {local}: only {ndev} GPU(s) visible (RCCL needs one per rank)")
+    device = torch.device("cuda", local % max(ndev, 1) if env_world > 1 else 0)
     torch.cuda.set_device(device)
     backend = None
+    coll_ranks = None
     if env_world > 1:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=device)
         else:
             dist.init_process_group(args.dist_backend)
         backend = dist.get_backend()
+        # the rank count the collective itself sees: one all-reduce of a 1 per rank over the
+        # process group (RCCL over xGMI under "nccl"), outside every timed region
+        one = torch.ones(1, dtype=torch.int64, device=device if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(one)
+        coll_ranks = int(one.item())
     # the rank count and rank the process group reports (RCCL under backend "nccl" on ROCm)
     world = dist.get_world_size() if env_world > 1 else 1
     rank = dist.get_rank() if env_world > 1 else 0
+    if world != args.gpus or (coll_ranks is not None and coll_ranks != args.gpus):
+        raise SystemExit(f"bench.py --gpus {args.gpus}: process group of {world} ranks, all-reduce saw {coll_ranks}")
     host_coll = world > 1 and args.dist_backend != "nccl"
 
     from merging_gym import MergeVecEnv
@@ -903,7 +1011,8 @@ def main():
             "unit": "env-steps/s",
             "n_gpus": world,
             "dist": {"backend": backend, "world_size": world, "rank_printing": rank,
-                     "launcher_world_size": env_world},
+                     "launcher_world_size": env_world, "launcher": launcher, "collective_ranks": coll_ranks,
+                     "gpus_requested": args.gpus},
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,

@@ -65,15 +65,35 @@ def is_current(lib_path: str = OUT, sha: str | None = None) -> bool:
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile OUT unless it is current. Several processes may get here at once (the ranks of a
+    multi-rank launch, each importing a stale library): an fcntl lock next to OUT serialises them,
+    the current-check is repeated under it so only the first one compiles, and each compile writes
+    its own temporary file, moved into place atomically."""
+    import fcntl
+    import tempfile
+
     sha = source_sha()
     if not force and os.path.exists(OUT) and is_current(OUT, sha):
         return OUT
-    tmp = OUT + ".tmp"
-    cmd = [hipcc(), *HIPCC_FLAGS, f'-DMG_SRC_SHA="{sha}"', "-I", INCLUDE, "-o", tmp, SRC]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.check_call(cmd)
-    os.replace(tmp, OUT)
+    with open(OUT + ".lock", "a+") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        try:
+            if not force and os.path.exists(OUT) and is_current(OUT, sha):
+                return OUT  # another process built it while this one waited
+            fd, tmp = tempfile.mkstemp(prefix=".libmerging_hip.", suffix=".so.tmp", dir=PKG)
+            os.close(fd)
+            try:
+                cmd = [hipcc(), *HIPCC_FLAGS, f'-DMG_SRC_SHA="{sha}"', "-I", INCLUDE, "-o", tmp, SRC]
+                if verbose:
+                    print(" ".join(cmd), file=sys.stderr)
+                subprocess.check_call(cmd)
+                os.chmod(tmp, 0o755)
+                os.replace(tmp, OUT)
+            finally:
+                if os.path.exists(tmp):
+                    os.unlink(tmp)
+        finally:
+            fcntl.flock(lock, fcntl.LOCK_UN)
     return OUT
 
 

@@ -169,3 +169,151 @@ def test_compact_line_of_a_full_record_is_small():
                 "size_2p22"):
         assert leg in d["legs"], leg
     assert d["roofline"]["frac"] == full["roofline"]["frac"] and d["cpu_baseline"]["cores"] == 16
+
+
+def check_requested(d, requested):
+    """A line answers the run that asked for it: n_gpus (and the process group's rank count) equal the
+    --gpus the driver passed, so an 8-GPU request cannot come back as a 1-GPU line."""
+    check_line(d)
+    assert d["n_gpus"] == requested, (d["n_gpus"], requested)
+    gr = d["dist"].get("gpus_requested")
+    assert gr is None or gr == requested, gr
+    cr = d["dist"].get("collective_ranks")
+    assert cr is None or cr == requested, cr
+
+
+def test_line_for_another_gpu_count_is_rejected():
+    check_requested(_synthetic(8), 8)
+    check_requested(_synthetic(1), 1)
+    with pytest.raises(AssertionError):
+        check_requested(_synthetic(1), 8)  # the round-5 failure: --gpus 8 measured one GPU
+    bad = _synthetic(8)
+    bad["dist"]["collective_ranks"] = 4
+    with pytest.raises(AssertionError):
+        check_requested(bad, 8)
+
+
+# ---- the self-launch (bench.py --gpus N > 1 without torchrun) -------------------------------------------
+
+def _bench():
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    return bench
+
+
+class _Args:
+    def __init__(self, gpus, backend="nccl"):
+        self.gpus, self.dist_backend = gpus, backend
+
+
+def test_rank_environments_for_two_gpus():
+    bench = _bench()
+    envs = bench.rank_envs(_Args(2), {"PATH": "/bin", "HSA_ENABLE_IPC_MODE_LEGACY": "0"}, 2, 29511)
+    assert len(envs) == 2
+    for r, e in enumerate(envs):
+        assert (e["RANK"], e["LOCAL_RANK"], e["WORLD_SIZE"], e["LOCAL_WORLD_SIZE"]) == (str(r), str(r), "2", "2")
+        assert (e["MASTER_ADDR"], e["MASTER_PORT"]) == ("127.0.0.1", "29511")
+        assert e["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" and e[bench.SELF_LAUNCH_ENV] == "1"
+
+
+def test_too_few_gpus_is_an_error_under_rccl_only():
+    bench = _bench()
+    with pytest.raises(SystemExit, match="only 1 GPU"):
+        bench.rank_envs(_Args(2), {}, 1, 1)
+    with pytest.raises(SystemExit, match="no GPU"):
+        bench.rank_envs(_Args(2, "gloo"), {}, 0, 1)
+    assert len(bench.rank_envs(_Args(8, "gloo"), {}, 1, 1)) == 8  # the gloo rehearsal shares one GPU
+
+
+_SPAWN_PROBE = r"""
+import json, os, sys
+sys.path.insert(0, {root!r})
+sys.argv = ["bench.py", "--gpus", "2", "--steps", "3"]
+os.environ.pop("WORLD_SIZE", None)
+os.environ["MG_BENCH_DEVICE_COUNT"] = "2"
+import bench
+calls = []
+class P:
+    def __init__(self, cmd, env):
+        calls.append((cmd, {{k: env[k] for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR")}}))
+    def poll(self):
+        return 0
+    def terminate(self):
+        pass
+try:
+    orig = bench.self_launch
+    bench.self_launch = lambda a, argv: orig(a, argv, popen=P)
+    bench.main()
+except SystemExit as e:
+    rc = e.code
+maps = open("/proc/self/maps").read()
+print(json.dumps({{"rc": rc, "calls": calls, "torch": "torch" in sys.modules,
+                   "hip_loaded": "amdhip64" in maps, "ctypes": "ctypes" in sys.modules}}))
+"""
+
+
+def test_gpus_two_spawns_two_ranks_before_anything_touches_hip():
+    """main() with --gpus 2 and no WORLD_SIZE starts two children of the same command with the
+    rank environment, and the parent has neither imported torch nor mapped libamdhip64 by then."""
+    import subprocess
+    import sys
+
+    out = subprocess.run([sys.executable, "-c", _SPAWN_PROBE.format(root=ROOT)], capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 0, out.stderr
+    d = json.loads(out.stdout.strip().splitlines()[-1])
+    assert d["rc"] == 0 and not d["torch"] and not d["hip_loaded"], d
+    assert len(d["calls"]) == 2
+    for r, (cmd, env) in enumerate(d["calls"]):
+        assert cmd[-4:] == ["--gpus", "2", "--steps", "3"] and cmd[-5].endswith("bench.py")
+        assert env == {"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": "2", "MASTER_ADDR": "127.0.0.1"}
+
+
+def test_gpus_two_with_one_visible_gpu_exits_nonzero():
+    import subprocess
+    import sys
+
+    env = dict(os.environ, MG_BENCH_DEVICE_COUNT="1")
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], capture_output=True,
+                         text=True, timeout=120, env=env)
+    assert out.returncode != 0 and "only 1 GPU" in out.stderr, (out.returncode, out.stderr[-500:])
+    assert not out.stdout.strip()  # no bench line at all
+
+
+def test_self_launch_relays_the_first_failure_and_stops_the_other_ranks(tmp_path):
+    """Real child processes (a stand-in rank script): rank 1 fails at once, rank 0 would run for a
+    minute; the launcher stops rank 0 and exits with rank 1's status."""
+    bench = _bench()
+    script = tmp_path / "rank.py"
+    script.write_text("import os, sys, time\n"
+                      "open(os.path.join(%r, 'r' + os.environ['RANK']), 'w').write(os.environ['WORLD_SIZE'] + ' ' "
+                      "+ os.environ['MASTER_PORT'])\n"
+                      "if os.environ['RANK'] == '1':\n    sys.exit(3)\n"
+                      "time.sleep(60)\n" % str(tmp_path))
+    os.environ[bench.DEVICE_COUNT_ENV] = "2"
+    try:
+        import time
+
+        t0 = time.time()
+        rc = bench.self_launch(_Args(2), ["--gpus", "2"], script=str(script))
+        assert rc == 3 and time.time() - t0 < 30
+    finally:
+        del os.environ[bench.DEVICE_COUNT_ENV]
+    w0, p0 = (tmp_path / "r0").read_text().split()
+    w1, p1 = (tmp_path / "r1").read_text().split()
+    assert w0 == w1 == "2" and p0 == p1
+
+
+def test_self_launch_all_ranks_green(tmp_path):
+    bench = _bench()
+    script = tmp_path / "rank.py"
+    script.write_text("import os\nassert os.environ['WORLD_SIZE'] == '3'\n")
+    os.environ[bench.DEVICE_COUNT_ENV] = "3"
+    try:
+        assert bench.self_launch(_Args(3), [], script=str(script)) == 0
+    finally:
+        del os.environ[bench.DEVICE_COUNT_ENV]

@@ -1,9 +1,10 @@
 """Offline half of the summation-order study: compares the Q-values mg_qnet_forward returned on the
 MI355X (saved by tools/mfma_order_dump.py) with the oracle's models of the matrix cores' addition
-order (oracle/merge_oracle.py qnet_reference_mfma, grouped and ungrouped) and with an fp32 matmul of
-the same bf16 operands. Prints the fraction of rows equal bit for bit per net and view.
+order (oracle/merge_oracle.py qnet_reference_mfma: the measured rule "mfma", round 5's "exact8" model)
+and with an fp32 matmul of the same bf16 operands. Prints the fraction of rows equal bit for bit per net
+and view.
 
-    python tools/mfma_order_study.py gpurun_out/r05i/qdump.npz > profiles/r05/mfma_order.txt
+    python tools/mfma_order_study.py gpurun_out/r05i/qdump.npz > profiles/r06/mfma_order.txt
 """
 import os
 import sys
@@ -47,12 +48,12 @@ def main(path):
         w = {k.split("/", 1)[1]: d[k] for k in d.files if k.startswith(name + "/")}
         cases.append((f"{name} (seeded signed)", w, d[f"{name}_x"], False, d[f"{name}_q"]))
     for label, w, x, swap, got in cases:
-        g = mo.qnet_reference_mfma(w, x, swap=swap, grouped=True)
-        u = mo.qnet_reference_mfma(w, x, swap=swap, grouped=False)
+        r = mo.qnet_reference_mfma(w, x, swap=swap, rule="mfma")
+        g = mo.qnet_reference_mfma(w, x, swap=swap, rule="exact8")
         m = fp32_matmul(w, x, swap)
-        print(f"  {label:22s} grouped-8 {rows_equal(g, got):.6f} ({int(np.sum(np.all(g == got, 1)))}/{len(got)})"
-              f"  ungrouped {rows_equal(u, got):.6f}  fp32 matmul {rows_equal(m, got):.6f}"
-              f"  max |grouped - kernel| {float(np.max(np.abs(g - got))):.3g}")
+        print(f"  {label:22s} measured rule {rows_equal(r, got):.6f} ({int(np.sum(np.all(r.view(np.uint32) == got.view(np.uint32), 1)))}/{len(got)})"
+              f"  round-5 exact-8 {rows_equal(g, got):.6f}  fp32 matmul {rows_equal(m, got):.6f}"
+              f"  max |rule - kernel| {float(np.max(np.abs(r - got))):.3g}")
 
 
 if __name__ == "__main__":
