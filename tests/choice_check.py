@@ -8,6 +8,12 @@ argmax is excused only when the action the kernel took has an emulated Q within 
 to max(1, |Q_max|)) of the row's maximum -- never any other action -- and every check counts
 the excused choices; `finish()` prints the fraction and asserts it is below the test's bound.
 Random (exploring) choices are exact: they come from the Philox draws alone.
+
+Round 6: the excusal is no longer the last word. A check given `q_exact` (exact_q below: the
+oracle's restatement of the matrix cores' accumulation, oracle.merge_oracle.qnet_reference_mfma,
+pinned to recorded MI355X outputs by tests/test_oracle_mfma.py) requires EVERY greedy choice to equal
+that model's argmax (first maximum, as the kernels' argmax_first), near-ties included; the fp32
+emulation's disagreements are still counted and bounded, and each one is thereby explained.
 """
 
 from __future__ import annotations
@@ -25,8 +31,10 @@ class ChoiceCheck:
         self.name, self.tol, self.max_frac = name, tol, max_frac
         self.greedy = 0
         self.excused = 0
+        self.exact = 0       # greedy choices checked against the oracle's MFMA-rule argmax
+        self.exact_fp32 = 0  # ... of which the fp32 emulation's argmax differs (near-ties)
 
-    def check(self, got, exp, greedy, q, what=""):
+    def check(self, got, exp, greedy, q, what="", q_exact=None):
         got = np.asarray(got).astype(np.int64)
         exp = np.asarray(exp).astype(np.int64)
         greedy = np.asarray(greedy, bool)
@@ -48,6 +56,20 @@ class ChoiceCheck:
                 f"{self.name} {what}: {i.size} of {n} choices differ beyond a near-tie; envs {i[:8].tolist()}, got "
                 f"{got[i[:8]].tolist()}, expected {exp[i[:8]].tolist()}, greedy {greedy[i[:8]].tolist()}, "
                 f"top-2 gap {gap[:8].tolist()}, q {q[i[:3]].tolist()}")
+        if q_exact is not None:
+            idx = np.flatnonzero(greedy)
+            if idx.size:
+                qx = q_exact(idx) if callable(q_exact) else np.asarray(q_exact)[idx]
+                want = np.asarray(qx).argmax(axis=1)
+                miss = got[idx] != want
+                if miss.any():
+                    j = idx[miss]
+                    raise AssertionError(
+                        f"{self.name} {what}: {j.size} of {idx.size} greedy choices differ from the oracle MFMA "
+                        f"rule's argmax; envs {j[:8].tolist()}, got {got[j[:8]].tolist()}, model "
+                        f"{want[miss][:8].tolist()}, model q {np.asarray(qx)[miss][:3].tolist()}")
+                self.exact += int(idx.size)
+                self.exact_fp32 += int((got[idx] != exp[idx]).sum())
         return excused
 
     @property
@@ -57,6 +79,9 @@ class ChoiceCheck:
     def finish(self) -> float:
         line = (f"[near-tie] {self.name}: {self.excused} of {self.greedy} greedy choices excused "
                 f"({100 * self.frac:.3f} %, bound {'-' if self.max_frac is None else f'{100 * self.max_frac:.2f} %'})")
+        if self.exact:
+            line += (f"; oracle MFMA rule: {self.exact} greedy choices checked, all equal its argmax "
+                     f"({self.exact_fp32} of them differ from the fp32 emulation's)")
         print(line)
         SUMMARY.append(line)
         if self.max_frac is not None:
@@ -65,18 +90,22 @@ class ChoiceCheck:
 
 
 def order_matched_q(qnet, sd, x, form, torch=None):
-    """The Q-values the kernel's own forward computes, in its summation order: for the 16x16x32
-    forward (net opponents, h-DQN) mg_qnet_forward -- the same qnet_mlp code and k order on the
-    device -- and for the 32x32x16 forward of config 5 without a net opponent, which has no standalone
-    entry point, the oracle's MFMA model of it (oracle.merge_oracle.qnet_reference_mfma, which
-    reproduces the kernels' Q-values of the shipped checkpoints bit for bit, tests/test_gpu_qnet.py)."""
+    """The Q-values the kernels compute, restated on the CPU: the oracle's model of the matrix cores'
+    accumulation (oracle.merge_oracle.qnet_reference_mfma, rule "mfma") in the kernel's packed k order,
+    form "16x16" (net opponents, h-DQN) or "32x32" (config 5 without a net opponent). Round 6: no
+    longer the device's own mg_qnet_forward for the 16x16 form -- the kernel is never its own reference.
+    `qnet` is unused (kept for the call sites' signature)."""
     import merge_oracle as mo
 
-    if form == "16x16":
-        import torch as t
-
-        return qnet.forward(t.from_numpy(np.ascontiguousarray(x, np.float32)).cuda()).cpu().numpy().astype(np.float64)
     return mo.qnet_reference_mfma(sd, x, form=form).astype(np.float64)
+
+
+def exact_q(sd, x, swap=False, form="16x16"):
+    """Lazy oracle-rule Q rows for ChoiceCheck.check(q_exact=...): idx -> qnet_reference_mfma of x[idx]."""
+    import merge_oracle as mo
+
+    x = np.asarray(x, np.float32)
+    return lambda idx: mo.qnet_reference_mfma(sd, x[idx], swap=swap, form=form)
 
 
 def check_q_eval(dev, exp, abs_sum, what="", pinned=None, model=None):
@@ -91,7 +120,8 @@ def check_q_eval(dev, exp, abs_sum, what="", pinned=None, model=None):
     reproduce fails the check. `model` (optional): the same sums from the oracle's CPU model of the
     kernel's summation order (oracle.merge_oracle.qnet_reference_mfma), which must reproduce every
     flagged env bit for bit too. Without `pinned`, every env must stay within 1e-2 (round 4's bound
-    before r04d; no widening)."""
+    before r04d; no widening). Round 6: `pinned` is the oracle's MFMA-rule sums (order_matched_q), and
+    EVERY logged env must equal them bit for bit."""
     import numpy as np
 
     dev, exp, abs_sum = (np.asarray(a, np.float64) for a in (dev, exp, abs_sum))
@@ -106,7 +136,9 @@ def check_q_eval(dev, exp, abs_sum, what="", pinned=None, model=None):
         bad = flagged & (dev != pinned)
         assert not bad.any(), (what, "unexplained q_eval", np.flatnonzero(bad)[:8].tolist(), dev[bad][:4].tolist(),
                                pinned[bad][:4].tolist(), exp[bad][:4].tolist())
-        assert (dev[logged] == pinned[logged]).mean() > 0.99, (what, (dev[logged] == pinned[logged]).mean())
+        same = dev[logged] == pinned[logged]
+        assert same.all(), (what, "q_eval differs from the oracle MFMA rule's sums", int((~same).sum()),
+                            np.flatnonzero(logged)[~same][:8].tolist())
     else:
         assert err[logged].max() < 1e-2, (what, float(err[logged].max()))
     if model is not None:
@@ -117,7 +149,7 @@ def check_q_eval(dev, exp, abs_sum, what="", pinned=None, model=None):
     SUMMARY.append(f"[q_eval] {what}: {int(logged.sum())} envs with logged episodes, median rel err "
                    f"{float(np.median(err[logged])):.2e}, max {float(err[logged].max()):.2e}; "
                    f"{int(flagged.sum())} above 1e-3, "
-                   + ("all reproduced bit for bit by the kernel-order forward"
+                   + ("every logged env bit for bit equal to the oracle MFMA rule's sums"
                       + (f" ({100 * float((dev[logged] == pinned[logged]).mean()):.2f} % of all envs bit-equal)")
                       if pinned is not None else "no order-matched pin")
                    + (f"; oracle MFMA model: flagged ones bit-equal, {100 * float((dev[logged] == model[logged]).mean()):.2f} "

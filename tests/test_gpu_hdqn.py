@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 
 import merge_oracle as mo
-from choice_check import ChoiceCheck, check_q_eval, order_matched_q
+from choice_check import ChoiceCheck, check_q_eval, exact_q, order_matched_q
 
 pytestmark = pytest.mark.gpu
 
@@ -105,7 +105,8 @@ def test_batched_hdqn_inner_loop(coracle):
         q1_ref = mo.qnet_reference(lower_sd, x.cpu().numpy(), bf16=True)
         g1 = greedy1.cpu().numpy()
         got = a1.cpu().numpy()
-        cc.check(got, np.where(g1, q1_ref.argmax(1), got), g1, q1_ref, f"step {t}")
+        cc.check(got, np.where(g1, q1_ref.argmax(1), got), g1, q1_ref, f"step {t}",
+                 q_exact=exact_q(lower_sd, x.cpu().numpy()))
         nobs, rew, done, info = env.step(a1.to(torch.int8), None)  # :302, L0 opponent
         s2 = torch.where(done[:, None], info["final_observation"], nobs)  # next_state before any reset
         q2 = meta.forward(s2)
@@ -204,8 +205,9 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
     cc_g = ChoiceCheck(f"fused h-DQN {opponent} n={n}: goals", max_frac=MAX_EXCUSED["signed" if kind == "signed" else "uniform"])
     cc_o = ChoiceCheck(f"fused h-DQN {opponent} n={n}: opponent", max_frac=MAX_EXCUSED[kind])
     reset_goal = meta.reset_argmax()
-    q_reset = mo.qnet_reference(meta_sd, coracle.reset(coracle.new_envs(1)).astype(np.float32), bf16=True)
-    ChoiceCheck("reset goal").check([reset_goal], q_reset.argmax(1), [True], q_reset)
+    reset_obs = coracle.reset(coracle.new_envs(1)).astype(np.float32)
+    q_reset = mo.qnet_reference(meta_sd, reset_obs, bf16=True)
+    ChoiceCheck("reset goal").check([reset_goal], q_reset.argmax(1), [True], q_reset, q_exact=exact_q(meta_sd, reset_obs))
     fresh_off = -(1 << 63)  # counter (env ^ 2^63, step): the fresh-goal stream
     op_off = 1 << 62  # counter (env ^ 2^62, step): the self-play opponent's stream
     selfplay = opponent != "none"  # the opponent acts through h-DQN nets
@@ -239,7 +241,7 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
             fx, fy, _ = mo.hdqn_fresh_draws(fresh_words, k0 - 1, opponent)
             qm = mo.qnet_reference(meta_sd, obs, bf16=True)
             exp = np.where(fx < thr, qm.argmax(1), _pick(fy, NUM_GOALS))
-            cc_g.check(g["goal"][0], exp, fx < thr, qm, f"launch {launch} first goals")
+            cc_g.check(g["goal"][0], exp, fx < thr, qm, f"launch {launch} first goals", q_exact=exact_q(meta_sd, obs))
         else:
             assert (g["goal"][0] == goal_prev).all(), launch
         if selfplay:  # the opponent's first goal (:285): carried over, or fresh with step k0 - 1's draw
@@ -248,7 +250,7 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
                 qo = mo.qnet_reference(op_meta_sd, _swap(obs), bf16=True)
                 gf0 = fc[:, 2] < thr
                 cc_g.check(g["goal_op"][0], np.where(gf0, qo.argmax(1), _pick(fc[:, 3], NUM_GOALS)), gf0, qo,
-                           f"launch {launch} opponent's first goals")
+                           f"launch {launch} opponent's first goals", q_exact=exact_q(op_meta_sd, _swap(obs)))
             else:
                 assert (g["goal_op"][0] == gop_prev).all(), launch
         else:
@@ -262,7 +264,7 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
             q1 = mo.qnet_reference(lower_sd, x, bf16=True)
             greedy = ua[:, 0] < thr
             exp_a = np.where(greedy, q1.argmax(1), _pick(ua[:, 1], 5))
-            cc_a.check(a1_all[t], exp_a, greedy, q1, f"ego action, launch {launch} step {t}")
+            cc_a.check(a1_all[t], exp_a, greedy, q1, f"ego action, launch {launch} step {t}", q_exact=exact_q(lower_sd, x))
             a2 = None
             if selfplay:  # lower_op.choose_action([goal_op] + swapped state), :299-300
                 uc = coracle.philox_batch(n, op_off, seed, k)
@@ -270,7 +272,8 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
                 qa = mo.qnet_reference(op_lower_sd, xo, bf16=True)
                 go = uc[:, 0] < thr
                 exp_a2 = np.where(go, qa.argmax(1), _pick(uc[:, 1], 5))
-                cc_o.check(a2_all[t], exp_a2, go, qa, f"opponent action, launch {launch} step {t}")
+                cc_o.check(a2_all[t], exp_a2, go, qa, f"opponent action, launch {launch} step {t}",
+                           q_exact=exact_q(op_lower_sd, xo))
                 a2 = a2_all[t].astype(np.int8)
             o_obs, o_rew, o_done, o_coll, _, o_fobs, err = coracle.step(envs, a1_all[t].astype(np.int8), a2,
                                                                         autoreset=True, final_obs=True, stats=stats)
@@ -286,7 +289,8 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
             gg = ua[:, 2] < thr
             exp_g2 = np.where(gg, q2.argmax(1), _pick(ua[:, 3], NUM_GOALS))
             g2 = g["next_goal"][t].astype(np.int64)
-            cc_g.check(g2, exp_g2, gg, q2, f"next goal, launch {launch} step {t}")
+            q2x = exact_q(meta_sd, s2)
+            cc_g.check(g2, exp_g2, gg, q2, f"next goal, launch {launch} step {t}", q_exact=q2x)
             # meta_eval_net(state)[goal] on the terminal state and the goal chosen on it (:330)
             qg = q2[np.arange(n), g2]
             qe += np.where(d, qg, 0.0)
@@ -310,13 +314,14 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
             fresh = np.where(gf, np.where(d, reset_goal, q2.argmax(1)), _pick(uby, NUM_GOALS))
             exp_next = np.where(brk, fresh, g2)
             nxt = g["goal"][t + 1] if t + 1 < T else env.hdqn_goal.cpu().numpy().astype(np.int64)
-            cc_g.check(nxt, exp_next, brk & gf & ~d, q2, f"fresh goal, launch {launch} step {t}")
+            cc_g.check(nxt, exp_next, brk & gf & ~d, q2, f"fresh goal, launch {launch} step {t}", q_exact=q2x)
             if selfplay:  # the opponent's goal of the next step: fresh at a new outer iteration (:285)
                 qo = mo.qnet_reference(op_meta_sd, _swap(o_all[t]), bf16=True)  # the state acted on next (reset obs after an end)
                 go = uc[:, 2] < thr
                 exp_op = np.where(brk, np.where(go, qo.argmax(1), _pick(uc[:, 3], NUM_GOALS)), g["goal_op"][t])
                 nxo = g["goal_op"][t + 1] if t + 1 < T else env.hdqn_goal_op.cpu().numpy().astype(np.int64)
-                cc_g.check(nxo, exp_op, brk & go, qo, f"opponent's fresh goal, launch {launch} step {t}")
+                cc_g.check(nxo, exp_op, brk & go, qo, f"opponent's fresh goal, launch {launch} step {t}",
+                           q_exact=exact_q(op_meta_sd, _swap(o_all[t])))
             for key, v in (("obs0", obs), ("obs", o_all[t]), ("fobs", fo_all[t]), ("a1", a1_all[t]),
                            ("rew", rew_all[t]), ("done", d), ("goal", g["goal"][t]), ("goal2", g["next_goal"][t]),
                            ("r_int", g["reward"][t])):
@@ -354,7 +359,7 @@ def test_fused_hdqn_rollout(coracle, n, opponent):
     # the episode statistics the launch's finishing envs recorded (both scripts' logged values)
     np.testing.assert_array_equal(env.returns.cpu().numpy(), stats[0])
     np.testing.assert_array_equal(env.counts.cpu().numpy().astype(np.uint32), stats[1])
-    check_q_eval(env.q_eval.cpu().numpy(), qe, qe_abs, f"fused h-DQN {opponent} n={n}", pinned=qe_pin)
+    check_q_eval(env.q_eval.cpu().numpy(), qe, qe_abs, f"fused h-DQN {opponent} n={n}", pinned=qe_pin, model=qe_pin)
     cc_a.finish()
     cc_g.finish()
     if selfplay:
@@ -420,15 +425,16 @@ def test_fused_hdqn_rollout_full_size(coracle, nets):
     fx, fy, _ = mo.hdqn_fresh_draws(fresh_words, k0 - 1, "none")
     qm = mo.qnet_reference(meta_sd, obs, bf16=True)
     exp0 = np.where(fx < thr, qm.argmax(1), _pick(fy, NUM_GOALS))
-    cc_g.check(sub["goal"][0], exp0, fx < thr, qm, "first goals")
+    cc_g.check(sub["goal"][0], exp0, fx < thr, qm, "first goals", q_exact=exact_q(meta_sd, obs))
     for t in range(T):
         ua = _philox_words(idx_np, seed, k0 + t)
         ubx, uby, _ = mo.hdqn_fresh_draws(fresh_words, k0 + t, "none")
         goal_t = sub["goal"][t].astype(np.int64)
-        q1 = mo.qnet_reference(lower_sd, np.concatenate([goal_t[:, None].astype(np.float32), obs], axis=1), bf16=True)
+        x1 = np.concatenate([goal_t[:, None].astype(np.float32), obs], axis=1)
+        q1 = mo.qnet_reference(lower_sd, x1, bf16=True)
         greedy = ua[:, 0] < thr
         exp_a = np.where(greedy, q1.argmax(1), _pick(ua[:, 1], 5))
-        cc_a.check(sub["a1"][t], exp_a, greedy, q1, f"step {t}")
+        cc_a.check(sub["a1"][t], exp_a, greedy, q1, f"step {t}", q_exact=exact_q(lower_sd, x1))
         o_obs, o_rew, o_done, o_coll, _, o_fobs, err = coracle.step(envs, sub["a1"][t].astype(np.int8), None,
                                                                     autoreset=True, final_obs=True, stats=stats)
         assert err == 0
@@ -442,7 +448,9 @@ def test_fused_hdqn_rollout_full_size(coracle, nets):
         q2 = mo.qnet_reference(meta_sd, s2, bf16=True)
         gg = ua[:, 2] < thr
         g2 = sub["next_goal"][t].astype(np.int64)
-        cc_g.check(g2, np.where(gg, q2.argmax(1), _pick(ua[:, 3], NUM_GOALS)), gg, q2, f"next goal, step {t}")
+        q2x = exact_q(meta_sd, s2)
+        cc_g.check(g2, np.where(gg, q2.argmax(1), _pick(ua[:, 3], NUM_GOALS)), gg, q2, f"next goal, step {t}",
+                   q_exact=q2x)
         qg = q2[np.arange(len(idx_np)), g2]  # hdqn.py:330
         qe += np.where(d, qg, 0.0)
         qe_abs += np.where(d, np.abs(q2).max(1), 0.0)
@@ -453,7 +461,7 @@ def test_fused_hdqn_rollout_full_size(coracle, nets):
         gf = ubx < thr
         exp_next = np.where(brk, np.where(gf, np.where(d, reset_goal, q2.argmax(1)), _pick(uby, NUM_GOALS)), g2)
         nxt = sub["goal"][t + 1] if t + 1 < T else env.hdqn_goal[idx].cpu().numpy()
-        cc_g.check(nxt, exp_next, brk & gf & ~d, q2, f"fresh goal, step {t}")
+        cc_g.check(nxt, exp_next, brk & gf & ~d, q2, f"fresh goal, step {t}", q_exact=q2x)
         obs = sub["obs"][t]
         obs64 = o_obs
     for name, src in (("pos1", env.p1), ("vel1", env.v1), ("pos2", env.p2), ("vel2", env.v2),
@@ -461,7 +469,8 @@ def test_fused_hdqn_rollout_full_size(coracle, nets):
         np.testing.assert_array_equal(src[idx].cpu().numpy(), envs[name], err_msg=name)
     np.testing.assert_array_equal(env.returns[idx].cpu().numpy(), stats[0])
     np.testing.assert_array_equal(env.counts[idx].cpu().numpy().astype(np.uint32), stats[1])
-    check_q_eval(env.q_eval[idx].cpu().numpy(), qe, qe_abs, f"full-size h-DQN ({nets})", pinned=qe_pin)
+    check_q_eval(env.q_eval[idx].cpu().numpy(), qe, qe_abs, f"full-size h-DQN ({nets})", pinned=qe_pin,
+                 model=qe_pin)
     # main.py's pending value where the ego has arrived first: what the next launch reads back
     # (the no-wait statistics load it only for those envs, pend_load)
     w1 = envs["winner"] == 1
