@@ -2087,8 +2087,11 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
   // begins the greedy bytes hold the need bits (qnet_need_bits, qnet_put_need)
   __shared__ uint8_t qlist[OPP >= 2 ? 4 : 1][OPP >= 2 ? 256 : 1];
   // OPP 2: each listed item's layer-1 B fragment halves (the view it needs), staged by the env's own
-  // lane, so one forward can hold both views' items (one net) and reads its inputs lane-linearly
-  __shared__ __attribute__((aligned(16))) u32x4 qstage[OPP == 2 ? 4 : 1][OPP == 2 ? 256 : 1][2];
+  // lane, so one forward can hold both views' items (one net) and reads its inputs lane-linearly:
+  // half-major ([wave][h][item]), so the 32 lanes reading one half read 512 contiguous bytes (round 6;
+  // item-major, the 32-B item stride left half of the banks idle: SQ_LDS_BANK_CONFLICT / IDX_ACTIVE
+  // 0.097, valu_busy.json)
+  __shared__ __attribute__((aligned(16))) u32x4 qstage[OPP == 2 ? 4 : 1][2][OPP == 2 ? 256 : 1];
   // OPP 3: phase p once opponent wave h has read every tile row an ego wave will overwrite with
   // Q-values (the may-finish rows, which it lists first)
   __shared__ int qrows_read[2];
@@ -2241,12 +2244,12 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
               }
               auto pk = [](float a, float b) { return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2)); };
               if (nb & 2) {  // the opponent's view state[5:] + state[:5] (main.py:199)
-                qstage[wave][po][0] = u32x4{pk(f[5], f[6]), pk(f[7], f[8]), pk(f[9], f[0]), pk(f[1], f[2])};
-                qstage[wave][po][1] = u32x4{pk(f[3], f[4]), 0u, 0x3F800000u, 0x3F803F80u};
+                qstage[wave][0][po] = u32x4{pk(f[5], f[6]), pk(f[7], f[8]), pk(f[9], f[0]), pk(f[1], f[2])};
+                qstage[wave][1][po] = u32x4{pk(f[3], f[4]), 0u, 0x3F800000u, 0x3F803F80u};
               }
               if (nb & 1) {
-                qstage[wave][pe][0] = u32x4{pk(f[0], f[1]), pk(f[2], f[3]), pk(f[4], f[5]), pk(f[6], f[7])};
-                qstage[wave][pe][1] = u32x4{pk(f[8], f[9]), 0u, 0x3F800000u, 0x3F803F80u};
+                qstage[wave][0][pe] = u32x4{pk(f[0], f[1]), pk(f[2], f[3]), pk(f[4], f[5]), pk(f[6], f[7])};
+                qstage[wave][1][pe] = u32x4{pk(f[8], f[9]), 0u, 0x3F800000u, 0x3F803F80u};
               }
             };
             stage(row_of(lane), nb0, lane_rank(mo0), Lo + lane_rank(me0));
@@ -2262,7 +2265,7 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
             // cost +35 % per launch, r05f q1 / q2)
             const int cnt = nq - c0 < 64 ? nq - c0 : 64;
             auto input = [&](int it) __attribute__((always_inline)) {
-              return __builtin_bit_cast(bf16x8, qstage[wave][c0 + (it < cnt ? it : 0)][h]);
+              return __builtin_bit_cast(bf16x8, qstage[wave][h][c0 + (it < cnt ? it : 0)]);
             };
             const int e_out = list[c0 + (lane < cnt ? lane : 0)];  // read ahead: its wait hides under the forward
             float q[8];
@@ -2414,7 +2417,7 @@ __global__ __launch_bounds__(kQWsThreads, kQWsWavesPerSimd) void qnet_rollout_ws
               }
             }
           } else {
-            const bf16x8 x = __builtin_bit_cast(bf16x8, qstage[ew][it][h]);
+            const bf16x8 x = __builtin_bit_cast(bf16x8, qstage[ew][h][it]);
             qnet_mlp<2 * kQLdsAhead, 1>(qnet_lds(lds_net), x, x, q);
             if (lane < cnt) {
               const int e = list[io];
