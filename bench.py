@@ -467,7 +467,11 @@ def hdqn_leg(env, args, world, dist, torch):
 
     from merging_gym.policy import NUM_GOALS, QNet
 
-    rng = np.random.default_rng(0)
+    # seed 15: the L0 leg's episodes mix collisions and ego wins (seed 0, rounds 2-5, gave a lower net
+    # that picks speed 10 for 97 % of states: every ego trailed the L0 car, collision and win rates
+    # 0.0). Chosen on the CPU from 40 seeds with the oracle and the bf16-emulated nets: collision
+    # rate 0.195, ego first 0.90 over 3,000 episodes (h-DQN bench nets).
+    rng = np.random.default_rng(15)
 
     def net(i, o):
         sd = {}
@@ -586,7 +590,8 @@ def hdqn_leg(env, args, world, dist, torch):
             "useful_tflops": l0_flop * per_s / 1e12, "peak_tflops": MFMA_BF16_PEAK_TFLOPS,
             "frac_useful": l0_flop * per_s / 1e12 / MFMA_BF16_PEAK_TFLOPS,
             "episodes_per_env_step": ep_rate,
-            "nets": "seeded, torch.nn.Linear default init U(-1/sqrt(in), 1/sqrt(in)) (signed)",
+            "nets": ("seeded (numpy default_rng(15)), torch.nn.Linear default init U(-1/sqrt(in), 1/sqrt(in)) "
+                     "(signed); the seed gives episodes with collisions and ego wins"),
             "goal_break_rate_per_step": break_rate, "next_goal_share": greedy_goal_spread,
             "episodes": episodes,
             "q_eval_logged_as": "meta_eval_net(state)[goal] on each episode's terminal state and its goal (hdqn.py:330)"}
@@ -1123,7 +1128,9 @@ def compact_line(line):
     h = line.get("hdqn_policy")
     if h is not None:
         legs["hdqn_L0"] = {"kernel": h["kernel"], "value": h["value"], "kernel_ms_mean": h["kernel_ms_mean"],
-                           "frac_useful": h["frac_useful"], "goal_break_rate": h["goal_break_rate_per_step"]}
+                           "frac_useful": h["frac_useful"], "goal_break_rate": h["goal_break_rate_per_step"],
+                           "episodes": h["episodes"]["completed"], "collision_rate": h["episodes"]["collision_rate"],
+                           "win_rate_hdqn": h["episodes"]["win_rate_hdqn"]}
         for key, name in (("selfplay", "hdqn_self"), ("other_checkpoint", "hdqn_other")):
             z = h[key]
             legs[name] = {"kernel": z["kernel"], "env_steps_per_s": z["env_steps_per_s"],
