@@ -1838,7 +1838,36 @@ __global__ __launch_bounds__(kBlock) void qnet_forward_kernel(const uint8_t* net
 // may_finish_next's constants (below)
 struct FinishBound {
   float smin, smax, g;  // min / max of action_dict, the MPC's speed gain per step
+  float lat, lon;       // collision reach before the step: lateral |y1 - y2| and longitudinal |x1 - x2|
+                        // (finish_bound, from veh_w / veh_h / R / dT and the speeds: 5.75 / 9 by default)
 };
+
+// may_finish_next's constants for these params (host). Collision after the step needs
+// trunc(y1) - trunc(y2) <= veh_w, so y1 - y2 < veh_w + 1, and |x1 - x2| < veh_h + 1 (the pygame
+// Rect truncation of vehicle_box). A step moves a car by dl <= dT vmax along its arc, vmax =
+// max(start_vel, action speeds) + 0.5 (a speed only moves toward an action's target), and so its
+// lateral y by at most dl |sin theta|; where y1 - y2 < lat the ego's 1 - cos theta < lat / R, so
+// |sin theta| < sqrt(2 lat / R) + dl / R over the step. lat = veh_w + 1 + max(0.75, 2 dl sin + 0.25):
+// the default params' 0.75 (5.75) stands unless the geometry needs more. The longitudinal reach of
+// the speeds is added at run time (rel in may_finish_next).
+inline FinishBound finish_bound(const mg_params& P) {
+  double smin = P.action_speed[0], smax = smin;
+  for (int a = 1; a < MG_NUM_ACTIONS; ++a) {
+    smin = std::min(smin, P.action_speed[a]);
+    smax = std::max(smax, P.action_speed[a]);
+  }
+  const double vmax = std::max(smax, P.start_vel) + 0.5;
+  const double dl = P.dT * vmax;
+  double lat = P.veh_w + 1.75;
+  for (int it = 0; it < 4; ++it) {  // lat appears in its own bound: a few fixed-point passes
+    const double sn = std::sqrt(2.0 * lat / P.R) + dl / P.R;
+    lat = P.veh_w + 1.0 + std::max(0.75, 2.0 * dl * sn + 0.25);
+  }
+  // rounded outward by a margin: the bound only has to contain every speed a step reaches
+  return FinishBound{static_cast<float>(smin) - 0.5f, static_cast<float>(smax) + 0.5f,
+                     static_cast<float>(P.dT * P.qp_z0 / P.qp_nz) * 1.01f, static_cast<float>(lat),
+                     static_cast<float>(P.veh_h + 1)};
+}
 struct QRollout {
   mg_params P;
   Reset0 R0;
@@ -1868,9 +1897,10 @@ struct QRollout {
 //   arrival   a car can pass END_POINT within the step and that ends the episode (the other car
 //             already won, or both arrive): p' = p + dT v' with v' between v and the action's target
 //             speed, so END_POINT - p < dT max(v, smax) + 0.5;
-//   collision the boxes can overlap afterwards. Laterally trunc(y1) - trunc(y2) <= 4 needs
-//             y1 - y2 < 5 (y1 >= y2 on the two arcs), and a step moves each y by at most
-//             |sin theta| dT v' < 0.3 m there. Longitudinally |t1 - t2| <= 8 needs |x1 - x2| < 9, and a
+//   collision the boxes can overlap afterwards. Laterally trunc(y1) - trunc(y2) <= veh_w needs
+//             y1 - y2 < veh_w + 1 (y1 >= y2 on the two arcs), and a step moves each y by at most
+//             |sin theta| dT v' (< 0.17 m there by default); B.lat (finish_bound) covers both.
+//             Longitudinally |t1 - t2| <= veh_h needs |x1 - x2| < veh_h + 1 (B.lon), and a
 //             step changes x1 - x2 by at most dT |v1' - v2'| (+ 0.2 % for the arc): the MPC moves each
 //             speed by g (s - v), g = dT z0 / z'n = 1/15 (mpc_acc), so |v1' - v2'| <= |v1 - v2| +
 //             g (max(smax, v1, v2) - min(smin, v1, v2)).
@@ -1883,7 +1913,7 @@ MG_HD bool may_finish_next(const mg_params& P, const Env& e, const obs_t (&o)[kO
   const bool arrive = e.winner == 1 ? opp : (e.winner == 2 ? ego : (ego && opp));
   const float spread = fmaxf(B.smax, fmaxf(o[4], o[9])) - fminf(B.smin, fminf(o[4], o[9]));
   const float rel = dt * (fabsf(o[2]) + B.g * spread) + 0.5f;  // o[2] = v2 - v1
-  const bool coll = -o[1] < 5.75f && fabsf(o[0]) < 9.0f + rel;  // o[1] = y2 - y1, o[0] = x2 - x1
+  const bool coll = -o[1] < B.lat && fabsf(o[0]) < B.lon + rel;  // o[1] = y2 - y1, o[0] = x2 - x1
   return arrive || coll;
 }
 
@@ -3868,14 +3898,7 @@ int mg_rollout_qnet(const mg_params* params, const mg_state* state, const mg_tra
   R.num_steps = num_steps;
   R.out_dim = out_dim;
   R.flags = flags;
-  double smin = params->action_speed[0], smax = smin;
-  for (int a = 1; a < MG_NUM_ACTIONS; ++a) {
-    smin = std::min(smin, params->action_speed[a]);
-    smax = std::max(smax, params->action_speed[a]);
-  }
-  // rounded outward by a margin: the bound only has to contain every speed a step reaches
-  R.fin = FinishBound{static_cast<float>(smin) - 0.5f, static_cast<float>(smax) + 0.5f,
-                      static_cast<float>(params->dT * params->qp_z0 / params->qp_nz) * 1.01f};
+  R.fin = finish_bound(*params);
   const int64_t block_envs = opponent_mode == 3 ? qws_envs<3>() : qws_envs<0>();
   const unsigned blocks = static_cast<unsigned>((n + block_envs - 1) / block_envs);
   hipStream_t st = static_cast<hipStream_t>(stream);

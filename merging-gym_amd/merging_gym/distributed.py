@@ -89,11 +89,11 @@ def _records_of(returns, counts):
     return base if base.untyped_storage().nbytes() >= (returns.storage_offset() + 8 * n) * 8 else None
 
 
-# (device, stream) -> mg_stats_reduce scratch (block partials). One buffer per stream: reductions
-# queued on two streams of a device must not share partials (nothing orders them), and a buffer is
-# allocated on the stream that uses it, so when it is regrown the caching allocator hands the old one
-# out again only in that stream's order.
-_SCRATCH = {}
+# mg_stats_reduce's scratch (block partials) is allocated per call on the stream that runs the
+# reduction: the caching allocator hands a freed block out again only in that stream's order, so
+# reductions on two streams never share partials, and nothing is cached per stream (round 6: the
+# per-(device, stream) dict of rounds 4-5 grew by one buffer for every new stream and could hand a
+# recycled stream handle a buffer of a dead one).
 
 
 def device_totals(records, events=None):
@@ -112,11 +112,8 @@ def device_totals(records, events=None):
     out = torch.empty(NUM_SUMS + NUM_COUNTS, dtype=torch.int64, device=dev)
     words = max(1, (_native.lib.mg_stats_reduce_scratch_bytes(n) + 7) // 8)
     stream = torch.cuda.current_stream(dev)
-    key = (dev, stream.cuda_stream)
-    scratch = _SCRATCH.get(key)
-    if scratch is None or scratch.numel() < words:  # reused in this stream's order
-        with torch.cuda.stream(stream):
-            scratch = _SCRATCH[key] = torch.empty(words, dtype=torch.int64, device=dev)
+    with torch.cuda.stream(stream):
+        scratch = torch.empty(words, dtype=torch.int64, device=dev)
     args = (ctypes.c_void_p(records.data_ptr()), n, ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(scratch.data_ptr()),
             scratch.numel() * 8, ctypes.c_void_p(stream.cuda_stream))
     if events:

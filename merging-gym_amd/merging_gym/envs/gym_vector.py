@@ -11,6 +11,10 @@ protocol here, at the cost of one device-to-host copy per step:
     obs, rew, dones, infos = venv.step(actions)  # rew [n, 2] float64 (both players, the
                                                  # reference's step(a1, a2) returns [r1, r2])
 
+Rewards are the kernel's fp32 [r1, r2] widened to float64: the reference's Python floats are fp64,
+so they agree to fp32 rounding (the path's stated tolerance), not beyond. Stock gym 0.20 wrappers
+expect a reward vector [n]: `gym_vector(ego_reward_only=True)` returns the ego's reward only.
+
 Observations take the observation space's dtype: gym 0.20's vector envs build their output
 arrays from the single space (create_empty_array), and the reference's space is float16
 (merging_env.py:75-78). actions: [n] ego actions (the opponent then None, merging_env.py:152),
@@ -25,8 +29,9 @@ import numpy as np
 class GymVectorEnv:
     """gym 0.20 VectorEnv protocol (duck-typed: gym is not a dependency) over a MergeVecEnv."""
 
-    def __init__(self, env, obs_dtype=None):
+    def __init__(self, env, obs_dtype=None, ego_reward_only=False):
         self.env = env
+        self.ego_reward_only = ego_reward_only
         self.num_envs = env.num_envs
         self.single_observation_space = env.single_observation_space
         self.single_action_space = env.single_action_space
@@ -67,7 +72,8 @@ class GymVectorEnv:
             rows = term[self._torch_index(idx)].cpu().numpy().astype(self.obs_dtype)
             for k, i in enumerate(idx):
                 infos[i]["terminal_observation"] = rows[k]
-        return self._host_obs(obs), rew.cpu().numpy().astype(np.float64), dones, tuple(infos)
+        r = rew.cpu().numpy().astype(np.float64)
+        return self._host_obs(obs), (r[:, 0].copy() if self.ego_reward_only else r), dones, tuple(infos)
 
     def step(self, actions):
         self.step_async(actions)
@@ -98,7 +104,11 @@ class GymVectorEnv:
         return torch.as_tensor(idx, device=getattr(self.env, "device", "cpu"))
 
     def _split(self, actions):
-        if isinstance(actions, tuple) and len(actions) == 2:
+        # a pair (a1, a2) only when each part is a whole batch of actions (a2 may be None): with
+        # num_envs == 2 a tuple of two scalars is the two envs' ego actions, not a pair
+        if isinstance(actions, tuple) and len(actions) == 2 and all(
+                x is None or np.shape(x.cpu() if hasattr(x, "cpu") else x) == (self.num_envs,) for x in actions) \
+                and actions[0] is not None:
             return actions
         a = np.asarray(actions.cpu() if hasattr(actions, "cpu") else actions)
         if a.ndim == 2 and a.shape == (self.num_envs, 2):

@@ -214,9 +214,11 @@ class MergeEnv(_EnvBase):
     (bench.py `dropin_single_env`): the host path ~7 us, the GPU path ~28 us (a launch plus a stream
     synchronisation per step), the reference-style Python step ~11 us. backend "gpu" (or any
     `device` given): the same step as a batch of one env in the step kernel (mg_step). Both give the
-    same doubles bit for bit on every state a live episode reaches; past about 2,875 m (|theta| >=
-    1/16, cars driving on long after the end point) sin / cos come from glibc on the host and from
-    the device library on the GPU, and the observation may differ there by an ulp (positions,
+    same doubles bit for bit wherever |theta| < 1/16, i.e. positions below about 2,875 m. A live
+    episode does go further: a car that has arrived keeps driving (up to 8 m per step) while the other
+    car runs the episode to the 2501-step timeout, to about 20 km. There sin / cos come from glibc on
+    the host and from the device library on the GPU, and an observation may differ by an ulp
+    between the two backends, and from the reference's numpy values (a known divergence; positions,
     speeds, rewards and flags stay equal; tests/test_host_step.py). Batches belong in MergeVecEnv,
     which is GPU-only.
     """

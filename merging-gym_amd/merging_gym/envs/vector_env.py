@@ -455,13 +455,13 @@ class MergeVecEnv:
             out.update(ext_reward=hb["ext_reward"], no_break=hb["no_break"])
         return out
 
-    def gym_vector(self, obs_dtype=None):
+    def gym_vector(self, obs_dtype=None, ego_reward_only=False):
         """gym 0.20's VectorEnv protocol over this env (envs/gym_vector.py): step_async / step_wait,
-        numpy outputs and per-env infos with "terminal_observation". The device-tensor API above stays
-        the fast path."""
+        numpy outputs and per-env infos with "terminal_observation" (ego_reward_only: rewards [n] of the
+        ego, for stock wrappers). The device-tensor API above stays the fast path."""
         from .gym_vector import GymVectorEnv
 
-        return GymVectorEnv(self, obs_dtype)
+        return GymVectorEnv(self, obs_dtype, ego_reward_only)
 
     def observe(self):
         """Observation of the current state without stepping (merging_env.py:118-132)."""

@@ -386,3 +386,40 @@ def test_rollout_qnet_full_size(torch, coracle, nets, opponent):
     cc1.finish()
     if opponent in ("self", "other"):
         cc2.finish()
+
+
+@pytest.mark.parametrize("opponent", ["none", "self"])
+def test_q_eval_with_non_default_vehicle_boxes(torch, nets, opponent):
+    """may_finish_next's collision reach comes from the params (finish_bound: veh_w + 1 and veh_h + 1
+    plus the arc's lateral drift), not the default boxes' 5.75 / 9 m: with 14 x 30 m boxes the cars
+    collide far earlier, and every episode's logged q_eval must still be eval_net(state)[action] of
+    its last step (main.py:221) -- the oracle MFMA rule's Q row of the kernel's own input
+    observation -- on explore steps too. (The env dynamics at these params have no oracle; the
+    transitions are the kernel's.)"""
+    from merging_gym import MergeVecEnv
+    from merging_gym.policy import QNet
+
+    n, T, seed = 4096, 48, 3
+    env = MergeVecEnv(n, device="cuda:0")
+    env.params.veh_w, env.params.veh_h = 14, 30
+    for k in range(150):
+        env.step_random(seed + 1, step_idx=k)
+    env.clear_statistics()
+    qnet = QNet.from_state_dict(nets["l1"], device="cuda:0")
+    form = "16x16" if opponent == "self" else "32x32"
+    obs_in = env.observe().cpu().numpy().copy()
+    qe0 = env.q_eval.cpu().numpy().copy()
+    traj = env.rollout_qnet(T, qnet, seed, opponent=opponent, first_step=500)
+    a1, done, coll = (traj[k].cpu().numpy() for k in ("a1", "done", "collision"))
+    obs = traj["obs"].cpu().numpy()
+    exp = qe0.copy()
+    for t in range(T):
+        d = done[t]
+        if d.any():
+            q = mo.qnet_reference_mfma(nets["l1"], obs_in, form=form).astype(np.float64)
+            exp += np.where(d, q[np.arange(n), a1[t].astype(np.int64)], 0.0)
+        obs_in = obs[t]
+    assert coll.sum() > 100 and done.sum() > 500, (int(coll.sum()), int(done.sum()))
+    got = env.q_eval.cpu().numpy()
+    bad = np.flatnonzero(got != exp)
+    assert bad.size == 0, (bad.size, bad[:8].tolist(), got[bad[:4]].tolist(), exp[bad[:4]].tolist())

@@ -104,3 +104,24 @@ def test_gym020_protocol_equals_the_device_api():
             assert np.array_equal(infos[i]["terminal_observation"], term[i])
         ends += int(dones.sum())
     assert ends > 100
+
+
+def test_pair_split_and_ego_reward_only():
+    """A 2-tuple is read as (a1, a2) only when each part is a whole batch (a2 may be None); with two
+    envs a tuple of two scalars is the two envs' ego actions. ego_reward_only returns rewards [n] (the
+    ego's), the vector stock gym 0.20 wrappers expect."""
+    env = OracleVecEnv(2)
+    v = GymVectorEnv(env)
+    v.reset()
+    a1, a2 = v._split((np.array([1, 2]), np.array([3, 4])))
+    assert a1.tolist() == [1, 2] and a2.tolist() == [3, 4]
+    a1, a2 = v._split((np.array([1, 2]), None))
+    assert a1.tolist() == [1, 2] and a2 is None
+    a1, a2 = v._split((3, 4))  # two envs' ego actions, not a pair
+    assert np.asarray(a1).tolist() == [3, 4] and a2 is None
+    _, rew, _, _ = v.step(np.array([1, 2]))
+    assert rew.shape == (2, 2) and rew.dtype == np.float64
+    ve = GymVectorEnv(OracleVecEnv(2), ego_reward_only=True)
+    ve.reset()
+    _, rew1, _, _ = ve.step(np.array([1, 2]))
+    assert rew1.shape == (2,) and np.array_equal(rew1, rew[:, 0])

@@ -229,9 +229,10 @@ def test_host_step_equals_kernel():
 
 @pytest.mark.gpu
 def test_host_step_equals_kernel_past_the_polynomial_range():
-    """Far past the end point (|theta| >= 1/16: positions beyond ~2,875 m, reached by cars that keep
-    driving after a finished episode without autoreset) sin / cos leave the shared polynomial: glibc
-    on the host, the device library on the GPU. The state, rewards and flags stay bit-equal (they do
+    """Far past the end point (|theta| >= 1/16: positions beyond ~2,875 m) sin / cos leave the shared
+    polynomial: glibc on the host, the device library on the GPU. Live episodes reach this range (an
+    arrived car keeps driving while the other runs the episode to the 2501-step timeout, to ~20 km),
+    as do cars stepped on after a finished episode without autoreset. The state, rewards and flags stay bit-equal (they do
     not depend on sin / cos there: the cars are far apart), and the observations agree to 1 fp32 ulp
     (the doubles differ by at most an ulp before the fp32 rounding)."""
     import torch

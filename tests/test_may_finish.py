@@ -19,6 +19,31 @@ DT, TIMEOUT = 0.2, 2501  # mg_params dT, timeout_steps
 SMIN, SMAX, G = -0.5, 40.5, (0.2 * 30.000000000000533 / 90.0000000000015) * 1.01  # FinishBound as launched
 
 
+def finish_bound(veh_w=4, veh_h=8, R=30000.0, dT=0.2, speeds=(0, 10, 20, 30, 40), start_vel=20.0):
+    """merging_hip.hip finish_bound's collision reach (lat, lon), restated."""
+    dl = dT * (max(max(speeds), start_vel) + 0.5)
+    lat = veh_w + 1.75
+    for _ in range(4):
+        sn = np.sqrt(2.0 * lat / R) + dl / R
+        lat = veh_w + 1.0 + max(0.75, 2.0 * dl * sn + 0.25)
+    return np.float32(lat), np.float32(veh_h + 1)
+
+
+LAT, LON = finish_bound()
+
+
+def test_finish_bound_defaults_and_scaling():
+    """The default params keep round 5's proven 5.75 / 9 m; the reach grows with the boxes, with a
+    tighter arc (the lateral drift per step) and with faster action speeds."""
+    assert finish_bound() == (np.float32(5.75), np.float32(9.0))
+    lat, lon = finish_bound(veh_w=14, veh_h=30)
+    assert lat >= 15.75 and lon == 31.0
+    lat_tight, _ = finish_bound(R=300.0)
+    assert lat_tight > 5.75
+    lat_fast, _ = finish_bound(R=3000.0, speeds=(0, 50, 100, 150, 200))
+    assert lat_fast > lat_tight - 1.0 and lat_fast > 5.75
+
+
 def may_finish(obs64, winner, steps):
     o = obs64.astype(np.float32)
     f = np.float32
@@ -28,7 +53,7 @@ def may_finish(obs64, winner, steps):
     arrive = np.where(winner == 1, opp, np.where(winner == 2, ego, ego & opp))
     spread = np.maximum(f(SMAX), np.maximum(o[:, 4], o[:, 9])) - np.minimum(f(SMIN), np.minimum(o[:, 4], o[:, 9]))
     rel = dt * (np.abs(o[:, 2]) + f(G) * spread) + f(0.5)
-    coll = (-o[:, 1] < f(5.75)) & (np.abs(o[:, 0]) < f(9.0) + rel)
+    coll = (-o[:, 1] < LAT) & (np.abs(o[:, 0]) < LON + rel)
     return (steps + 1 >= TIMEOUT) | arrive | coll
 
 
