@@ -120,7 +120,8 @@ __device__ __forceinline__ bf16x8 l1x16_input(const float* tile, int row0, int t
   return lane < 32 ? x : bf16x8{};
 }
 
-template <int WAVES, int MODE>  // MODE 0: shipped qnet_forward_swp; 1: the layer-1 16x16x32 variant
+template <int WAVES, int MODE>  // MODE 0: shipped qnet_forward_swp; 1: the layer-1 16x16x32 variant;
+                                // 2 / 3 / 4: the shipped forward with 3 / 4 / 6 fragments in flight
 __global__ __launch_bounds__(64 * WAVES) void probe(const uint8_t* net, int iters, unsigned long long* cyc, float* out) {
   __shared__ __attribute__((aligned(16))) uint8_t lds_net[kQNetBytes];
   __shared__ __attribute__((aligned(16))) float tile[64 * WAVES * kObs];
@@ -135,6 +136,11 @@ __global__ __launch_bounds__(64 * WAVES) void probe(const uint8_t* net, int iter
     const bool swap = (it & 1) != 0;
     if constexpr (MODE == 0) {
       qnet_forward_swp(lds_net, tile, wave * 64, swap, q);
+    } else if constexpr (MODE >= 2) {
+      constexpr int D = MODE == 2 ? 3 : MODE == 3 ? 4 : 6;
+      const int r = lane & 31, h = lane >> 5;
+      qnet_mlp<D>(qnet_lds(lds_net), qnet_input(tile + (wave * 64 + r) * kObs, swap, h),
+                  qnet_input(tile + (wave * 64 + 32 + r) * kObs, swap, h), q);
     } else {
       bf16x8 xt[4];
 #pragma unroll
@@ -171,8 +177,10 @@ void run(const uint8_t* dnet, int blocks, int iters) {
     mean /= c.size();
     std::printf("{\"forward\": \"%s\", \"q_waves_per_simd\": %d, \"blocks\": %d, \"iters\": %d, "
                 "\"cycles_per_forward\": %.0f, \"mfma_pipe_cycles\": %d, \"wall_ms\": %.3f}\n",
-                MODE == 0 ? "shipped (layer 1 32x32x16 + permlane16_swap)" : "layer 1 16x16x32, no swaps", WAVES / 4,
-                blocks, iters, mean / iters, MODE == 0 ? 3840 : 4288, ms);
+                MODE == 0 ? "shipped (layer 1 32x32x16 + permlane16_swap), 2 fragments ahead"
+                : MODE == 1 ? "layer 1 16x16x32, no swaps"
+                : MODE == 2 ? "shipped, 3 ahead" : MODE == 3 ? "shipped, 4 ahead" : "shipped, 6 ahead",
+                WAVES / 4, blocks, iters, mean / iters, MODE == 1 ? 4288 : 3840, ms);
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
   }
@@ -191,6 +199,12 @@ int main() {
   run<4, 1>(dnet, 256, 2000);
   run<8, 0>(dnet, 256, 2000);
   run<8, 1>(dnet, 256, 2000);
+  run<4, 2>(dnet, 256, 2000);
+  run<4, 3>(dnet, 256, 2000);
+  run<4, 4>(dnet, 256, 2000);
+  run<8, 2>(dnet, 256, 2000);
+  run<8, 3>(dnet, 256, 2000);
+  run<4, 0>(dnet, 256, 2000);
   (void)hipFree(dnet);
   return 0;
 }
