@@ -769,6 +769,7 @@ def self_launch(args, argv, popen=None, script=None) -> int:
 
     old = signal.signal(signal.SIGTERM, lambda *a: (stop(), sys.exit(143)))
     first_bad = None
+    stopped_at = None
     try:
         rcs = [None] * len(procs)
         while any(rc is None for rc in rcs):
@@ -779,6 +780,12 @@ def self_launch(args, argv, popen=None, script=None) -> int:
                         first_bad = rcs[i]
                         print(f"bench.py: rank {i} exited with {rcs[i]}; stopping the others", file=sys.stderr)
                         stop()  # a failed rank would leave the others at a barrier
+                        stopped_at = time.time()
+            if stopped_at is not None and time.time() - stopped_at > 30:
+                for p in procs:  # a rank that ignored SIGTERM for 30 s (stuck in a collective)
+                    if p.poll() is None:
+                        p.kill()
+                stopped_at = None
             time.sleep(0.05)
     finally:
         signal.signal(signal.SIGTERM, old)
