@@ -7,7 +7,11 @@
 // its Q values are not a forward's.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -I include \
 //         -o tools/micro/qfwd_l1x16 tools/micro/qfwd_l1x16.hip && tools/micro/qfwd_l1x16
+#ifndef MG_SRC
 #include "../../merging-gym_amd/csrc/merging_hip.hip"
+#else
+#include MG_SRC  // an edited copy of the source (tools/micro/qfwd_ablate.sh: the forward's parts removed)
+#endif
 
 #include <cstdio>
 #include <vector>
@@ -120,8 +124,19 @@ __device__ __forceinline__ bf16x8 l1x16_input(const float* tile, int row0, int t
   return lane < 32 ? x : bf16x8{};
 }
 
+// weights from registers: the fragment index picks one of four (timing only: no LDS reads)
+struct QSrcReg {
+  bf16x8 r[4];
+  __device__ __forceinline__ bf16x8 operator()(int s) const {
+    bf16x8 v = r[s & 3];
+    asm volatile("" : "+v"(v));  // opaque: no two fragments are the same value (no MFMA is merged)
+    return v;
+  }
+};
+
 template <int WAVES, int MODE>  // MODE 0: shipped qnet_forward_swp; 1: the layer-1 16x16x32 variant;
-                                // 2 / 3 / 4: the shipped forward with 3 / 4 / 6 fragments in flight
+                                // 2 / 3 / 4: the shipped forward with 3 / 4 / 6 fragments in flight;
+                                // 5: the shipped forward with its weights in registers
 __global__ __launch_bounds__(64 * WAVES) void probe(const uint8_t* net, int iters, unsigned long long* cyc, float* out) {
   __shared__ __attribute__((aligned(16))) uint8_t lds_net[kQNetBytes];
   __shared__ __attribute__((aligned(16))) float tile[64 * WAVES * kObs];
@@ -136,6 +151,13 @@ __global__ __launch_bounds__(64 * WAVES) void probe(const uint8_t* net, int iter
     const bool swap = (it & 1) != 0;
     if constexpr (MODE == 0) {
       qnet_forward_swp(lds_net, tile, wave * 64, swap, q);
+    } else if constexpr (MODE == 5) {
+      const int r = lane & 31, h = lane >> 5;
+      QSrcReg src;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) src.r[j] = *reinterpret_cast<const bf16x8*>(lds_net + 1024 * j + 16 * lane);
+      qnet_mlp<2>(src, qnet_input(tile + (wave * 64 + r) * kObs, swap, h),
+                  qnet_input(tile + (wave * 64 + 32 + r) * kObs, swap, h), q);
     } else if constexpr (MODE >= 2) {
       constexpr int D = MODE == 2 ? 3 : MODE == 3 ? 4 : 6;
       const int r = lane & 31, h = lane >> 5;
@@ -179,7 +201,8 @@ void run(const uint8_t* dnet, int blocks, int iters) {
                 "\"cycles_per_forward\": %.0f, \"mfma_pipe_cycles\": %d, \"wall_ms\": %.3f}\n",
                 MODE == 0 ? "shipped (layer 1 32x32x16 + permlane16_swap), 2 fragments ahead"
                 : MODE == 1 ? "layer 1 16x16x32, no swaps"
-                : MODE == 2 ? "shipped, 3 ahead" : MODE == 3 ? "shipped, 4 ahead" : "shipped, 6 ahead",
+                : MODE == 2 ? "shipped, 3 ahead" : MODE == 3 ? "shipped, 4 ahead"
+                : MODE == 4 ? "shipped, 6 ahead" : "shipped, weights in registers",
                 WAVES / 4, blocks, iters, mean / iters, MODE == 1 ? 4288 : 3840, ms);
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
@@ -189,7 +212,21 @@ void run(const uint8_t* dnet, int blocks, int iters) {
 }
 }  // namespace
 
-int main() {
+int main(int argc, char** argv) {
+  if (argc > 1) {  // ablation binaries: the shipped forward (and with register weights), one and two waves
+    std::vector<uint16_t> h(kQNetBytes / 2);
+    for (size_t i = 0; i < h.size(); ++i) h[i] = static_cast<uint16_t>(0x3C00 + (i * 7919) % 512);
+    uint8_t* dnet;
+    (void)hipMalloc(&dnet, kQNetBytes);
+    (void)hipMemcpy(dnet, h.data(), kQNetBytes, hipMemcpyHostToDevice);
+    std::printf("{\"variant\": \"%s\"}\n", argv[1]);
+    run<4, 0>(dnet, 256, 2000);
+    run<4, 5>(dnet, 256, 2000);
+    run<8, 0>(dnet, 256, 2000);
+    run<8, 5>(dnet, 256, 2000);
+    (void)hipFree(dnet);
+    return 0;
+  }
   std::vector<uint16_t> h(kQNetBytes / 2);
   for (size_t i = 0; i < h.size(); ++i) h[i] = static_cast<uint16_t>(0x3C00 + (i * 7919) % 512);  // small bf16
   uint8_t* dnet;
