@@ -41,3 +41,45 @@ def test_build_skips_a_current_library():
     before = os.path.getmtime(build.OUT)
     assert build.build() == build.OUT  # current by content: no hipcc run
     assert os.path.getmtime(build.OUT) == before
+
+
+_RACE = r"""
+import os, sys
+sys.path.insert(0, {pkgroot!r})
+from merging_gym import build
+build.OUT = os.path.join({d!r}, "libmerging_hip.so")
+build.PKG = {d!r}
+print(build.build())
+"""
+
+
+def test_concurrent_builds_compile_once(tmp_path):
+    """N ranks importing a stale library used to run hipcc into one shared `.tmp` path.
+    build() now holds an fcntl lock next to the library, re-checks it under the lock and writes a
+    per-process temporary file: four processes racing on a stale library run the compiler once and
+    leave an intact library (a stand-in compiler that takes a second and logs each run)."""
+    import subprocess
+    import sys
+
+    d = tmp_path / "pkg"
+    d.mkdir()
+    (d / "libmerging_hip.so").write_bytes(b"stale, no source sha")
+    log = tmp_path / "runs.log"
+    fake = tmp_path / "hipcc"
+    fake.write_text("#!/usr/bin/env python3\nimport sys, time\n"
+                    f"open({str(log)!r}, 'a').write('run\\n')\n"
+                    "time.sleep(1.0)\n"
+                    "args = sys.argv[1:]\nout = args[args.index('-o') + 1]\n"
+                    "sha = [a for a in args if a.startswith('-DMG_SRC_SHA=')][0].split('=', 1)[1].strip('\"')\n"
+                    "open(out, 'wb').write(b'ELF; src ' + sha.encode() + b'\\x00built')\n")
+    fake.chmod(0o755)
+    pkgroot = os.path.dirname(os.path.dirname(os.path.abspath(build.__file__)))
+    env = dict(os.environ, HIPCC=str(fake))
+    code = _RACE.format(pkgroot=pkgroot, d=str(d))
+    procs = [subprocess.Popen([sys.executable, "-c", code], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+             for _ in range(4)]
+    outs = [p.communicate(timeout=120) for p in procs]
+    assert all(p.returncode == 0 for p in procs), [o[1][-400:] for o in outs]
+    assert log.read_text().count("run") == 1
+    assert build.embedded_sha(str(d / "libmerging_hip.so")) == build.source_sha()
+    assert not [f for f in os.listdir(d) if f.endswith(".tmp")]
