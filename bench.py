@@ -795,16 +795,25 @@ def self_launch(args, argv, popen=None, script=None) -> int:
     return first_bad if first_bad > 0 else 128 - first_bad  # killed by signal s: 128 + s, as a shell reports
 
 
-def sync_spin():
-    """hipDeviceScheduleSpin for this process, before the HIP context exists: a synchronize then
-    spins on the host instead of yielding, so the host thread that issues the timed launches is
-    awake when the window opens (tools/window_probe.py)."""
+def sync_spin(local_rank=None):
+    """hipDeviceScheduleSpin for this rank's device, before the HIP context exists: a synchronize
+    then spins on the host instead of yielding, so the host thread that issues the timed launches
+    is awake when the window opens (tools/window_probe.py). The flags belong to the calling
+    thread's current device, so a rank first makes its own device current (device LOCAL_RANK mod
+    the visible count, as main() picks it below; rank r > 0 would otherwise set device 0's)."""
     import ctypes
 
     try:
-        return ctypes.CDLL("libamdhip64.so").hipSetDeviceFlags(ctypes.c_uint(1))  # hipDeviceScheduleSpin
+        hip = ctypes.CDLL("libamdhip64.so")
     except OSError:
         return None
+    if local_rank is not None:
+        count = ctypes.c_int(0)
+        if hip.hipGetDeviceCount(ctypes.byref(count)) != 0 or count.value < 1:
+            return None
+        if hip.hipSetDevice(ctypes.c_int(local_rank % count.value)) != 0:
+            return None
+    return hip.hipSetDeviceFlags(ctypes.c_uint(1))  # hipDeviceScheduleSpin
 
 
 def main():
@@ -817,11 +826,11 @@ def main():
     if env_world != args.gpus:
         raise SystemExit(f"bench.py --gpus {args.gpus} under a launcher with WORLD_SIZE={env_world}")
     launcher = ("self" if os.environ.get(SELF_LAUNCH_ENV) == "1" else "external") if env_world > 1 else None
-    spin_rc = sync_spin() if args.sync_spin else None
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    spin_rc = sync_spin(local if env_world > 1 else None) if args.sync_spin else None
     import torch
     import torch.distributed as dist
 
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     ndev = torch.cuda.device_count()
     if env_world > 1 and args.dist_backend == "nccl" and local >= ndev:
         raise SystemExit(f"rank with LOCAL_RANK {local}: only {ndev} GPU(s) visible (RCCL needs one per rank)")

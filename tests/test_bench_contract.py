@@ -317,3 +317,38 @@ def test_self_launch_all_ranks_green(tmp_path):
         assert bench.self_launch(_Args(3), [], script=str(script)) == 0
     finally:
         del os.environ[bench.DEVICE_COUNT_ENV]
+
+
+class _FakeHip:
+    """Stands in for libamdhip64 in sync_spin: records the calls, reports `count` devices."""
+
+    def __init__(self, count):
+        self.count, self.calls = count, []
+
+    def hipGetDeviceCount(self, ref):
+        ref._obj.value = self.count
+        self.calls.append(("count",))
+        return 0
+
+    def hipSetDevice(self, d):
+        self.calls.append(("set", d.value))
+        return 0 if d.value < self.count else 101
+
+    def hipSetDeviceFlags(self, f):
+        self.calls.append(("flags", f.value))
+        return 0
+
+
+@pytest.mark.parametrize("local,count,expect", [
+    (None, 8, [("flags", 1)]),                                   # one process: the default device
+    (3, 8, [("count",), ("set", 3), ("flags", 1)]),              # rank 3 of 8: its own device
+    (5, 1, [("count",), ("set", 0), ("flags", 1)]),              # gloo rehearsal on one GPU
+])
+def test_sync_spin_sets_the_flags_on_the_ranks_own_device(monkeypatch, local, count, expect):
+    import ctypes
+
+    bench = _bench()
+    fake = _FakeHip(count)
+    monkeypatch.setattr(ctypes, "CDLL", lambda name: fake)
+    assert bench.sync_spin(local) == 0
+    assert fake.calls == expect
