@@ -16,7 +16,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LINES = sorted(glob.glob(os.path.join(ROOT, "profiles", "r04", "bench_default_r04*.json")) +
                glob.glob(os.path.join(ROOT, "profiles", "r04", "bench_k20_r04*.json")))
 # round 5: the compact last line (bench.compact_line), incl. the multi-rank rehearsals
-LINES5 = sorted(glob.glob(os.path.join(ROOT, "profiles", "r05", "bench_*.json")))
+LINES5 = sorted(glob.glob(os.path.join(ROOT, "profiles", "r05", "bench_*.json")) +
+                glob.glob(os.path.join(ROOT, "profiles", "r06", "bench_*.json")))
 
 TOP = {"metric": str, "value": float, "unit": str, "n_gpus": int, "steps": int, "warmup": int,
        "ms_per_step": float, "higher_is_better": bool, "scaling": str, "dtype": str, "data": str,
@@ -55,7 +56,8 @@ def test_recorded_bench_line_keeps_the_contract(path):
 
 
 GRIDS = sorted(glob.glob(os.path.join(ROOT, "profiles", "r04", "kernel_stats_by_grid_r04*.json")) +
-               glob.glob(os.path.join(ROOT, "profiles", "r05", "kernel_stats_by_grid_r05*.json")))
+               glob.glob(os.path.join(ROOT, "profiles", "r05", "kernel_stats_by_grid_r05*.json")) +
+               glob.glob(os.path.join(ROOT, "profiles", "r06", "kernel_stats_by_grid_r06*.json")))
 
 
 @pytest.mark.skipif(not GRIDS, reason="no recorded rocprofv3 summaries")
@@ -65,7 +67,7 @@ def test_rocprof_step_kernel_average_agrees_with_the_bench_line(path):
     the step kernel's average at the 2^20 grid agrees with roofline.kernel_ms_mean within 5 %."""
     tag = os.path.basename(path)[len("kernel_stats_by_grid_"):-len(".json")]
     rnd = os.path.basename(os.path.dirname(path))
-    # round 4: the default bench line of the same pass; round 5: the profiled run's own line
+    # round 4: the default bench line of the same pass; rounds 5-6: the profiled run's own line
     bench = os.path.join(ROOT, "profiles", rnd, f"bench_default_{tag}.json" if rnd == "r04" else f"prof_bench_{tag}.json")
     if not os.path.exists(bench):
         pytest.skip(f"no bench line for {tag}")
@@ -141,6 +143,8 @@ def test_recorded_round5_line(path):
     assert len(text) < 6144, len(text)  # the driver keeps ~8 KB of the output's tail
     d = json.loads(text)
     check_line(d)
+    if "gpus_requested" in d["dist"]:  # round 6 on: the line names the --gpus it answers
+        check_requested(d, d["dist"]["gpus_requested"])
     if "legs" in d and d["n_gpus"] == 1:
         for leg in ("rollout", "replay", "qnet_none", "qnet_self", "qnet_other", "hdqn_L0", "hdqn_self", "hdqn_other"):
             assert leg in d["legs"], leg
