@@ -163,6 +163,19 @@ def load_pmc(envs: int, kernel: str = "step"):
         return None
 
 
+def load_pmc_replay(envs: int, T: int):
+    """HBM bytes of one replay store (the scan, group-scan and write kernels) from the committed
+    rocprofv3 PMC summary (tools/profile_pmc_replay.py -> profiles/pmc_replay.json), if it was
+    measured on this workload shape."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_replay.json")) as f:
+            d = json.load(f)
+        w = d["workload"]
+        return d["store_hbm_bytes"] if (w["envs"], w["T"]) == (envs, T) else None
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def load_valu():
     """Per-kernel VALU-issue figures from the committed rocprofv3 summary (tools/pmc_valu.sh +
     tools/valu_summary.py -> profiles/valu_busy.json): VALUBusy = VALU issue cycles of every SIMD
@@ -647,11 +660,15 @@ def replay_leg(env, args, torch):
         ring.sample_rows(128, seed=args.seed, draw=j)
     e.record()
     torch.cuda.synchronize()
+    traffic = load_pmc_replay(E, T)
     return {"kernels": "replay_scan_kernel + replay_group_scan_kernel + replay_write_kernel",
             "transitions_per_store": T * E, "stored_per_store": kept, "capacity": 1 << 24,
             "value": kept / (ms * 1e-3), "unit": "transitions/s", "ms_per_store": ms,
             "bytes_per_store": nbytes, "achieved": achieved,
             "peak": HBM_PEAK_GBPS, "unit_bw": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
+            # HBM bytes the store really moves (PMC): the write blocks re-read the observation row
+            # before their 2-step chunk (Replay memory), ~1.16x the algorithmic bytes
+            "traffic": traffic, "frac_traffic": None if traffic is None else traffic / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
             "sample_128_us": s.elapsed_time(e) / 100 * 1e3}
 
 
@@ -1135,7 +1152,8 @@ def compact_line(line):
                                                 "traffic")}
     if "replay" in line:
         z = line["replay"]
-        legs["replay"] = {k: z.get(k) for k in ("value", "unit", "ms_per_store", "frac", "sample_128_us")}
+        legs["replay"] = {k: z.get(k) for k in ("value", "unit", "ms_per_store", "frac", "traffic", "frac_traffic",
+                                               "sample_128_us")}
     for z in line.get("qnet_policy") or []:
         legs["qnet_" + z["opponent"].split(" ")[0]] = {
             k: z.get(k) for k in ("kernel", "value", "kernel_ms_mean", "frac_useful", "reference_forwards_per_env_step",
