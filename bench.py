@@ -666,7 +666,7 @@ def replay_leg(env, args, torch):
             "value": kept / (ms * 1e-3), "unit": "transitions/s", "ms_per_store": ms,
             "bytes_per_store": nbytes, "achieved": achieved,
             "peak": HBM_PEAK_GBPS, "unit_bw": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
-            # HBM bytes the store really moves (PMC): the write blocks re-read the observation row
+            # bytes L2 really moves for the store (PMC): the write blocks re-read the observation row
             # before their 2-step chunk (Replay memory), ~1.16x the algorithmic bytes
             "traffic": traffic, "frac_traffic": None if traffic is None else traffic / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
             "sample_128_us": s.elapsed_time(e) / 100 * 1e3}
