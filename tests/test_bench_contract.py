@@ -356,3 +356,25 @@ def test_sync_spin_sets_the_flags_on_the_ranks_own_device(monkeypatch, local, co
     monkeypatch.setattr(ctypes, "CDLL", lambda name: fake)
     assert bench.sync_spin(local) == 0
     assert fake.calls == expect
+
+
+def test_replay_traffic_record_is_consistent():
+    """profiles/pmc_replay.json (tools/profile_pmc_replay.py, FETCH_SIZE / WRITE_SIZE passes): the
+    store's bytes are the sum of its three kernels', the calibration kernels read back the bytes
+    they move (the gfx950 counter rule holds on that build), the row writes are exactly 88 B per
+    kept transition, and bench.py attaches the figure only to the same workload shape."""
+    path = os.path.join(ROOT, "profiles", "pmc_replay.json")
+    if not os.path.exists(path):
+        pytest.skip("no replay PMC record")
+    with open(path) as f:
+        d = json.load(f)
+    k = d["per_launch"]
+    total = sum(k[x]["hbm_bytes"] for x in ("scan", "group_scan", "write"))
+    assert math.isclose(d["store_hbm_bytes"], total, rel_tol=1e-9)
+    assert math.isclose(d["ratio_to_algorithmic"], total / d["store_algorithmic_bytes"], rel_tol=1e-9)
+    assert abs(d["check_reset_write_ratio"] - 1) < 0.02 and abs(d["check_observe_read_ratio"] - 1) < 0.02
+    w = d["workload"]
+    assert abs(k["write"]["write_bytes"] / (88.0 * w["kept_per_store"]) - 1) < 0.01
+    bench = _bench()
+    assert bench.load_pmc_replay(w["envs"], w["T"]) == d["store_hbm_bytes"]
+    assert bench.load_pmc_replay(w["envs"] * 2, w["T"]) is None
